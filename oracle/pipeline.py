@@ -1,0 +1,143 @@
+"""Oracle: ``VC.pipeline`` (main/inference/convert.py:388-458) on torch-CPU / numpy / scipy.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  f0 method "rmvpe", no
+FAISS index (retrieval is a §8(f) "next" row), volume_envelope = 1, no f0
+file, no autotune.  Noise is injected through ``noise(seg, name, shape)``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from scipy import signal
+
+from . import contentvec as cv
+from . import rmvpe as rm
+from . import synth as sy
+
+BH, AH = signal.butter(N=5, Wn=48, btype="high", fs=16000)  # convert.py:30
+
+
+class Consts:
+    """VC.__init__ (convert.py:181-204) with the fp32 Config windows (1, 6, 38, 41)."""
+
+    def __init__(self, tgt_sr, x_pad=1, x_query=6, x_center=38, x_max=41):
+        self.sr, self.window = 16000, 160
+        self.x_pad = x_pad
+        self.t_pad = self.sr * x_pad
+        self.t_pad_tgt = tgt_sr * x_pad
+        self.t_pad2 = self.t_pad * 2
+        self.t_query = self.sr * x_query
+        self.t_center = self.sr * x_center
+        self.t_max = self.sr * x_max
+        self.f0_min, self.f0_max = 50, 1100
+        self.f0_mel_min = 1127 * np.log(1 + self.f0_min / 700)
+        self.f0_mel_max = 1127 * np.log(1 + self.f0_max / 700)
+
+
+def coarse_f0(f0: np.ndarray, pitch: float, c: Consts):
+    """VC.get_f0 tail (convert.py:311-323)."""
+    f0 = f0 * pow(2, pitch / 12)
+    f0_mel = 1127 * np.log(1 + f0 / 700)
+    f0_mel[f0_mel > 0] = (f0_mel[f0_mel > 0] - c.f0_mel_min) * 254 / (c.f0_mel_max - c.f0_mel_min) + 1
+    f0_mel[f0_mel <= 1] = 1
+    f0_mel[f0_mel > 255] = 255
+    return np.rint(f0_mel).astype(np.int32), f0.copy()
+
+
+def segment_points(audio: np.ndarray, c: Consts):
+    """Quiet-point segmentation for long inputs (convert.py:404-412)."""
+    opt_ts = []
+    audio_pad = np.pad(audio, (c.window // 2, c.window // 2), mode="reflect")
+    if audio_pad.shape[0] > c.t_max:
+        audio_sum = np.zeros_like(audio)
+        for i in range(c.window):
+            audio_sum += audio_pad[i: i - c.window]
+        for t in range(c.t_center, audio.shape[0], c.t_center):
+            seg = np.abs(audio_sum[t - c.t_query: t + c.t_query])
+            opt_ts.append(t - c.t_query + np.where(seg == seg.min())[0][0])
+    return opt_ts
+
+
+def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, z_noise, sine_noise, trace=None):
+    """VC.voice_conversion (convert.py:328-386), ``.pt`` embedder, ``.pth`` model, no index."""
+    window = 160
+    feats = torch.from_numpy(audio0).float().view(1, -1)
+    with torch.no_grad():
+        x = cv.extract_features(Wc, feats, 9 if version == "v1" else 12)
+        feats = cv.final_proj(Wc, x) if version == "v1" else x
+        if trace is not None:
+            trace["feats"] = feats.clone()
+        if protect < 0.5:
+            feats0 = feats.clone()
+        feats = F.interpolate(feats.permute(0, 2, 1), scale_factor=2).permute(0, 2, 1)
+        if protect < 0.5:
+            feats0 = F.interpolate(feats0.permute(0, 2, 1), scale_factor=2).permute(0, 2, 1)
+        p_len = audio0.shape[0] // window
+        if feats.shape[1] < p_len:
+            p_len = feats.shape[1]
+            pitch = pitch[:, :p_len]
+            pitchf = pitchf[:, :p_len]
+        if protect < 0.5:
+            pitchff = pitchf.clone()
+            pitchff[pitchf > 0] = 1
+            pitchff[pitchf < 1] = protect
+            pitchff = pitchff.unsqueeze(-1)
+            feats = (feats * pitchff + feats0 * (1 - pitchff)).to(feats0.dtype)
+        p_len_t = torch.tensor([p_len]).long()
+        o, _, (z, z_p, m_p, logs_p) = sy.infer(Ws, cfg, feats.float(), p_len_t, pitch, pitchf.float(), sid,
+                                               z_noise, sine_noise)
+        if trace is not None:
+            trace.update(phone=feats, z_p=z_p, z=z, m_p=m_p, logs_p=logs_p)
+    return o[0, 0].numpy()
+
+
+def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None):
+    """VC.pipeline (convert.py:388-458): f0 = rmvpe, no index, volume_envelope = 1.
+
+    noise(seg_index, name, shape) -> torch tensor for "z" [1, 192, T] and "sine" [1, T*upp, 1]."""
+    tgt_sr = cfg[-1]
+    upp = int(np.prod(cfg[12]))
+    c = Consts(tgt_sr)
+    audio = signal.filtfilt(BH, AH, audio)
+    opt_ts = segment_points(audio, c)
+    s = 0
+    t = None
+    audio_opt = []
+    audio_pad = np.pad(audio, (c.t_pad, c.t_pad), mode="reflect")
+    sid_t = torch.tensor(sid).unsqueeze(0).long()
+    p_len = audio_pad.shape[0] // c.window
+    f0 = rm.infer_from_audio(Wr, mel_basis, audio_pad, thred=0.03)
+    pitch_c, pitchf = coarse_f0(f0, pitch, c)
+    if trace is not None:
+        trace["f0_raw"] = f0
+        trace["coarse"] = pitch_c.copy()
+    pitch_c, pitchf = pitch_c[:p_len], pitchf[:p_len]
+    pitch_t = torch.tensor(pitch_c).unsqueeze(0).long()
+    pitchf_t = torch.tensor(pitchf).unsqueeze(0).float()
+
+    def run(seg, a0, pch, pchf):
+        T = min(a0.shape[0] // c.window, 2 * cv.frames(a0.shape[0]))
+        tr = {} if trace is not None else None
+        out = voice_conversion(Wc, Ws, cfg, sid_t, a0, pch, pchf, version, protect,
+                               noise(seg, "z", (1, cfg[2], T)), noise(seg, "sine", (1, T * upp, 1)), tr)
+        if trace is not None:
+            trace.setdefault("segments", []).append(tr)
+        return out[c.t_pad_tgt: -c.t_pad_tgt]
+
+    seg = 0
+    for t in opt_ts:
+        t = t // c.window * c.window
+        audio_opt.append(run(seg, audio_pad[s: t + c.t_pad2 + c.window],
+                             pitch_t[:, s // c.window: (t + c.t_pad2) // c.window],
+                             pitchf_t[:, s // c.window: (t + c.t_pad2) // c.window]))
+        s = t
+        seg += 1
+    audio_opt.append(run(seg, audio_pad[t:] if t is not None else audio_pad,
+                         pitch_t[:, t // c.window:] if t is not None else pitch_t,
+                         pitchf_t[:, t // c.window:] if t is not None else pitchf_t))
+    audio_opt = np.concatenate(audio_opt)
+    audio_max = np.abs(audio_opt).max() / 0.99
+    if audio_max > 1:
+        audio_opt /= audio_max
+    return audio_opt

@@ -1,0 +1,257 @@
+"""Generate golden vectors by running the REFERENCE (RVC-MAKER) itself on CPU.
+
+Run in the survey container only (``/root/reference`` must exist):
+
+    python tests/golden/make_golden.py
+
+The reference is imported from ``/root/reference`` through a scratch working
+directory (``main`` -> the reference's ``main``, ``assets/languages`` linked,
+``assets/logs`` and ``assets/models`` writable) with stub modules for the
+packages this image lacks: ``librosa`` (only ``filters.mel`` is
+used on the path; the stub returns ``rvc_amd.melbasis`` -- parity vs librosa
+itself is therefore unpinned), ``omegaconf``, ``faiss``, ``onnxruntime``,
+``soundfile``, ``pydub``.  Weights are the seeded synthetic checkpoints of
+``rvc_amd.synthetic`` written in the reference's own checkpoint layouts and
+loaded through the reference's loaders.  Every RNG draw the reference makes
+(``torch.randn_like`` / ``torch.rand``) is recorded and stored, so the HIP path
+can be run with identical noise.
+
+Outputs (data only -- inputs and expected outputs) go to ``tests/golden/*.npz``.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "rvc-maker_amd"))
+from rvc_amd import melbasis, synthetic  # noqa: E402
+
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def _stub_modules():
+    lib = types.ModuleType("librosa")
+    filt = types.ModuleType("librosa.filters")
+
+    def mel(sr, n_fft, n_mels, fmin, fmax, htk=False, **kw):
+        assert htk
+        return melbasis.mel_filterbank(sr, n_fft, n_mels, fmin, fmax)
+
+    filt.mel = mel
+    lib.filters = filt
+    sys.modules["librosa"] = lib
+    sys.modules["librosa.filters"] = filt
+    om = types.ModuleType("omegaconf")
+    om.DictConfig = dict
+
+    class _Ctx:
+        def __init__(self, x):
+            self.x = x
+
+        def __enter__(self):
+            return self.x
+
+        def __exit__(self, *a):
+            return False
+
+    om.open_dict = _Ctx
+    sys.modules["omegaconf"] = om
+    for name in ("faiss", "soundfile", "pydub"):
+        m = types.ModuleType(name)
+        sys.modules[name] = m
+    sys.modules["pydub"].AudioSegment = object
+    ort = types.ModuleType("onnxruntime")
+    ort.get_available_providers = lambda: ["CPUExecutionProvider"]
+    sys.modules["onnxruntime"] = ort
+
+
+class NoiseRecorder:
+    """Wraps torch.randn_like / torch.rand to record every draw in order."""
+
+    def __init__(self):
+        self.draws = []
+        self._rl, self._r = torch.randn_like, torch.rand
+
+    def __enter__(self):
+        def rl(*a, **k):
+            out = self._rl(*a, **k)
+            self.draws.append(("randn_like", out.detach().clone()))
+            return out
+
+        def r(*a, **k):
+            out = self._r(*a, **k)
+            self.draws.append(("rand", out.detach().clone()))
+            return out
+
+        torch.randn_like, torch.rand = rl, r
+        return self
+
+    def __exit__(self, *a):
+        torch.randn_like, torch.rand = self._rl, self._r
+
+
+class Pbar:
+    def update(self, n):
+        pass
+
+
+def setup_harness():
+    work = tempfile.mkdtemp(prefix="rvc_golden_")
+    os.symlink(os.path.join(REF, "main"), os.path.join(work, "main"))
+    os.makedirs(os.path.join(work, "assets", "logs"))
+    os.makedirs(os.path.join(work, "assets", "models", "predictors"))
+    os.makedirs(os.path.join(work, "assets", "models", "embedders"))
+    os.symlink(os.path.join(REF, "assets", "languages"), os.path.join(work, "assets", "languages"))
+    os.chdir(work)
+    sys.path.insert(0, work)
+    sys.dont_write_bytecode = True
+    _stub_modules()
+    return work
+
+
+def build_ref_synth(ckpt):
+    from main.library.algorithm.synthesizers import Synthesizer
+    version = ckpt["version"]
+    net_g = Synthesizer(*ckpt["config"], use_f0=1, text_enc_hidden_dim=768 if version == "v2" else 256,
+                        vocoder="Default", checkpointing=False)
+    del net_g.enc_q
+    missing, unexpected = net_g.load_state_dict(ckpt["weight"], strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    return net_g.eval().float()
+
+
+def gen_synth(name, sr, version, T, seed):
+    """Synthesizer.infer on seeded phone / pitch / pitchf (synthesizers.py:446)."""
+    ckpt = synthetic.make_synth_ckpt(sr, version, seed=seed)
+    net_g = build_ref_synth(ckpt)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    emb = 768 if version == "v2" else 256
+    phone = rng.standard_normal((1, T, emb)).astype(np.float32)
+    pitch = rng.integers(1, 256, size=(1, T)).astype(np.int64)
+    pitchf = rng.uniform(60, 500, size=(1, T)).astype(np.float32)
+    pitchf[:, rng.random(T) < 0.25] = 0.0  # unvoiced frames
+    sid = np.array([3], dtype=np.int64)
+    torch.manual_seed(seed + 2)
+    with torch.no_grad(), NoiseRecorder() as rec:
+        o, x_mask, (z, z_p, m_p, logs_p) = net_g.infer(torch.from_numpy(phone), torch.tensor([T]),
+                                                       torch.from_numpy(pitch), torch.from_numpy(pitchf),
+                                                       torch.from_numpy(sid))
+    kinds = [k for k, _ in rec.draws]
+    assert kinds == ["randn_like", "rand", "randn_like"], kinds
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), sr=sr, version=version, seed=seed, T=T,
+                        phone=phone, pitch=pitch, pitchf=pitchf, sid=sid,
+                        z_noise=rec.draws[0][1].numpy(), sine_noise=rec.draws[2][1].numpy(),
+                        o=o.numpy(), z=z.numpy(), z_p=z_p.numpy(), m_p=m_p.numpy(), logs_p=logs_p.numpy())
+    print(name, "o rms", float(o.pow(2).mean().sqrt()))
+
+
+def gen_contentvec(seconds, seed):
+    from main.library.architectures import fairseq
+    ck = synthetic.make_contentvec_ckpt(seed)
+    path = os.path.join("assets", "models", "embedders", "contentvec_synth.pt")
+    torch.save(ck, path)
+    models, _, _ = fairseq.load_model(path)
+    m = models[0].float().eval()
+    audio = synthetic.synthetic_audio(seconds, seed=seed + 5)
+    src = torch.from_numpy(audio).view(1, -1)
+    with torch.no_grad():
+        pm = torch.BoolTensor(src.shape).fill_(False)
+        v2 = m.extract_features(source=src, padding_mask=pm, output_layer=12)[0]
+        l9 = m.extract_features(source=src, padding_mask=pm, output_layer=9)[0]
+        v1 = m.final_proj(l9)
+        conv = m.extract_features(source=src, padding_mask=pm, ret_conv=True)[0]
+    np.savez_compressed(os.path.join(OUT, "contentvec.npz"), seed=seed, audio=audio, feats_v2=v2.numpy(),
+                        feats_v1=v1.numpy(), conv_feats=conv.numpy())
+    print("contentvec", tuple(v2.shape), float(v2.std()))
+
+
+def gen_rmvpe(seconds, seed):
+    from main.library.predictors.RMVPE import RMVPE
+    sd = synthetic.rmvpe_state_dict(seed)
+    path = os.path.join("assets", "models", "predictors", "rmvpe.pt")
+    torch.save(sd, path)
+    r = RMVPE(path, is_half=False, device="cpu")
+    audio = synthetic.synthetic_audio(seconds, seed=seed + 5).astype(np.float64)
+    with torch.no_grad():
+        mel = r.mel_extractor(torch.from_numpy(audio).float().unsqueeze(0), center=True)
+        hidden = r.mel2hidden(mel)
+    f0 = r.infer_from_audio(audio, thred=0.03)
+    # decode on a peaked synthetic salience (exercises the 9-bin average and threshold)
+    rng = np.random.Generator(np.random.PCG64(seed + 9))
+    T = 257
+    sal = (rng.random((T, 360)) * 0.02).astype(np.float32)
+    c = rng.integers(0, 360, size=T)
+    for i in range(T):
+        for d in range(-4, 5):
+            if 0 <= c[i] + d < 360:
+                sal[i, c[i] + d] += np.float32(max(0.0, 0.9 - 0.2 * abs(d)) * rng.random())
+    sal[::7] *= 0.5
+    sal[::11] = (sal[::11] * 0.03).astype(np.float32)
+    f0_kat = r.decode(sal, thred=0.03)
+    np.savez_compressed(os.path.join(OUT, "rmvpe.npz"), seed=seed, audio=audio, mel=mel.numpy(),
+                        hidden=hidden.numpy(), f0=f0, kat_salience=sal, kat_f0=f0_kat)
+    print("rmvpe", tuple(mel.shape), tuple(hidden.shape), float(np.mean(f0)))
+
+
+def gen_pipeline(name, sr, version, seconds, seed, pitch, protect):
+    import main.inference.convert as conv
+    ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
+    net_g = build_ref_synth(ck)
+    from main.library.architectures import fairseq
+    cpath = os.path.join("assets", "models", "embedders", "contentvec_synth.pt")
+    torch.save(synthetic.make_contentvec_ckpt(seed + 1), cpath)
+    hub = fairseq.load_model(cpath)[0][0].float().eval()
+    torch.save(synthetic.rmvpe_state_dict(seed + 2), os.path.join("assets", "models", "predictors", "rmvpe.pt"))
+    vc = conv.VC(sr, conv.config)
+    audio = synthetic.synthetic_audio(seconds, seed=seed + 3)
+    torch.manual_seed(seed + 4)
+    with NoiseRecorder() as rec:
+        out = vc.pipeline(model=hub, net_g=net_g, sid=0, audio=audio.copy(), pitch=pitch, f0_method="rmvpe",
+                          file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3, volume_envelope=1,
+                          version=version, protect=protect, hop_length=64, f0_autotune=False,
+                          f0_autotune_strength=1, suffix=".pth", embed_suffix=".pt", f0_file=None, f0_onnx=False,
+                          pbar=Pbar())
+    kinds = [k for k, _ in rec.draws]
+    assert len(kinds) % 3 == 0 and kinds[:3] == ["randn_like", "rand", "randn_like"], kinds
+    nseg = len(kinds) // 3
+    arrs = {}
+    for s in range(nseg):
+        arrs[f"z_noise_{s}"] = rec.draws[3 * s][1].numpy()
+        arrs[f"sine_noise_{s}"] = rec.draws[3 * s + 2][1].numpy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), sr=sr, version=version, seed=seed, pitch=pitch,
+                        protect=protect, audio=audio, out=out, nseg=nseg, x_pad=conv.config.x_pad, **arrs)
+    print(name, "out", out.shape, float(np.sqrt(np.mean(out ** 2))), "segments", nseg)
+
+
+def gen_filtfilt(seed):
+    from scipy import signal
+    import main.inference.convert as conv
+    rng = np.random.Generator(np.random.PCG64(seed))
+    x = rng.standard_normal(20000) * 0.3
+    np.savez_compressed(os.path.join(OUT, "filtfilt.npz"), x=x, y=signal.filtfilt(conv.bh, conv.ah, x),
+                        bh=conv.bh, ah=conv.ah)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    setup_harness()
+    torch.set_num_threads(8)
+    gen_synth("synth_48k_v2", 48000, "v2", 120, seed=11)
+    gen_synth("synth_40k_v2", 40000, "v2", 100, seed=12)
+    gen_synth("synth_32k_v1", 32000, "v1", 100, seed=13)
+    gen_contentvec(1.0, seed=21)
+    gen_rmvpe(1.0, seed=31)
+    gen_filtfilt(seed=41)
+    gen_pipeline("pipeline_48k_v2", 48000, "v2", 2.0, seed=51, pitch=0, protect=0.33)
+    gen_pipeline("pipeline_32k_v1", 32000, "v1", 1.5, seed=52, pitch=3, protect=0.5)
+
+
+if __name__ == "__main__":
+    main()

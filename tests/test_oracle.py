@@ -1,0 +1,113 @@
+"""The oracle (CPU restatement) pinned against golden vectors produced by the reference itself."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import contentvec as ocv
+from oracle import pipeline as opl
+from oracle import rmvpe as orm
+from oracle import synth as osy
+from rvc_amd import melbasis, synthetic
+
+
+def rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
+
+
+@pytest.mark.parametrize("name", ["synth_48k_v2", "synth_40k_v2", "synth_32k_v1"])
+def test_synth_infer_matches_reference(golden, name):
+    g = golden(name)
+    ck = synthetic.make_synth_ckpt(int(g["sr"]), str(g["version"]), seed=int(g["seed"]))
+    W = osy.load_weights(ck["weight"])
+    with torch.no_grad():
+        o, _, (z, z_p, m_p, logs_p) = osy.infer(
+            W, ck["config"], torch.from_numpy(g["phone"]), torch.tensor([int(g["T"])]), torch.from_numpy(g["pitch"]),
+            torch.from_numpy(g["pitchf"]), torch.from_numpy(g["sid"]), torch.from_numpy(g["z_noise"]),
+            torch.from_numpy(g["sine_noise"]))
+    assert rms(m_p, g["m_p"]) < 1e-5
+    assert rms(logs_p, g["logs_p"]) < 1e-5
+    assert rms(z, g["z"]) < 1e-5
+    assert o.shape == g["o"].shape
+    assert rms(o, g["o"]) < 1e-5
+
+
+def test_contentvec_matches_reference(golden):
+    g = golden("contentvec")
+    W = ocv.load_weights(synthetic.make_contentvec_ckpt(int(g["seed"])))
+    src = torch.from_numpy(g["audio"]).view(1, -1)
+    with torch.no_grad():
+        conv = torch.nn.functional.layer_norm(ocv.feature_extractor(W, src).transpose(1, 2), (512,),
+                                              W["layer_norm.weight"], W["layer_norm.bias"], 1e-5)
+        conv = torch.nn.functional.linear(conv, W["post_extract_proj.weight"], W["post_extract_proj.bias"])
+        v2 = ocv.extract_features(W, src, 12)
+        v1 = ocv.final_proj(W, ocv.extract_features(W, src, 9))
+    assert rms(conv, g["conv_feats"]) < 1e-5
+    assert rms(v2, g["feats_v2"]) < 1e-4
+    assert rms(v1, g["feats_v1"]) < 1e-4
+    assert ocv.frames(len(g["audio"])) == g["feats_v2"].shape[1]
+
+
+def test_rmvpe_matches_reference(golden):
+    g = golden("rmvpe")
+    W = orm.load_weights(synthetic.rmvpe_state_dict(int(g["seed"])))
+    mb = torch.from_numpy(melbasis.mel_filterbank())
+    with torch.no_grad():
+        mel = orm.mel_spectrogram(torch.from_numpy(g["audio"]).float().unsqueeze(0), mb)
+        hid = orm.mel2hidden(W, mel)
+    assert rms(mel, g["mel"]) < 1e-5
+    assert rms(hid, g["hidden"]) < 1e-5
+    f0 = orm.decode(hid.squeeze(0).numpy(), 0.03)
+    assert np.max(np.abs(f0 - g["f0"])) < 1e-2
+    # decode known-answer on a peaked salience: exact f64 arithmetic
+    np.testing.assert_allclose(orm.decode(g["kat_salience"], 0.03), g["kat_f0"], rtol=0, atol=1e-12)
+
+
+def test_own_gru_matches_torch_gru(golden):
+    W = orm.load_weights(synthetic.rmvpe_state_dict(31))
+    x = torch.randn(1, 40, 384, generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        a = orm.bigru(W, x)
+        b = orm.bigru_torch(W, x)
+    assert float((a - b).abs().max()) < 1e-5
+
+
+def test_filtfilt_matches_reference(golden):
+    from scipy import signal
+    g = golden("filtfilt")
+    np.testing.assert_array_equal(opl.BH, g["bh"])
+    np.testing.assert_array_equal(opl.AH, g["ah"])
+    np.testing.assert_allclose(signal.filtfilt(opl.BH, opl.AH, g["x"]), g["y"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1"])
+def test_pipeline_matches_reference(golden, name):
+    g = golden(name)
+    sr, version, seed = int(g["sr"]), str(g["version"]), int(g["seed"])
+    ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
+    Ws = osy.load_weights(ck["weight"])
+    Wc = ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1))
+    Wr = orm.load_weights(synthetic.rmvpe_state_dict(seed + 2))
+    mb = torch.from_numpy(melbasis.mel_filterbank())
+
+    def noise(seg, kind, shape):
+        a = torch.from_numpy(g[f"{'z' if kind == 'z' else 'sine'}_noise_{seg}"])
+        assert tuple(a.shape) == tuple(shape)
+        return a
+
+    out = opl.pipeline(Wc, Ws, Wr, mb, ck["config"], 0, g["audio"].astype(np.float32), float(g["pitch"]), version,
+                       float(g["protect"]), noise)
+    assert out.shape == g["out"].shape
+    assert rms(out, g["out"]) < 1e-5
+
+
+def test_coarse_quantiser_sweep():
+    """VC.get_f0's mel quantiser (convert.py:318-323) on a 0-1500 Hz sweep: unvoiced -> 1, saturates at 255."""
+    c = opl.Consts(48000)
+    f0 = np.linspace(0, 1500, 3001)
+    coarse, f0s = opl.coarse_f0(f0.copy(), 0, c)
+    assert coarse[0] == 1 and coarse[-1] == 255
+    assert np.all(np.diff(coarse) >= 0)
+    assert coarse.dtype == np.int32
+    # mute fixture semantics (assets/logs/mute/f0/mute.wav.npy): silence -> coarse 1
+    z, _ = opl.coarse_f0(np.zeros(301), 0, c)
+    assert np.all(z == 1)
