@@ -1,0 +1,141 @@
+/*
+ * rvc_amd.h -- C ABI of librvc_amd.so, the MI355X (gfx950) kernels behind the
+ * RVC-MAKER voice-conversion hot path (main/inference/convert.py:VC.pipeline).
+ *
+ * The reference is pure Python/PyTorch: it has no FFI of its own on this path
+ * (SURVEY §0).  Every entry point below replaces the torch op(s) the reference
+ * executes at the cited file:line; the Python host package (rvc-maker_amd/rvc_amd)
+ * binds them with ctypes the way the reference's only native binding
+ * (main/library/predictors/WORLD_WRAPPER.py:30-90: ctypes.CDLL, option structs,
+ * caller-allocated outputs) does.  INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All tensors are caller-owned DEVICE buffers (fp32 unless stated), dense,
+ *     channels-first [B][C][L] like torch's NCL.  The library allocates nothing.
+ *   - Every call is stream-ordered on the given hipStream_t and never
+ *     synchronises; it returns RVC_OK or a negative code, with the message in
+ *     rvc_last_error() (thread-local).
+ *   - Weights are pre-packed by the host loader (weight-norm / BatchNorm folded,
+ *     transposed to K-major "KM" = [groups][Cin/groups * K][Cout/groups]).
+ */
+#ifndef RVC_AMD_H
+#define RVC_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* rvc_stream_t; /* == hipStream_t */
+
+enum { RVC_OK = 0, RVC_EINVAL = -22, RVC_EHIP = -5 };
+
+enum {
+    RVC_ACT_NONE = 0,
+    RVC_ACT_LRELU = 1,
+    RVC_ACT_RELU = 2,
+    RVC_ACT_TANH = 3,
+    RVC_ACT_GELU = 4, /* exact erf GELU (torch.nn.GELU / F.gelu) */
+    RVC_ACT_SIGMOID = 5,
+};
+
+const char* rvc_last_error(void);
+int rvc_version(void);
+
+/* ------------------------------------------------------------------ conv1d
+ * Implicit-GEMM 1-D convolution on f32 MFMA (v_mfma_f32_16x16x4_f32).
+ * Replaces every torch.nn.Conv1d / F.conv1d on the path:
+ *   NSF-HiFiGAN conv_pre / noise_convs / ResBlock convs / conv_post
+ *     (synthesizers.py:123,136,161; residuals.py:16-17,32-36),
+ *   flow WaveNet + 1x1 convs (modules.py:27-44, residuals.py:120-129),
+ *   TextEncoder FFN / q,k,v,o / proj (synthesizers.py:198-202,298-305,364),
+ *   ContentVec conv feature extractor and pos_conv and every nn.Linear
+ *     (fairseq.py:1165-1195, 585-592, 204-225, 778-814) as a K=1 conv,
+ *   and, one phase per grid.z, ConvTranspose1d (synthesizers.py:133) through
+ *   the polyphase weight packing done by the host.
+ *
+ *   v = out_scale * act(sum_{c,k} W[m][c][k] * pre(x[b][c][col*stride - pad + k*dil]) + bias[m] + bias2[m])
+ *   v += res[b][m][t]                       (if res)
+ *   y[b][m][t] = v  or  y[b][m][t] += v     (accumulate),   t = col*ostride + ooffset + phase
+ *   pre(v) = in_act(v * in_scale)
+ */
+typedef struct rvc_conv1d_args {
+    const float* x;    /* [B][Ci][Lin] with batch stride x_bstride           */
+    const float* w;    /* KM packed: [nphase][groups][Ci/g*K][Co/g]            */
+    const float* bias; /* [Co] or NULL                                          */
+    const float* bias2;/* [Co] or NULL: second per-channel term added after bias
+                          (speaker conditioning: synthesizers.py:147, modules.py:39-43) */
+    const float* res;  /* [B][Co][Lout] residual added after the activation, or NULL */
+    float* y;          /* [B][Co][Lout]                                         */
+    int64_t B, Ci, Co, Lin, Lout;
+    int64_t ncols;     /* GEMM columns per phase (== Lout for a plain conv)     */
+    int64_t x_bstride, y_bstride, res_bstride, w_bstride; /* 0 = dense default; w: 0 = shared */
+    int K, stride, dil, pad, groups;
+    int nphase, ostride, ooffset;
+    int in_act, out_act, accumulate, _pad0;
+    float in_scale, in_slope, out_slope, out_scale;
+} rvc_conv1d_args;
+
+int rvc_conv1d(const rvc_conv1d_args* a, rvc_stream_t stream);
+
+/* ------------------------------------------------------------------ attention
+ * Flash-style multi-head attention on f32 MFMA over channels-first Q/K/V
+ * ([B][H][D][T], channel stride ldc, t contiguous); O written in the same layout.
+ * Replaces F.multi_head_attention_forward in ContentVec (fairseq.py:355-357,
+ * D = 64, no mask: the single padded key of :1106-1111 has weight exactly 0) and
+ * the TextEncoder's relative-position MHA (synthesizers.py:227-251, D = 96,
+ * window W = 10): pass rk = scale * Q^T Ek as [B][H][2W+1][T], ev = Ev [2W+1][D]
+ * and an ml scratch [B][H][2][T]; the value band term is added in a second pass.
+ */
+typedef struct rvc_attn_args {
+    const float* q;
+    const float* k;
+    const float* v;
+    float* o;
+    const float* rk; /* NULL = no relative band                */
+    const float* ev; /* [2W+1][D] (shared by heads) or NULL     */
+    float* ml;       /* [B][H][2][T] scratch (required with rk) */
+    int64_t B, H, D, T;
+    int64_t ldc;                    /* channel stride (0 = T) */
+    int64_t q_hs, k_hs, v_hs, o_hs; /* head strides           */
+    int64_t q_bs, k_bs, v_bs, o_bs; /* batch strides          */
+    int W, _pad0;
+    float scale, _pad1;
+} rvc_attn_args;
+
+int rvc_attention(const rvc_attn_args* a, rvc_stream_t stream);
+
+/* ------------------------------------------------------------------ elementwise
+ * Memory-bound pieces of Synthesizer.infer (synthesizers.py:446-465).  All
+ * [B][C][T] channels-first.
+ */
+/* out = lrelu((lin + emb[pitch]) * scale, slope)       synthesizers.py:367 */
+int rvc_textenc_embed(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B, int64_t C,
+                      int64_t T, float scale, float slope, rvc_stream_t stream);
+/* LayerNorm over channels of (x + res)                  synthesizers.py:170-181, fairseq.py:700 */
+int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out, int64_t B,
+                     int64_t C, int64_t T, float eps, rvc_stream_t stream);
+/* GroupNorm(C, C) over time + affine (+ exact GELU)      fairseq.py:1149-1155,1183-1185 */
+int rvc_chnorm_gelu(const float* x, const float* gamma, const float* beta, float* out, int64_t B, int64_t C, int64_t L,
+                    float eps, int gelu, rvc_stream_t stream);
+/* z_p = m + exp(logs) * noise * nscale, stats = [m; logs]  synthesizers.py:449 */
+int rvc_prior_sample(const float* stats, const float* noise, float* zp, int64_t B, int64_t C, int64_t T, float nscale,
+                     rvc_stream_t stream);
+/* out = tanh(a[:H]) * sigmoid(a[H:])                    commons.py:35-41 */
+int rvc_gate(const float* a, float* out, int64_t B, int64_t H, int64_t T, rvc_stream_t stream);
+/* out[c] = x[C-1-c]                                      residuals.py:53-58 */
+int rvc_flip_channels(const float* x, float* out, int64_t B, int64_t C, int64_t T, rvc_stream_t stream);
+/* out[b][c][r] = in[b][r][c] */
+int rvc_transpose(const float* in, float* out, int64_t B, int64_t R, int64_t C, rvc_stream_t stream);
+/* standard normal noise, Philox4x32-10 counter stream (seed, offset) */
+int rvc_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, rvc_stream_t stream);
+/* NSF harmonic source: SineGen + Linear(1,1) + tanh    synthesizers.py:69-112
+ * f0 [B][T] -> har [B][T*upp]; noise [B][T*upp]; work: [B][T] floats scratch */
+int rvc_sine_source(const float* f0, const float* noise, float* har, float* work, int64_t B, int64_t T, int upp,
+                    float sr, float lin_w, float lin_b, rvc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RVC_AMD_H */

@@ -1,0 +1,227 @@
+// Memory-bound kernels of the synthesizer path (HBM-bound; one pass each).
+#include "rvc_common.h"
+
+// ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
+RVC_DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+
+__global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread -> 4 normals
+    int64_t base = i * 4;
+    if (base >= n) return;
+    uint64_t ctr = (uint64_t)i + offset;
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x7A3Bu, 0x52u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    float r[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        float u1 = ((c[2 * j] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+        float u2 = (c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
+        float rad = sqrtf(-2.0f * logf(u1));
+        float s, co;
+        sincosf(6.2831853071795864f * u2, &s, &co);
+        r[2 * j] = rad * co;
+        r[2 * j + 1] = rad * s;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (base + j < n) out[base + j] = r[j];
+}
+
+extern "C" int rvc_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, rvc_stream_t stream) {
+    RVC_CHECK_ARG(out && n >= 0, "randn: bad args");
+    if (n == 0) return RVC_OK;
+    int64_t thr = (n + 3) / 4;
+    hipLaunchKernelGGL(randn_kernel, dim3(cdiv(thr, 256)), dim3(256), 0, (hipStream_t)stream, out, n, seed, offset);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- TextEncoder input
+// out[c][t] = lrelu((lin[c][t] + emb[pitch[t]][c]) * scale, slope)     (synthesizers.py:367)
+__global__ void textenc_embed_kernel(const float* lin, const float* emb, const int64_t* pitch, float* out, int C,
+                                     int64_t T, float scale, float slope) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = blockIdx.y;
+    int b = blockIdx.z;
+    if (t >= T) return;
+    int64_t o = ((int64_t)b * C + c) * T + t;
+    float v = lin[o];
+    if (emb) v += emb[pitch[(int64_t)b * T + t] * C + c];
+    v *= scale;
+    out[o] = v >= 0.f ? v : v * slope;
+}
+
+extern "C" int rvc_textenc_embed(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B,
+                                 int64_t C, int64_t T, float scale, float slope, rvc_stream_t stream) {
+    RVC_CHECK_ARG(lin && out && (!emb || pitch) && B > 0 && C > 0 && T > 0, "textenc_embed: bad args");
+    hipLaunchKernelGGL(textenc_embed_kernel, dim3(cdiv(T, 256), (unsigned)C, (unsigned)B), dim3(256), 0,
+                       (hipStream_t)stream, lin, emb, pitch, out, (int)C, T, scale, slope);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- prior sample
+// z_p[c][t] = (m[c][t] + exp(logs[c][t]) * noise[c][t] * 0.66666) * mask   (synthesizers.py:449)
+// stats = [m; logs] stacked on channels ([2C][T]); mask is all ones at full length.
+__global__ void prior_kernel(const float* stats, const float* noise, float* zp, int C, int64_t T, float nscale) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = blockIdx.y, b = blockIdx.z;
+    if (t >= T) return;
+    const float* sb = stats + (int64_t)b * 2 * C * T;
+    float m = sb[(int64_t)c * T + t];
+    float lg = sb[(int64_t)(c + C) * T + t];
+    int64_t o = ((int64_t)b * C + c) * T + t;
+    zp[o] = (m + expf(lg) * noise[o] * nscale);
+}
+
+extern "C" int rvc_prior_sample(const float* stats, const float* noise, float* zp, int64_t B, int64_t C, int64_t T,
+                                float nscale, rvc_stream_t stream) {
+    RVC_CHECK_ARG(stats && noise && zp && B > 0 && C > 0 && T > 0, "prior_sample: bad args");
+    hipLaunchKernelGGL(prior_kernel, dim3(cdiv(T, 256), (unsigned)C, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                       stats, noise, zp, (int)C, T, nscale);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- WaveNet gate
+// out[c][t] = tanh(a[c][t]) * sigmoid(a[c+H][t])     (commons.py:35-41; the cond term is
+// already in a through the conv's bias2)
+__global__ void gate_kernel(const float* a, float* out, int H, int64_t T) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = blockIdx.y, b = blockIdx.z;
+    if (t >= T) return;
+    const float* ab = a + (int64_t)b * 2 * H * T;
+    float x0 = ab[(int64_t)c * T + t], x1 = ab[(int64_t)(c + H) * T + t];
+    out[((int64_t)b * H + c) * T + t] = tanhf(x0) * (1.f / (1.f + expf(-x1)));
+}
+
+extern "C" int rvc_gate(const float* a, float* out, int64_t B, int64_t H, int64_t T, rvc_stream_t stream) {
+    RVC_CHECK_ARG(a && out && B > 0 && H > 0 && T > 0, "gate: bad args");
+    hipLaunchKernelGGL(gate_kernel, dim3(cdiv(T, 256), (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                       a, out, (int)H, T);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- channel flip  (residuals.py:53-58)
+__global__ void flip_kernel(const float* x, float* out, int C, int64_t T) {
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = blockIdx.y, b = blockIdx.z;
+    if (t >= T) return;
+    out[((int64_t)b * C + c) * T + t] = x[((int64_t)b * C + (C - 1 - c)) * T + t];
+}
+
+extern "C" int rvc_flip_channels(const float* x, float* out, int64_t B, int64_t C, int64_t T, rvc_stream_t stream) {
+    RVC_CHECK_ARG(x && out && x != out && B > 0 && C > 0 && T > 0, "flip: bad args");
+    hipLaunchKernelGGL(flip_kernel, dim3(cdiv(T, 256), (unsigned)C, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                       x, out, (int)C, T);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- 2-D transpose (batched)
+__global__ void transpose_kernel(const float* in, float* out, int64_t R, int64_t C) {
+    __shared__ float tile[32][33];
+    int b = blockIdx.z;
+    const float* ib = in + (int64_t)b * R * C;
+    float* ob = out + (int64_t)b * R * C;
+    int64_t c0 = (int64_t)blockIdx.x * 32, r0 = (int64_t)blockIdx.y * 32;
+    int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+    for (int k = ty; k < 32; k += 8) {
+        int64_t r = r0 + k, c = c0 + tx;
+        tile[k][tx] = (r < R && c < C) ? ib[r * C + c] : 0.f;
+    }
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8) {
+        int64_t c = c0 + k, r = r0 + tx;
+        if (c < C && r < R) ob[c * R + r] = tile[tx][k];
+    }
+}
+
+extern "C" int rvc_transpose(const float* in, float* out, int64_t B, int64_t R, int64_t C, rvc_stream_t stream) {
+    RVC_CHECK_ARG(in && out && in != out && B > 0 && R > 0 && C > 0, "transpose: bad args");
+    hipLaunchKernelGGL(transpose_kernel, dim3(cdiv(C, 32), cdiv(R, 32), (unsigned)B), dim3(256), 0,
+                       (hipStream_t)stream, in, out, R, C);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- NSF source (SineGen + SourceModuleHnNSF)
+// synthesizers.py:82-112, harmonic_num = 0.  Frame phase offsets follow torch-CPU's
+// float32 cumsum exactly: f32 increments, f64 running sum, f32 per-element result,
+// then fmodf (SURVEY §0 "CPU-only precision traps").
+__global__ void sine_offsets_kernel(const float* f0, float* off, int64_t T, float sr, float upp) {
+    // one block of 1024 per batch row: exclusive f64 prefix over frames
+    __shared__ double part[1024];
+    const int b = blockIdx.x;
+    const float* fb = f0 + (int64_t)b * T;
+    float* ob = off + (int64_t)b * T;
+    const int tid = threadIdx.x;
+    const int64_t per = (T + 1023) / 1024;
+    const int64_t lo = tid * per, hi = lo + per < T ? lo + per : T;
+    double s = 0.0;
+    for (int64_t t = lo; t < hi; ++t) {
+        if (t >= T - 1) break;  // increments exist for frames 0..T-2
+        float r = (fb[t] / sr) * upp;
+        float inc = fmodf(r + 0.5f, 1.0f) - 0.5f;
+        s += (double)inc;
+    }
+    part[tid] = s;
+    __syncthreads();
+    // inclusive scan over 1024 partials (Hillis-Steele in f64)
+    for (int o = 1; o < 1024; o <<= 1) {
+        double v = tid >= o ? part[tid - o] : 0.0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    double run = tid > 0 ? part[tid - 1] : 0.0;
+    for (int64_t t = lo; t < hi; ++t) {
+        // offset for frame t = fmod(cum[t-1], 1) with cum[-1] := padded 0
+        ob[t] = (t == 0) ? 0.f : fmodf((float)run, 1.0f);
+        if (t < T - 1) {
+            float r = (fb[t] / sr) * upp;
+            float inc = fmodf(r + 0.5f, 1.0f) - 0.5f;
+            run += (double)inc;
+        }
+    }
+}
+
+__global__ void sine_source_kernel(const float* f0, const float* off, const float* noise, float* har, int64_t T,
+                                   int upp, float sr, float lw, float lb) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int b = blockIdx.y;
+    int64_t L = T * upp;
+    if (i >= L) return;
+    int64_t t = i / upp;
+    int j = (int)(i - t * upp);
+    float f = f0[(int64_t)b * T + t];
+    float rad = (f / sr) * (float)(j + 1) + off[(int64_t)b * T + t];
+    float s = sinf(6.2831855f * rad) * 0.1f;
+    float uv = f > 0.f ? 1.f : 0.f;
+    float n = noise[(int64_t)b * L + i];
+    float v = s * uv + ((uv * 0.003f + ((1.f - uv) * 0.1f) / 3.0f) * n);
+    har[(int64_t)b * L + i] = tanhf(v * lw + lb);
+}
+
+extern "C" int rvc_sine_source(const float* f0, const float* noise, float* har, float* work, int64_t B, int64_t T,
+                               int upp, float sr, float lin_w, float lin_b, rvc_stream_t stream) {
+    RVC_CHECK_ARG(f0 && noise && har && work && B > 0 && T > 0 && upp > 0, "sine_source: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(sine_offsets_kernel, dim3((unsigned)B), dim3(1024), 0, s, f0, work, T, sr, (float)upp);
+    RVC_HIP(hipGetLastError());
+    hipLaunchKernelGGL(sine_source_kernel, dim3(cdiv(T * upp, 256), (unsigned)B), dim3(256), 0, s, f0, work, noise,
+                       har, T, upp, sr, lin_w, lin_b);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}

@@ -1,0 +1,105 @@
+// Normalisations over the channels-first activations ([B][C][T], t contiguous).
+#include "rvc_common.h"
+
+// ---------------------------------------------------------------- LayerNorm over channels
+// out[c][t] = (v - mean_t) * rstd_t * gamma[c] + beta[c],  v = x[c][t] (+ res[c][t])
+// A block owns 16 columns: the [C][16] tile is read once from HBM into LDS (64-B row
+// segments), 16 threads reduce each column (two-pass mean / variance, as F.layer_norm),
+// then the tile is written back.  Covers synthesizers.py:170-181 and the fairseq
+// LayerNorms (fairseq.py:700, 1418, 1104) on this build's [C][T] layout.
+__global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const float* res, const float* gamma,
+                                                           const float* beta, float* out, int C, int64_t T,
+                                                           float eps) {
+    extern __shared__ __attribute__((aligned(16))) float tile[];  // [C][17]
+    const int tid = threadIdx.x;
+    const int col = tid & 15, grp = tid >> 4;  // 16 columns x 16 channel groups
+    const int b = blockIdx.y;
+    const int64_t t0 = (int64_t)blockIdx.x * 16;
+    const int64_t t = t0 + col;
+    const bool ok = t < T;
+    const float* xb = x + (int64_t)b * C * T;
+    const float* rb = res ? res + (int64_t)b * C * T : nullptr;
+    float s = 0.f;
+    for (int c = grp; c < C; c += 16) {
+        float v = 0.f;
+        if (ok) {
+            v = xb[(int64_t)c * T + t];
+            if (rb) v += rb[(int64_t)c * T + t];
+        }
+        tile[c * 17 + col] = v;
+        s += v;
+    }
+    float* red = tile + C * 17;  // [16][17]
+    red[grp * 17 + col] = s;
+    __syncthreads();
+    float mean = 0.f;
+    for (int g = 0; g < 16; ++g) mean += red[g * 17 + col];
+    mean /= (float)C;
+    float q = 0.f;
+    for (int c = grp; c < C; c += 16) {
+        float d = tile[c * 17 + col] - mean;
+        q += d * d;
+    }
+    __syncthreads();
+    red[grp * 17 + col] = q;
+    __syncthreads();
+    float var = 0.f;
+    for (int g = 0; g < 16; ++g) var += red[g * 17 + col];
+    const float rstd = 1.0f / sqrtf(var / (float)C + eps);
+    if (!ok) return;
+    float* ob = out + (int64_t)b * C * T;
+    for (int c = grp; c < C; c += 16) ob[(int64_t)c * T + t] = (tile[c * 17 + col] - mean) * rstd * gamma[c] + beta[c];
+}
+
+extern "C" int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out,
+                                int64_t B, int64_t C, int64_t T, float eps, rvc_stream_t stream) {
+    RVC_CHECK_ARG(x && gamma && beta && out && B > 0 && C > 0 && T > 0, "layernorm_cf: bad args");
+    RVC_CHECK_ARG(C <= 2048, "layernorm_cf: C=%lld > 2048", (long long)C);
+    size_t lds = (size_t)(C + 16) * 17 * 4;
+    hipLaunchKernelGGL(layernorm_cf_kernel, dim3(cdiv(T, 16), (unsigned)B), dim3(256), lds, (hipStream_t)stream, x,
+                       res, gamma, beta, out, (int)C, T, eps);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- per-channel norm (+GELU)
+// GroupNorm(C, C) over time, affine, then exact GELU: the ContentVec conv feature
+// extractor's first block (fairseq.py:1149-1155, 1183-1185).  One block per (b, c).
+__global__ __launch_bounds__(256) void chnorm_gelu_kernel(const float* x, const float* gamma, const float* beta,
+                                                          float* out, int C, int64_t L, float eps, int gelu) {
+    const int c = blockIdx.x, b = blockIdx.y;
+    const float* xr = x + ((int64_t)b * C + c) * L;
+    float* orow = out + ((int64_t)b * C + c) * L;
+    __shared__ float red[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float s = 0.f;
+    for (int64_t i = tid; i < L; i += 256) s += xr[i];
+    s = wave_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)L;
+    __syncthreads();
+    float q = 0.f;
+    for (int64_t i = tid; i < L; i += 256) {
+        float d = xr[i] - mean;
+        q += d * d;
+    }
+    q = wave_sum(q);
+    if (lane == 0) red[w] = q;
+    __syncthreads();
+    const float rstd = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)L + eps);
+    const float g = gamma[c], bt = beta[c];
+    for (int64_t i = tid; i < L; i += 256) {
+        float v = (xr[i] - mean) * rstd * g + bt;
+        orow[i] = gelu ? act_apply(v, RVC_ACT_GELU, 0.f) : v;
+    }
+}
+
+extern "C" int rvc_chnorm_gelu(const float* x, const float* gamma, const float* beta, float* out, int64_t B, int64_t C,
+                               int64_t L, float eps, int gelu, rvc_stream_t stream) {
+    RVC_CHECK_ARG(x && gamma && beta && out && B > 0 && C > 0 && L > 0, "chnorm_gelu: bad args");
+    hipLaunchKernelGGL(chnorm_gelu_kernel, dim3((unsigned)C, (unsigned)B), dim3(256), 0, (hipStream_t)stream, x, gamma,
+                       beta, out, (int)C, L, eps, gelu);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}

@@ -1,0 +1,82 @@
+"""ctypes binding of librvc_amd.so (include/rvc_amd.h).
+
+The library is built in-tree (``rvc-maker_amd/lib/librvc_amd.so``) by
+``__graft_entry__.build()`` / ``make -C rvc-maker_amd/csrc``.  There is no
+fallback: if the library is missing or a call fails, a RuntimeError is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_int64, c_uint64, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "librvc_amd.so")
+
+ACT_NONE, ACT_LRELU, ACT_RELU, ACT_TANH, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
+
+
+class Conv1dArgs(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("bias2", c_void_p), ("res", c_void_p),
+                ("y", c_void_p),
+                ("B", c_int64), ("Ci", c_int64), ("Co", c_int64), ("Lin", c_int64), ("Lout", c_int64),
+                ("ncols", c_int64), ("x_bstride", c_int64), ("y_bstride", c_int64), ("res_bstride", c_int64),
+                ("w_bstride", c_int64),
+                ("K", c_int), ("stride", c_int), ("dil", c_int), ("pad", c_int), ("groups", c_int),
+                ("nphase", c_int), ("ostride", c_int), ("ooffset", c_int),
+                ("in_act", c_int), ("out_act", c_int), ("accumulate", c_int), ("_pad0", c_int),
+                ("in_scale", c_float), ("in_slope", c_float), ("out_slope", c_float), ("out_scale", c_float)]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("rk", c_void_p),
+                ("ev", c_void_p), ("ml", c_void_p),
+                ("B", c_int64), ("H", c_int64), ("D", c_int64), ("T", c_int64), ("ldc", c_int64),
+                ("q_hs", c_int64), ("k_hs", c_int64), ("v_hs", c_int64), ("o_hs", c_int64),
+                ("q_bs", c_int64), ("k_bs", c_int64), ("v_bs", c_int64), ("o_bs", c_int64),
+                ("W", c_int), ("_pad0", c_int), ("scale", c_float), ("_pad1", c_float)]
+
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+SIGNATURES = {
+    "rvc_last_error": [],
+    "rvc_version": [],
+    "rvc_conv1d": [POINTER(Conv1dArgs), c_void_p],
+    "rvc_attention": [POINTER(AttnArgs), c_void_p],
+    "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
+                          c_void_p],
+    "rvc_layernorm_cf": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
+                         c_void_p],
+    "rvc_chnorm_gelu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_int, c_void_p],
+    "rvc_prior_sample": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
+    "rvc_gate": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_flip_channels": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_transpose": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_randn": [c_void_p, c_int64, c_uint64, c_uint64, c_void_p],
+    "rvc_sine_source": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_float, c_float, c_float,
+                        c_void_p],
+}
+_RESTYPES = {"rvc_last_error": ctypes.c_char_p}
+
+_lib = None
+
+
+def load():
+    """Load the HIP library once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"rvc_amd: HIP library not built ({LIB_PATH}); run __graft_entry__.build() "
+                           "or `make -C rvc-maker_amd/csrc`. There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = _RESTYPES.get(name, c_int)
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"rvc_amd: {what} failed ({rc}): {load().rvc_last_error().decode()}")

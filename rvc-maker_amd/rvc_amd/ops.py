@@ -1,0 +1,204 @@
+"""Tensor-level wrappers over the C ABI (torch tensors are only device buffers + streams here).
+
+Every function checks shapes on the host before launching (a kernel that reads out
+of bounds can reset the GPU), passes raw pointers, and raises on a non-zero status.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import ACT_GELU, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, check  # noqa: F401
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    if t is None:
+        return None
+    if not t.is_cuda or t.dtype not in (torch.float32, torch.int64, torch.int32):
+        raise TypeError(f"rvc_amd: expected a CUDA f32/int tensor, got {t.dtype} on {t.device}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# ------------------------------------------------------------------ weight packing (host, load time)
+def pack_km(w: torch.Tensor, groups: int = 1) -> torch.Tensor:
+    """Conv weight [Co, Ci/g, K] -> KM layout [g][Ci/g*K][Co/g] (k = c*K + tap, m contiguous)."""
+    Co, Cig, K = w.shape
+    Cog = Co // groups
+    return w.reshape(groups, Cog, Cig, K).permute(0, 2, 3, 1).reshape(groups, Cig * K, Cog).contiguous()
+
+
+def pack_convT(w: torch.Tensor, u: int) -> tuple[torch.Tensor, int]:
+    """ConvTranspose1d weight [Ci, Co, K] (stride u) -> polyphase KM [u][Ci*T][Co], T = ceil(K/u).
+
+    Phase r computes outputs t with (t + pad) % u == r as a stride-1 conv over x with taps
+    tp in [0, T): x[q - (T-1) + tp] * W[ci][co][r + (T-1-tp)*u]  (zero where that tap >= K)."""
+    Ci, Co, K = w.shape
+    T = -(-K // u)
+    out = torch.zeros(u, Ci, T, Co, dtype=w.dtype)
+    for r in range(u):
+        for tp in range(T):
+            j = r + (T - 1 - tp) * u
+            if j < K:
+                out[r, :, tp, :] = w[:, :, j]
+    return out.reshape(u, Ci * T, Co).contiguous(), T
+
+
+class Conv:
+    """A packed Conv1d (weight [Co, Ci/g, K], bias [Co]) resident on the device."""
+
+    def __init__(self, w, b=None, groups=1, device="cuda"):
+        self.Co, self.Cig, self.K = (int(s) for s in w.shape)
+        self.groups = groups
+        self.Ci = self.Cig * groups
+        self.w = pack_km(w.float(), groups).to(device)
+        self.b = b.float().to(device) if b is not None else None
+
+    def __call__(self, x, Lout=None, stride=1, pad=0, dil=1, **kw):
+        return conv1d(x, self.w, self.Ci, self.Co, self.K, bias=self.b, stride=stride, pad=pad, dil=dil,
+                      groups=self.groups, Lout=Lout, **kw)
+
+
+class ConvT:
+    """ConvTranspose1d(Ci, Co, K, stride u, padding p, output_padding 0) as u phase convs."""
+
+    def __init__(self, w, b, u, pad, device="cuda"):
+        self.Ci, self.Co, self.K = (int(s) for s in w.shape)
+        self.u, self.pad = u, pad
+        wp, self.T = pack_convT(w.float(), u)
+        self.w = wp.to(device)
+        self.b = b.float().to(device)
+
+    def out_len(self, Lin):
+        return (Lin - 1) * self.u - 2 * self.pad + self.K
+
+    def __call__(self, x, out=None, **kw):
+        B, Ci, Lin = _shape3(x)
+        Lout = self.out_len(Lin)
+        ncols = (Lout - 1 + self.pad) // self.u + 1
+        return conv1d(x, self.w, Ci, self.Co, self.T, bias=self.b, stride=1, pad=self.T - 1, dil=1, Lout=Lout,
+                      ncols=ncols, nphase=self.u, ostride=self.u, ooffset=-self.pad, out=out, **kw)
+
+
+def _shape3(x):
+    if x.dim() == 2:
+        return 1, x.shape[0], x.shape[1]
+    return x.shape[0], x.shape[1], x.shape[2]
+
+
+def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, groups=1, Lout=None, ncols=0,
+           nphase=1, ostride=1, ooffset=0, out=None, res=None, in_act=ACT_NONE, in_slope=0.0, in_scale=1.0,
+           out_act=ACT_NONE, out_slope=0.0, out_scale=1.0, accumulate=False, B=None, Lin=None, x_bstride=0,
+           w_bstride=0, y_bstride=0, res_bstride=0):
+    """y = conv(pre(x)) with fused epilogue.  x: [B][Ci][Lin] device f32 (t contiguous)."""
+    if B is None:
+        B, Cx, Lx = _shape3(x)
+        if Lin is None:
+            Lin = Lx
+        if Cx != Ci:
+            raise ValueError(f"conv1d: x has {Cx} channels, weight expects {Ci}")
+        if not x.is_contiguous():
+            raise ValueError("conv1d: x must be contiguous")
+    if Lout is None:
+        Lout = (Lin + 2 * pad - dil * (K - 1) - 1) // stride + 1
+    if Lout <= 0:
+        raise ValueError("conv1d: empty output")
+    Cig = Ci // groups
+    need_w = nphase * Cig * K * Co
+    if w.numel() < need_w or (w_bstride and w.numel() < need_w + (B - 1) * w_bstride):
+        raise ValueError("conv1d: packed weight too small")
+    if out is None:
+        out = torch.empty(B, Co, Lout, device=x.device, dtype=torch.float32) if B > 1 else \
+            torch.empty(Co, Lout, device=x.device, dtype=torch.float32)
+    elif out.numel() < (B - 1) * (y_bstride or Co * Lout) + Co * Lout:
+        raise ValueError("conv1d: output buffer too small")
+    if res is not None and res.numel() < (B - 1) * (res_bstride or Co * Lout) + Co * Lout:
+        raise ValueError("conv1d: residual too small")
+    if bias is not None and bias.numel() < Co:
+        raise ValueError("conv1d: bias too small")
+    a = _lib.Conv1dArgs()
+    a.x, a.w, a.bias, a.bias2, a.res, a.y = _p(x), _p(w), _p(bias), _p(bias2), _p(res), _p(out)
+    a.B, a.Ci, a.Co, a.Lin, a.Lout, a.ncols = B, Ci, Co, Lin, Lout, ncols
+    a.x_bstride, a.y_bstride, a.res_bstride, a.w_bstride = x_bstride, y_bstride, res_bstride, w_bstride
+    a.K, a.stride, a.dil, a.pad, a.groups = K, stride, dil, pad, groups
+    a.nphase, a.ostride, a.ooffset = nphase, ostride, ooffset
+    a.in_act, a.out_act, a.accumulate = in_act, out_act, int(bool(accumulate))
+    a.in_scale, a.in_slope, a.out_slope, a.out_scale = in_scale, in_slope, out_slope, out_scale
+    check(_lib.load().rvc_conv1d(ctypes.byref(a), _stream()), "conv1d")
+    return out
+
+
+def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_bs=0, k_bs=0, v_bs=0, o_bs=0,
+              rk=None, ev=None, ml=None, W=0):
+    a = _lib.AttnArgs()
+    a.q, a.k, a.v, a.o, a.rk, a.ev, a.ml = _p(q), _p(k), _p(v), _p(o), _p(rk), _p(ev), _p(ml)
+    a.B, a.H, a.D, a.T, a.ldc = B, H, D, T, ldc
+    a.q_hs, a.k_hs, a.v_hs, a.o_hs = q_hs, k_hs, v_hs, o_hs
+    a.q_bs, a.k_bs, a.v_bs, a.o_bs = q_bs, k_bs, v_bs, o_bs
+    a.W, a.scale = W, scale
+    check(_lib.load().rvc_attention(ctypes.byref(a), _stream()), "attention")
+    return o
+
+
+def textenc_embed(lin, emb, pitch, out, B, C, T, scale, slope):
+    check(_lib.load().rvc_textenc_embed(_p(lin), _p(emb), _p(pitch), _p(out), B, C, T, scale, slope, _stream()),
+          "textenc_embed")
+    return out
+
+
+def layernorm_cf(x, res, gamma, beta, out, B, C, T, eps=1e-5):
+    if x.numel() < B * C * T or out.numel() < B * C * T or gamma.numel() < C:
+        raise ValueError("layernorm_cf: size mismatch")
+    check(_lib.load().rvc_layernorm_cf(_p(x), _p(res), _p(gamma), _p(beta), _p(out), B, C, T, eps, _stream()),
+          "layernorm_cf")
+    return out
+
+
+def chnorm_gelu(x, gamma, beta, out, B, C, L, eps=1e-5, gelu=True):
+    if x.numel() < B * C * L or out.numel() < B * C * L:
+        raise ValueError("chnorm_gelu: size mismatch")
+    check(_lib.load().rvc_chnorm_gelu(_p(x), _p(gamma), _p(beta), _p(out), B, C, L, eps, int(gelu), _stream()),
+          "chnorm_gelu")
+    return out
+
+
+def prior_sample(stats, noise, zp, B, C, T, nscale=0.66666):
+    check(_lib.load().rvc_prior_sample(_p(stats), _p(noise), _p(zp), B, C, T, nscale, _stream()), "prior_sample")
+    return zp
+
+
+def gate(a, out, B, H, T):
+    check(_lib.load().rvc_gate(_p(a), _p(out), B, H, T, _stream()), "gate")
+    return out
+
+
+def flip_channels(x, out, B, C, T):
+    check(_lib.load().rvc_flip_channels(_p(x), _p(out), B, C, T, _stream()), "flip")
+    return out
+
+
+def transpose(x, out, B, R, C):
+    check(_lib.load().rvc_transpose(_p(x), _p(out), B, R, C, _stream()), "transpose")
+    return out
+
+
+def randn(out, seed, offset=0):
+    check(_lib.load().rvc_randn(_p(out), out.numel(), seed, offset, _stream()), "randn")
+    return out
+
+
+def sine_source(f0, noise, har, work, B, T, upp, sr, lin_w, lin_b):
+    if f0.numel() < B * T or noise.numel() < B * T * upp or har.numel() < B * T * upp or work.numel() < B * T:
+        raise ValueError("sine_source: size mismatch")
+    check(_lib.load().rvc_sine_source(_p(f0), _p(noise), _p(har), _p(work), B, T, upp, sr, lin_w, lin_b, _stream()),
+          "sine_source")
+    return har
+
+
+SQRT = math.sqrt

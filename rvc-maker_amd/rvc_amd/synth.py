@@ -1,0 +1,260 @@
+"""MI355X Synthesizer: drop-in for ``Synthesizer.infer`` (main/library/algorithm/synthesizers.py:446-465).
+
+Built from a voice-model checkpoint in the reference layout (``train.py:729-742``):
+weight-norm folded once in fp32 on the host at load (``torch._weight_norm``, as the
+reference's parametrization computes it), weights packed K-major and uploaded.
+All compute runs in librvc_amd.so kernels on the current torch stream:
+
+  TextEncoder  conv1d(K=1) + textenc_embed + 6 x [fused QKV conv, rel-pos flash attention,
+               conv_o, LN, FFN (conv k3 ReLU, conv k3), LN] + proj + prior_sample
+  flow^-1      4 x [flip, pre, WaveNet(3 x conv k5 + gate + res/skip convs), post (fused x1 - m)]
+  NSF-HiFiGAN  sine_source, conv_pre(+cond), 4 x [ConvT (polyphase, lrelu fused on staging)
+               + noise_conv (accumulate) + 3 ResBlocks (lrelu fused, residual / running sum
+               fused in the epilogue)], conv_post (lrelu 0.01 + tanh fused)
+
+Only full-length phones are supported (x_mask all ones): in ``VC.voice_conversion``
+``p_len == phone length`` always holds (2*T_f <= N//160).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+from .ops import ACT_LRELU, ACT_RELU, ACT_TANH, Conv, ConvT
+
+LRELU_SLOPE = 0.1
+
+
+def fold_weight_norm(weight: dict) -> dict:
+    """ckpt ``{..., x.weight_g, x.weight_v}`` (fp16) -> fp32 ``{x.weight}`` (dim 0 norm)."""
+    W = {}
+    for k, v in weight.items():
+        if k.endswith(".weight_v"):
+            base = k[: -len(".weight_v")]
+            W[base + ".weight"] = torch._weight_norm(v.float(), weight[base + ".weight_g"].float(), 0)
+        elif not k.endswith(".weight_g"):
+            W[k] = v.float()
+    return W
+
+
+class SynthesizerAMD:
+    def __init__(self, cpt: dict, device: str = "cuda"):
+        cfg = list(cpt["config"])
+        cfg[-3] = cpt["weight"]["emb_g.weight"].shape[0]  # convert.py:558
+        self.cfg = cfg
+        (_, _, self.inter, self.hidden, self.filt, self.n_heads, self.n_layers, self.ksz, _, _, self.rks, self.rds,
+         self.ur, self.uic, self.uks, self.spk, self.gin, self.sr) = cfg
+        self.version = cpt.get("version", "v1")
+        if cpt.get("f0", 1) != 1 or cpt.get("vocoder", "Default") != "Default":
+            raise NotImplementedError("rvc_amd: only NSF-HiFiGAN (f0=1, vocoder Default) models are on the hot path")
+        self.upp = math.prod(self.ur)
+        self.device = device
+        W = fold_weight_norm(cpt["weight"])
+        dev = device
+        H = self.hidden
+        self.kc = H // self.n_heads
+        # ---- TextEncoder
+        self.emb_dim = W["enc_p.emb_phone.weight"].shape[1]
+        self.emb_phone = Conv(W["enc_p.emb_phone.weight"].unsqueeze(-1), W["enc_p.emb_phone.bias"], device=dev)
+        self.emb_pitch = W["enc_p.emb_pitch.weight"].contiguous().to(dev)
+        self.layers = []
+        for i in range(self.n_layers):
+            p = f"enc_p.encoder.attn_layers.{i}."
+            wqkv = torch.cat([W[p + "conv_q.weight"], W[p + "conv_k.weight"], W[p + "conv_v.weight"]], 0)
+            bqkv = torch.cat([W[p + "conv_q.bias"], W[p + "conv_k.bias"], W[p + "conv_v.bias"]], 0)
+            ek = W[p + "emb_rel_k"][0]  # [21, kc]
+            L = dict(
+                qkv=Conv(wqkv, bqkv, device=dev),
+                relk=Conv(ek.unsqueeze(-1), None, device=dev),  # Rk[r][t] = Ek[r] . q[:, t]
+                ev=W[p + "emb_rel_v"][0].contiguous().to(dev),
+                o=Conv(W[p + "conv_o.weight"], W[p + "conv_o.bias"], device=dev),
+                ln1=(W[f"enc_p.encoder.norm_layers_1.{i}.gamma"].to(dev), W[f"enc_p.encoder.norm_layers_1.{i}.beta"].to(dev)),
+                ffn1=Conv(W[f"enc_p.encoder.ffn_layers.{i}.conv_1.weight"], W[f"enc_p.encoder.ffn_layers.{i}.conv_1.bias"], device=dev),
+                ffn2=Conv(W[f"enc_p.encoder.ffn_layers.{i}.conv_2.weight"], W[f"enc_p.encoder.ffn_layers.{i}.conv_2.bias"], device=dev),
+                ln2=(W[f"enc_p.encoder.norm_layers_2.{i}.gamma"].to(dev), W[f"enc_p.encoder.norm_layers_2.{i}.beta"].to(dev)),
+            )
+            self.layers.append(L)
+        self.proj = Conv(W["enc_p.proj.weight"], W["enc_p.proj.bias"], device=dev)
+        # ---- speaker conditioning: all cond convs stacked (4 flows x 3*2H, then dec.cond)
+        conds_w = [W[f"flow.flows.{2 * f}.enc.cond_layer.weight"] for f in range(4)] + [W["dec.cond.weight"]]
+        conds_b = [W[f"flow.flows.{2 * f}.enc.cond_layer.bias"] for f in range(4)] + [W["dec.cond.bias"]]
+        self.cond = Conv(torch.cat(conds_w, 0), torch.cat(conds_b, 0), device=dev)
+        self.emb_g = W["emb_g.weight"].contiguous().to(dev)
+        # ---- flow
+        self.flows = []
+        for f in range(4):
+            p = f"flow.flows.{2 * f}."
+            F = dict(pre=Conv(W[p + "pre.weight"], W[p + "pre.bias"], device=dev), ins=[], rs_a=[], rs_b=[],
+                     post=Conv(W[p + "post.weight"], W[p + "post.bias"], device=dev))
+            for l in range(3):
+                F["ins"].append(Conv(W[p + f"enc.in_layers.{l}.weight"], W[p + f"enc.in_layers.{l}.bias"], device=dev))
+                rw, rb = W[p + f"enc.res_skip_layers.{l}.weight"], W[p + f"enc.res_skip_layers.{l}.bias"]
+                if l < 2:
+                    F["rs_a"].append(Conv(rw[:H], rb[:H], device=dev))
+                    F["rs_b"].append(Conv(rw[H:], rb[H:], device=dev))
+                else:
+                    F["rs_b"].append(Conv(rw, rb, device=dev))
+            self.flows.append(F)
+        # ---- generator
+        self.lin_w = float(W["dec.m_source.l_linear.weight"].reshape(-1)[0])
+        self.lin_b = float(W["dec.m_source.l_linear.bias"].reshape(-1)[0])
+        self.conv_pre = Conv(W["dec.conv_pre.weight"], W["dec.conv_pre.bias"], device=dev)
+        nup = len(self.ur)
+        self.chans = [self.uic // (2 ** (i + 1)) for i in range(nup)]
+        strides = [math.prod(self.ur[i + 1:]) if i + 1 < nup else 1 for i in range(nup)]
+        self.ups, self.noise, self.res = [], [], []
+        for i, (u, k) in enumerate(zip(self.ur, self.uks)):
+            if u % 2:
+                raise NotImplementedError("odd upsample rates (output_padding) are not used by any shipped config")
+            self.ups.append(ConvT(W[f"dec.ups.{i}.weight"], W[f"dec.ups.{i}.bias"], u, (k - u) // 2, device=dev))
+            s = strides[i]
+            kn = 1 if s == 1 else s * 2 - s % 2
+            self.noise.append((Conv(W[f"dec.noise_convs.{i}.weight"], W[f"dec.noise_convs.{i}.bias"], device=dev), s,
+                               0 if s == 1 else (kn - s) // 2))
+            blocks = []
+            for j, (kk, ds) in enumerate(zip(self.rks, self.rds)):
+                rb = f"dec.resblocks.{i * len(self.rks) + j}."
+                blocks.append((kk, [(d, Conv(W[rb + f"convs1.{m}.weight"], W[rb + f"convs1.{m}.bias"], device=dev),
+                                     Conv(W[rb + f"convs2.{m}.weight"], W[rb + f"convs2.{m}.bias"], device=dev))
+                                    for m, d in enumerate(ds)]))
+            self.res.append(blocks)
+        self.conv_post = Conv(W["dec.conv_post.weight"], None, device=dev)
+
+    # ------------------------------------------------------------------ stages
+    def text_encoder(self, phone_cf, pitch, T):
+        """TextEncoder.forward (synthesizers.py:366-371) on phone [E][T] -> stats [2*inter][T]."""
+        H, dev = self.hidden, phone_cf.device
+        lin = self.emb_phone(phone_cf)
+        x = torch.empty(H, T, device=dev)
+        ops.textenc_embed(lin, self.emb_pitch if pitch is not None else None, pitch, x, 1, H, T, math.sqrt(H), 0.1)
+        tmp = torch.empty(H, T, device=dev)
+        o = torch.empty(H, T, device=dev)
+        ml = torch.empty(self.n_heads, 2, T, device=dev)
+        kc = self.kc
+        scale = 1.0 / math.sqrt(kc)
+        for L in self.layers:
+            qkv = L["qkv"](x)
+            rk = L["relk"](qkv, B=self.n_heads, Lin=T, x_bstride=kc * T, Lout=T, out_scale=scale)
+            ops.attention(qkv, qkv[H:], qkv[2 * H:], o, B=1, H=self.n_heads, D=kc, T=T, ldc=T, q_hs=kc * T,
+                          k_hs=kc * T, v_hs=kc * T, o_hs=kc * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10)
+            y = L["o"](o, out=tmp)
+            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, 1, H, T)
+            h = L["ffn1"](x, pad=(self.ksz - 1) // 2, out_act=ACT_RELU)
+            y = L["ffn2"](h, pad=(self.ksz - 1) // 2, out=tmp)
+            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, 1, H, T)
+        return self.proj(x)
+
+    def flow_reverse(self, z_p, gc, T):
+        """ResidualCouplingBlock reverse (residuals.py:87-95, 127-137) + WaveNet (modules.py:35-51)."""
+        H, half, dev = self.hidden, self.inter // 2, z_p.device
+        x = z_p
+        bufs = (torch.empty_like(z_p), torch.empty_like(z_p))
+        h = torch.empty(H, T, device=dev)
+        acts = torch.empty(H, T, device=dev)
+        out_acc = torch.empty(H, T, device=dev)
+        for f in reversed(range(4)):
+            F = self.flows[f]
+            xf = bufs[0] if x is not bufs[0] else bufs[1]
+            ops.flip_channels(x, xf, 1, self.inter, T)
+            x0, x1 = xf[:half], xf[half:]
+            F["pre"](x0, out=h)
+            for l in range(3):
+                g_l = gc[f * 6 * H + l * 2 * H: f * 6 * H + (l + 1) * 2 * H]
+                xin = F["ins"][l](h, pad=2, bias2=g_l)
+                ops.gate(xin, acts, 1, H, T)
+                if l < 2:
+                    F["rs_a"][l](acts, out=h, res=h)
+                    F["rs_b"][l](acts, out=out_acc, accumulate=(l > 0))
+                else:
+                    F["rs_b"][l](acts, out=out_acc, accumulate=True)
+            F["post"](out_acc, out=x1, res=x1, out_scale=-1.0)
+            x = xf
+        return x
+
+    def generator(self, z, nsff0, gdec, T, sine_noise):
+        """GeneratorNSF.forward (synthesizers.py:144-161)."""
+        dev = z.device
+        L = T * self.upp
+        har = torch.empty(L, device=dev)
+        work = torch.empty(T, device=dev)
+        ops.sine_source(nsff0, sine_noise, har, work, 1, T, self.upp, float(self.sr), self.lin_w, self.lin_b)
+        x = self.conv_pre(z, pad=3, bias2=gdec)
+        scale = 1.0
+        nk = len(self.rks)
+        for i in range(len(self.ur)):
+            up = self.ups[i]
+            y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale)
+            Li = y.shape[-1]
+            nc, s, pad = self.noise[i]
+            nc(har.view(1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True)
+            C = self.chans[i]
+            t1 = torch.empty(C, Li, device=dev)
+            xa = torch.empty(C, Li, device=dev)
+            xb = torch.empty(C, Li, device=dev)
+            xs = torch.empty(C, Li, device=dev)
+            for j, (kk, pairs) in enumerate(self.res[i]):
+                cur = y
+                for m, (d, c1, c2) in enumerate(pairs):
+                    c1(cur, pad=(kk * d - d) // 2, dil=d, out=t1, in_act=ACT_LRELU, in_slope=LRELU_SLOPE)
+                    if m == len(pairs) - 1:
+                        c2(t1, pad=(kk - 1) // 2, out=xs, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
+                           accumulate=(j > 0))
+                    else:
+                        nxt = xa if cur is not xa else xb
+                        c2(t1, pad=(kk - 1) // 2, out=nxt, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE)
+                        cur = nxt
+            del t1, xa, xb, y
+            x = xs
+            scale = 1.0 / nk
+        return self.conv_post(x, pad=3, in_act=ACT_LRELU, in_slope=0.01, in_scale=scale, out_act=ACT_TANH)
+
+    # ------------------------------------------------------------------ public API
+    def speaker_cond(self, sid: int):
+        g = self.emb_g[sid].view(self.gin, 1)
+        return self.cond(g).view(-1)
+
+    def infer_cf(self, phone_cf, pitch, nsff0, sid: int, z_noise=None, sine_noise=None, seed: int = 0):
+        """Channels-first core: phone [E][T], pitch int64 [T], nsff0 f32 [T] -> (o [T*upp], z, z_p, stats)."""
+        E, T = phone_cf.shape
+        dev = phone_cf.device
+        if E != self.emb_dim:
+            raise ValueError(f"phone dim {E} != model's {self.emb_dim}")
+        gc = self.speaker_cond(sid)
+        stats = self.text_encoder(phone_cf, pitch, T)
+        if z_noise is None:
+            z_noise = ops.randn(torch.empty(self.inter, T, device=dev), seed, 0)
+        z_p = torch.empty(self.inter, T, device=dev)
+        ops.prior_sample(stats, z_noise.reshape(self.inter, T), z_p, 1, self.inter, T, 0.66666)
+        z = self.flow_reverse(z_p, gc, T)
+        if sine_noise is None:
+            sine_noise = ops.randn(torch.empty(T * self.upp, device=dev), seed, 1 << 40)
+        o = self.generator(z, nsff0.reshape(T).float().contiguous(), gc[4 * 6 * self.hidden:], T,
+                           sine_noise.reshape(T * self.upp))
+        return o.view(-1), z, z_p, stats
+
+    def infer(self, phone, phone_lengths, pitch=None, nsff0=None, sid=None, rate=None, z_noise=None,
+              sine_noise=None, seed: int = 0):
+        """Synthesizer.infer signature (synthesizers.py:446): phone [1, T, E] -> (o [1,1,L], x_mask, (z, z_p, m_p, logs_p)).
+
+        z_noise [1, inter, T] / sine_noise [1, T*upp, 1] inject the reference's randn_like draws
+        (parity mode); None draws them on the device (Philox, ``seed``)."""
+        if rate is not None:
+            raise NotImplementedError("rate (partial inference) is not used by VC.pipeline")
+        if pitch is None or nsff0 is None:
+            raise NotImplementedError("only f0 (NSF) models are on the hot path")
+        B, T, E = phone.shape
+        if B != 1:
+            raise NotImplementedError("batch 1 (as VC.voice_conversion calls it)")
+        if int(phone_lengths.reshape(-1)[0]) != T:
+            raise NotImplementedError("phone_lengths must equal the phone length (always true in VC.pipeline)")
+        dev = phone.device
+        phone_cf = torch.empty(E, T, device=dev)
+        ops.transpose(phone.contiguous().float(), phone_cf, 1, T, E)
+        sid_i = int(sid.reshape(-1)[0]) if torch.is_tensor(sid) else int(sid)
+        o, z, z_p, stats = self.infer_cf(phone_cf, pitch.reshape(T).to(torch.int64).contiguous(), nsff0, sid_i,
+                                         z_noise, sine_noise, seed)
+        m_p, logs_p = stats[: self.inter], stats[self.inter:]
+        x_mask = torch.ones(1, 1, T, device=dev)
+        return o.view(1, 1, -1), x_mask, (z.unsqueeze(0), z_p.unsqueeze(0), m_p.unsqueeze(0), logs_p.unsqueeze(0))

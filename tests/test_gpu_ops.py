@@ -1,0 +1,184 @@
+"""Op-level parity of the HIP kernels (through the C ABI) against torch-CPU fp32 references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def close(a, b, rtol=2e-5, atol=2e-5):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item()
+    assert err <= atol + rtol * scale, f"max err {err} (scale {scale})"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from rvc_amd import ops as o
+    o._lib.load()
+    return o
+
+
+CONV_CASES = [
+    # Ci, Co, K, stride, dil, pad, groups, L
+    (32, 32, 3, 1, 1, 1, 1, 5000),
+    (32, 32, 11, 1, 5, 25, 1, 3000),
+    (64, 64, 7, 1, 3, 9, 1, 2000),
+    (128, 128, 3, 1, 1, 1, 1, 1500),
+    (192, 768, 3, 1, 1, 1, 1, 700),
+    (768, 192, 3, 1, 1, 1, 1, 700),
+    (1, 256, 80, 40, 1, 20, 1, 40 * 50),
+    (1, 512, 10, 5, 1, 0, 1, 4000),
+    (512, 512, 3, 2, 1, 0, 1, 1200),
+    (512, 512, 2, 2, 1, 0, 1, 800),
+    (768, 768, 128, 1, 1, 64, 16, 300),
+    (32, 1, 7, 1, 1, 3, 1, 3000),
+    (192, 21, 1, 1, 1, 0, 1, 500),
+    (256, 4608, 1, 1, 1, 0, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv1d(ops, case):
+    Ci, Co, K, s, d, p, g, L = case
+    x = torch.randn(Ci, L, generator=gen(1))
+    w = torch.randn(Co, Ci // g, K, generator=gen(2)) / math.sqrt(Ci // g * K)
+    b = torch.randn(Co, generator=gen(3))
+    ref = F.conv1d(x.unsqueeze(0), w, b, s, p, d, g)[0]
+    c = ops.Conv(w, b, groups=g)
+    y = c(x.to(DEV), stride=s, pad=p, dil=d)
+    close(y, ref)
+
+
+def test_conv1d_fused_epilogue(ops):
+    Ci, Co, K, L = 64, 64, 5, 3000
+    x = torch.randn(Ci, L, generator=gen(4))
+    w = torch.randn(Co, Ci, K, generator=gen(5)) / math.sqrt(Ci * K)
+    b = torch.randn(Co, generator=gen(6))
+    b2 = torch.randn(Co, generator=gen(7))
+    res = torch.randn(Co, L, generator=gen(8))
+    acc0 = torch.randn(Co, L, generator=gen(9))
+    pre = F.leaky_relu(x * (1 / 3), 0.1)
+    ref = acc0 + (torch.tanh(F.conv1d(pre.unsqueeze(0), w, b, 1, 2)[0] + b2[:, None]) * -1.0 + res)
+    c = ops.Conv(w, b)
+    y = acc0.to(DEV)
+    c(x.to(DEV), pad=2, bias2=b2.to(DEV), res=res.to(DEV), out=y, accumulate=True, in_act=ops.ACT_LRELU,
+      in_slope=0.1, in_scale=1 / 3, out_act=ops.ACT_TANH, out_scale=-1.0)
+    close(y, ref)
+
+
+@pytest.mark.parametrize("u,k,ci,co,L", [(12, 24, 64, 32, 300), (10, 20, 64, 32, 300), (10, 16, 64, 32, 200),
+                                          (2, 4, 32, 16, 2000), (8, 16, 64, 32, 100)])
+def test_conv_transpose(ops, u, k, ci, co, L):
+    x = torch.randn(ci, L, generator=gen(10))
+    w = torch.randn(ci, co, k, generator=gen(11)) / math.sqrt(ci * k / u)
+    b = torch.randn(co, generator=gen(12))
+    p = (k - u) // 2
+    ref = F.conv_transpose1d(F.leaky_relu(x, 0.1).unsqueeze(0), w, b, u, p)[0]
+    c = ops.ConvT(w, b, u, p)
+    y = c(x.to(DEV), in_act=ops.ACT_LRELU, in_slope=0.1)
+    close(y, ref)
+
+
+@pytest.mark.parametrize("H,D,T", [(12, 64, 333), (12, 64, 1600), (2, 96, 257)])
+def test_attention_plain(ops, H, D, T):
+    q = torch.randn(H * D, T, generator=gen(20))
+    k = torch.randn(H * D, T, generator=gen(21))
+    v = torch.randn(H * D, T, generator=gen(22))
+    scale = D ** -0.5
+    qh = q.view(H, D, T).transpose(1, 2) * scale
+    kh = k.view(H, D, T).transpose(1, 2)
+    vh = v.view(H, D, T).transpose(1, 2)
+    ref = torch.softmax(qh @ kh.transpose(1, 2), -1) @ vh  # [H, T, D]
+    ref = ref.transpose(1, 2).reshape(H * D, T)
+    o = torch.empty(H * D, T, device=DEV)
+    ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), o, B=1, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T,
+                  v_hs=D * T, o_hs=D * T, scale=scale)
+    close(o, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_attention_relpos_band(ops):
+    """TextEncoder rel-pos MHA vs the oracle's restatement (synthesizers.py:227-251)."""
+    from oracle import synth as osy
+    H, D, T = 2, 96, 300
+    C = H * D
+    W = {}
+    g = gen(30)
+    x = torch.randn(1, C, T, generator=g)
+    for n in ("q", "k", "v", "o"):
+        W[f"a.conv_{n}.weight"] = torch.randn(C, C, 1, generator=g) / math.sqrt(C)
+        W[f"a.conv_{n}.bias"] = torch.randn(C, generator=g) * 0.1
+    W["a.emb_rel_k"] = torch.randn(1, 21, D, generator=g) * D ** -0.5
+    W["a.emb_rel_v"] = torch.randn(1, 21, D, generator=g) * D ** -0.5
+    mask = torch.ones(1, 1, T, T)
+    ref = osy._mha(W, "a.", x, mask, H)[0]
+    wqkv = torch.cat([W["a.conv_q.weight"], W["a.conv_k.weight"], W["a.conv_v.weight"]], 0)
+    bqkv = torch.cat([W["a.conv_q.bias"], W["a.conv_k.bias"], W["a.conv_v.bias"]], 0)
+    qkv = ops.Conv(wqkv, bqkv)(x[0].to(DEV))
+    scale = 1 / math.sqrt(D)
+    rk = ops.Conv(W["a.emb_rel_k"][0].unsqueeze(-1), None)(qkv, B=H, Lin=T, x_bstride=D * T, Lout=T, out_scale=scale)
+    o = torch.empty(C, T, device=DEV)
+    ml = torch.empty(H, 2, T, device=DEV)
+    ops.attention(qkv, qkv[C:], qkv[2 * C:], o, B=1, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
+                  o_hs=D * T, scale=scale, rk=rk, ev=W["a.emb_rel_v"][0].contiguous().to(DEV), ml=ml, W=10)
+    y = ops.Conv(W["a.conv_o.weight"], W["a.conv_o.bias"])(o)
+    close(y, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_layernorm_gate_flip_transpose(ops):
+    C, T = 192, 1000
+    x = torch.randn(C, T, generator=gen(40))
+    r = torch.randn(C, T, generator=gen(41))
+    gm = torch.rand(C, generator=gen(42)) + 0.5
+    bt = torch.randn(C, generator=gen(43))
+    ref = F.layer_norm((x + r).t(), (C,), gm, bt, 1e-5).t()
+    out = torch.empty(C, T, device=DEV)
+    ops.layernorm_cf(x.to(DEV), r.to(DEV), gm.to(DEV), bt.to(DEV), out, 1, C, T)
+    close(out, ref)
+    a = torch.randn(2 * C, T, generator=gen(44))
+    out = torch.empty(C, T, device=DEV)
+    ops.gate(a.to(DEV), out, 1, C, T)
+    close(out, torch.tanh(a[:C]) * torch.sigmoid(a[C:]))
+    out = torch.empty(C, T, device=DEV)
+    ops.flip_channels(x.to(DEV), out, 1, C, T)
+    close(out, torch.flip(x, [0]), 0, 0)
+    xt = torch.randn(777, 129, generator=gen(45))
+    out = torch.empty(129, 777, device=DEV)
+    ops.transpose(xt.to(DEV), out, 1, 777, 129)
+    close(out, xt.t(), 0, 0)
+
+
+@pytest.mark.parametrize("sr,upp,T", [(48000, 480, 400), (40000, 400, 2500), (32000, 320, 4100)])
+def test_sine_source_matches_oracle(ops, sr, upp, T):
+    from oracle import synth as osy
+    f0 = (torch.rand(1, T, generator=gen(50)) * 1200).float()
+    f0[:, torch.rand(T, generator=gen(51)) < 0.2] = 0
+    noise = torch.randn(1, T * upp, 1, generator=gen(52))
+    W = {"dec.m_source.l_linear.weight": torch.tensor([[0.9]]), "dec.m_source.l_linear.bias": torch.tensor([0.01])}
+    ref = osy.sine_source(W, f0, upp, sr, noise)[0, 0]
+    har = torch.empty(T * upp, device=DEV)
+    work = torch.empty(T, device=DEV)
+    ops.sine_source(f0.to(DEV), noise.to(DEV).view(-1), har, work, 1, T, upp, float(sr), 0.9, 0.01)
+    close(har, ref, rtol=0, atol=2e-5)
+
+
+def test_randn_moments(ops):
+    out = torch.empty(1 << 20, device=DEV)
+    ops.randn(out, seed=123)
+    x = out.cpu().double()
+    assert abs(x.mean().item()) < 5e-3 and abs(x.std().item() - 1) < 5e-3
+    out2 = torch.empty(1 << 20, device=DEV)
+    ops.randn(out2, seed=123)
+    assert torch.equal(out.cpu(), out2.cpu())
