@@ -1,0 +1,190 @@
+"""Bench: end-to-end VC (ContentVec + RMVPE + TextEncoder/flow/NSF-HiFiGAN), 48k v2, one 30 s clip
+per GPU per step (BASELINE.json configs[1]; N>1 = configs[3]-style utterance sharding with the
+output waveforms gathered to rank 0 over RCCL).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0 (contract in the task statement): metric/value = output
+audio-seconds per wall-second for the whole job, plus "roofline" for the dominant kernel
+family (the f32-MFMA implicit-GEMM conv engine, measured live with HIP events on its stream)
+and "cpu_baseline" (the torch-CPU oracle on a bounded clip, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "rvc-maker_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "audio-seconds/sec/GPU (xRT) end-to-end VC, 48k v2; 1/2/4/8 GPU scaling"
+PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
+
+
+def build_models(dev, sr=48000, version="v2", seed=1234):
+    from rvc_amd import synthetic
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD
+    net_g = SynthesizerAMD(synthetic.make_synth_ckpt(sr, version, seed=seed), dev)
+    hub = ContentVecAMD(synthetic.make_contentvec_ckpt(seed + 1), dev)
+    vc = VC(sr, Config(dev), rmvpe=RMVPEAMD(synthetic.rmvpe_state_dict(seed + 2), dev))
+    return vc, hub, net_g
+
+
+class ConvProbe:
+    """Wraps ops.conv1d during one instrumented step: HIP events around every launch on the launch
+    stream + the launch's algorithmic FLOPs (reference conv FLOPs)."""
+
+    def __init__(self):
+        from rvc_amd import ops
+        self.ops = ops
+        self.orig = ops.conv1d
+        self.rec = []
+
+    def __enter__(self):
+        def wrapped(*a, **k):
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            out = self.orig(*a, **k)
+            e1.record(s)
+            self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS))
+            return out
+        self.ops.conv1d = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        self.ops.conv1d = self.orig
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [e0.elapsed_time(e1) for e0, e1, _ in self.rec]
+        fl = [f for _, _, f in self.rec]
+        return len(ms), float(sum(ms)), float(sum(fl))
+
+
+def cpu_baseline(seconds=8.0):
+    """The torch-CPU oracle (a restatement of the reference's CPU path) on a bounded clip."""
+    from oracle import contentvec as ocv
+    from oracle import pipeline as opl
+    from oracle import rmvpe as orm
+    from oracle import synth as osy
+    from rvc_amd import melbasis, synthetic
+    seed = 1234
+    ck = synthetic.make_synth_ckpt(48000, "v2", seed=seed)
+    Ws, Wc = osy.load_weights(ck["weight"]), ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1))
+    Wr = orm.load_weights(synthetic.rmvpe_state_dict(seed + 2))
+    mb = torch.from_numpy(melbasis.mel_filterbank())
+    audio = synthetic.synthetic_audio(seconds, seed=1000)
+    g = torch.Generator().manual_seed(0)
+    noise = lambda s, k, sh: torch.randn(*sh, generator=g)  # noqa: E731
+    t0 = time.perf_counter()
+    out = opl.pipeline(Wc, Ws, Wr, mb, ck["config"], 0, audio, 0.0, "v2", 0.33, noise)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(out) / 48000 / dt, 4), "unit": "audio-s/s", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"{seconds:g} s clip, 48k v2, RMVPE, fp32, torch-CPU oracle (oracle/), "
+            f"wall {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seconds", type=float, default=30.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = f"cuda:{local}"
+    torch.cuda.set_device(local)
+
+    from rvc_amd import synthetic
+    vc, hub, net_g = build_models(dev)
+    audio = synthetic.synthetic_audio(args.seconds, seed=1000 + rank).astype(np.float64)
+    vc.seed = 17 + rank
+
+    def step():
+        out = vc.pipeline_device(hub, net_g, 0, audio, 0, "v2", 0.33)
+        if dist is not None:
+            # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
+            n = torch.tensor([out.numel()], device=dev, dtype=torch.int64)
+            sizes = [torch.zeros_like(n) for _ in range(world)]
+            dist.all_gather(sizes, n)
+            mx = int(max(int(s) for s in sizes))
+            buf = torch.zeros(mx, device=dev)
+            buf[: out.numel()] = out
+            gl = [torch.zeros(mx, device=dev) for _ in range(world)] if rank == 0 else None
+            dist.gather(buf, gl, dst=0)
+        return out
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    out_len = out.numel()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    audio_s = out_len / 48000.0
+    value = world * args.steps * audio_s / dt
+
+    roof = None
+    if rank == 0:
+        with ConvProbe() as probe:
+            step()
+        n, ms, flops = probe.summary()
+        achieved = flops / (ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+                "kernel": "conv1d_mfma_kernel<*> (implicit-GEMM conv engine, f32 MFMA)",
+                "launches_per_step": n, "avg_launch_ms": round(ms / n, 4),
+                "algorithmic_gflop_per_step": round(flops / 1e9, 1), "kernel_ms_per_step": round(ms, 3)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(value, 3), "unit": "audio-s/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic 16 kHz audio (SURVEY §8d generator), random-init weights of the true shapes",
+                "config": {"workload": f"VC.pipeline 48k v2, ContentVec-768, RMVPE f0, one {args.seconds:g} s clip "
+                                       "per GPU per step, no index, protect 0.33",
+                           "model": "RVC v2 48k (NSF-HiFiGAN) + ContentVec + RMVPE", "global_batch": world,
+                           "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",
+                           "output_seconds_per_clip": round(audio_s, 4)},
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -38,6 +38,7 @@ enum {
     RVC_ACT_TANH = 3,
     RVC_ACT_GELU = 4, /* exact erf GELU (torch.nn.GELU / F.gelu) */
     RVC_ACT_SIGMOID = 5,
+    RVC_ACT_LOGCLAMP = 6, /* log(max(v, slope))  (RMVPE.py:181) */
 };
 
 const char* rvc_last_error(void);
@@ -75,6 +76,11 @@ typedef struct rvc_conv1d_args {
     int nphase, ostride, ooffset;
     int in_act, out_act, accumulate, _pad0;
     float in_scale, in_slope, out_slope, out_scale;
+    /* 2-D mode (RMVPE 3x3 convs on zero-bordered [C][H+2][W+2] images flattened to L):
+       ntoff > 0 replaces tap*dil by toff[tap]; wrap > 0 skips stores to border cells
+       (t % wrap in {0, wrap-1}, or t / wrap in {0, Lout/wrap - 1}). */
+    int ntoff, wrap;
+    int toff[16];
 } rvc_conv1d_args;
 
 int rvc_conv1d(const rvc_conv1d_args* a, rvc_stream_t stream);
@@ -134,6 +140,40 @@ int rvc_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, rvc_stream_
  * f0 [B][T] -> har [B][T*upp]; noise [B][T*upp]; work: [B][T] floats scratch */
 int rvc_sine_source(const float* f0, const float* noise, float* har, float* work, int64_t B, int64_t T, int upp,
                     float sr, float lin_w, float lin_b, rvc_stream_t stream);
+
+/* ------------------------------------------------------------------ RMVPE (RMVPE.py)
+ * framesT[n][f] = x[reflect(f*hop + n - nfft/2)] * win[n]               RMVPE.py:168 (torch.stft center)
+ * mag[k][f] = |spec[k][f] + i spec[K+k][f]|                            RMVPE.py:169
+ * img (bordered [Tp+2][M+2]) = BN(mel^T), frames reflect-padded to Tp     RMVPE.py:64,144,213
+ * avgpool2 / interleave4 on bordered images                              RMVPE.py:35,93
+ * img_to_seq: [C][H][W] image -> [C*W][H] sequence                       RMVPE.py:144
+ * bigru: recurrence of nn.GRU(384, 256, bidirectional); gi = W_ih x + b_ih
+ *        [2][768][T], whh [2][768][256], bhh [2][768], y [512][T];
+ *        gran_ws: 8 KiB scratch (zeroed by the call), err: device int set on timeout
+ * rmvpe_decode: salience [360][ld] -> f0 (f64, optional), coarse (int64), pitchf (f32)
+ *        RMVPE.py:217-252 + convert.py:311-323, f64, numpy's reduction order
+ */
+int rvc_stft_frames(const float* x, const float* win, float* framesT, int64_t N, int64_t F, int nfft, int hop,
+                    rvc_stream_t stream);
+int rvc_spec_mag(const float* spec, float* mag, int64_t K, int64_t F, rvc_stream_t stream);
+int rvc_mel_image(const float* mel, float* img, int64_t M, int64_t F, int64_t Tp, float scale, float shift,
+                  rvc_stream_t stream);
+int rvc_avgpool2(const float* in, float* out, int64_t C, int64_t H, int64_t W, rvc_stream_t stream);
+int rvc_interleave4(const float* phases, float* out, int64_t C, int64_t H, int64_t W, rvc_stream_t stream);
+int rvc_img_to_seq(const float* img, float* x, int64_t C, int64_t H, int64_t W, rvc_stream_t stream);
+int rvc_bigru(const float* gi, const float* whh, const float* bhh, float* y, void* gran_ws, int* err, int64_t T,
+              rvc_stream_t stream);
+int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, double shift, double* f0, int64_t* coarse,
+                     float* pitchf, rvc_stream_t stream);
+
+/* ------------------------------------------------------------------ VC.pipeline glue
+ * phone_upsample: nearest x2 + protect blend (convert.py:361-378) -> phone [C][T]
+ * peak_normalize: x /= max|x|/0.99 when > 1 (convert.py:450-451); ws: 16 B scratch;
+ *                 scale_out (optional device float) receives max|x|/0.99
+ */
+int rvc_phone_upsample(const float* feats, const float* feats0, const float* pitchf, float* out, int64_t C, int64_t Tf,
+                       int64_t T, float protect, rvc_stream_t stream);
+int rvc_peak_normalize(float* x, int64_t n, void* ws, float* scale_out, rvc_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,8 @@ struct ConvParams {
     float in_scale, in_slope, out_slope, out_scale;
     int CK, KC, span, span_s;  // channels per chunk, padded k per chunk, staged row length / stride
     int mtiles_per_group;
+    int ntoff, wrap;
+    int toff[16];
 };
 
 template <int FM, int FN, int WM, int WN>
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
 
     for (int i = tid; i < p.KC; i += 256) {
         int c = i / p.K, t = i - c * p.K;
-        koff[i] = (i < kreal) ? c * p.span_s + t * p.dil : 0;
+        koff[i] = (i < kreal) ? c * p.span_s + (p.ntoff ? p.toff[t] : t * p.dil) : 0;
     }
 
     floatx4 acc[FM][FN];
@@ -141,6 +143,10 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
                 if (n >= p.ncols) continue;
                 const int64_t t = n * p.ostride + p.ooffset + phase;
                 if (t < 0 || t >= p.Lout) continue;
+                if (p.wrap) {
+                    const int64_t row = t / p.wrap, col = t - row * p.wrap;
+                    if (col == 0 || col == p.wrap - 1 || row == 0 || row == p.Lout / p.wrap - 1) continue;
+                }
                 float v = acc[i][j][r] + bs;
                 if (p.bias2) v += bs2;
                 v = act_apply(v, p.out_act, p.out_slope) * p.out_scale;
@@ -205,7 +211,19 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, rvc_stream_t stream) {
     p.nphase = a->nphase; p.ostride = a->ostride; p.ooffset = a->ooffset;
     p.in_act = a->in_act; p.out_act = a->out_act; p.accumulate = a->accumulate;
     p.in_scale = a->in_scale; p.in_slope = a->in_slope; p.out_slope = a->out_slope; p.out_scale = a->out_scale;
-    p.span = (BN - 1) * a->stride + (a->K - 1) * a->dil + 1;
+    int maxoff = (a->K - 1) * a->dil;
+    p.ntoff = a->ntoff;
+    p.wrap = a->wrap;
+    if (a->ntoff) {
+        RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
+        maxoff = 0;
+        for (int i = 0; i < a->K; ++i) {
+            RVC_CHECK_ARG(a->toff[i] >= 0, "conv1d: negative tap offset");
+            p.toff[i] = a->toff[i];
+            if (a->toff[i] > maxoff) maxoff = a->toff[i];
+        }
+    }
+    p.span = (BN - 1) * a->stride + maxoff + 1;
     p.span_s = p.span + 1;
     const int Cig = (int)(a->Ci / a->groups);
     // channels per chunk: aim for KC <= 128 and <= 56 KiB of LDS

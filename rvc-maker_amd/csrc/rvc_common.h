@@ -23,6 +23,7 @@ RVC_DEV float act_apply(float v, int act, float slope) {
         case RVC_ACT_TANH: return tanhf(v);
         case RVC_ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
         case RVC_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+        case RVC_ACT_LOGCLAMP: return logf(fmaxf(v, slope));
         default: return v;
     }
 }

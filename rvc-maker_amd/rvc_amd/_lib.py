@@ -8,11 +8,11 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_float, c_int, c_int64, c_uint64, c_void_p
+from ctypes import POINTER, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "librvc_amd.so")
 
-ACT_NONE, ACT_LRELU, ACT_RELU, ACT_TANH, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_LRELU, ACT_RELU, ACT_TANH, ACT_GELU, ACT_SIGMOID, ACT_LOGCLAMP = 0, 1, 2, 3, 4, 5, 6
 
 
 class Conv1dArgs(ctypes.Structure):
@@ -24,7 +24,8 @@ class Conv1dArgs(ctypes.Structure):
                 ("K", c_int), ("stride", c_int), ("dil", c_int), ("pad", c_int), ("groups", c_int),
                 ("nphase", c_int), ("ostride", c_int), ("ooffset", c_int),
                 ("in_act", c_int), ("out_act", c_int), ("accumulate", c_int), ("_pad0", c_int),
-                ("in_scale", c_float), ("in_slope", c_float), ("out_slope", c_float), ("out_scale", c_float)]
+                ("in_scale", c_float), ("in_slope", c_float), ("out_slope", c_float), ("out_scale", c_float),
+                ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -54,6 +55,16 @@ SIGNATURES = {
     "rvc_randn": [c_void_p, c_int64, c_uint64, c_uint64, c_void_p],
     "rvc_sine_source": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_float, c_float, c_float,
                         c_void_p],
+    "rvc_stft_frames": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p],
+    "rvc_spec_mag": [c_void_p, c_void_p, c_int64, c_int64, c_void_p],
+    "rvc_mel_image": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float, c_void_p],
+    "rvc_avgpool2": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_interleave4": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_img_to_seq": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_bigru": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p],
+    "rvc_phone_upsample": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
+    "rvc_peak_normalize": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p}
 

@@ -11,7 +11,7 @@ import math
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, check  # noqa: F401
+from ._lib import ACT_GELU, ACT_LOGCLAMP, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH, check  # noqa: F401
 
 
 def _stream():
@@ -83,7 +83,11 @@ class ConvT:
         Lout = self.out_len(Lin)
         ncols = (Lout - 1 + self.pad) // self.u + 1
         return conv1d(x, self.w, Ci, self.Co, self.T, bias=self.b, stride=1, pad=self.T - 1, dil=1, Lout=Lout,
-                      ncols=ncols, nphase=self.u, ostride=self.u, ooffset=-self.pad, out=out, **kw)
+                      ncols=ncols, nphase=self.u, ostride=self.u, ooffset=-self.pad, out=out,
+                      flops=2.0 * B * Ci * self.Co * self.K * Lin, **kw)
+
+
+LAST_CONV_FLOPS = 0.0
 
 
 def _shape3(x):
@@ -95,8 +99,12 @@ def _shape3(x):
 def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, groups=1, Lout=None, ncols=0,
            nphase=1, ostride=1, ooffset=0, out=None, res=None, in_act=ACT_NONE, in_slope=0.0, in_scale=1.0,
            out_act=ACT_NONE, out_slope=0.0, out_scale=1.0, accumulate=False, B=None, Lin=None, x_bstride=0,
-           w_bstride=0, y_bstride=0, res_bstride=0):
-    """y = conv(pre(x)) with fused epilogue.  x: [B][Ci][Lin] device f32 (t contiguous)."""
+           w_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, flops=None):
+    """y = conv(pre(x)) with fused epilogue.  x: [B][Ci][Lin] device f32 (t contiguous).
+
+    ``flops`` is the launch's ALGORITHMIC FLOP count for roofline accounting (recorded in
+    LAST_CONV_FLOPS); the default is 2*B*Co*(Ci/g)*K*(valid outputs)."""
+    global LAST_CONV_FLOPS
     if B is None:
         B, Cx, Lx = _shape3(x)
         if Lin is None:
@@ -130,6 +138,17 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
     a.nphase, a.ostride, a.ooffset = nphase, ostride, ooffset
     a.in_act, a.out_act, a.accumulate = in_act, out_act, int(bool(accumulate))
     a.in_scale, a.in_slope, a.out_slope, a.out_scale = in_scale, in_slope, out_slope, out_scale
+    if toff is not None:
+        if len(toff) != K or K > 16:
+            raise ValueError("conv1d: toff must have K <= 16 entries")
+        a.ntoff = K
+        for i, v in enumerate(toff):
+            a.toff[i] = int(v)
+    a.wrap = wrap
+    if flops is None:
+        valid = (Lout // wrap - 2) * (wrap - 2) if wrap else (ncols or Lout) * nphase
+        flops = 2.0 * B * Co * Cig * K * min(valid, Lout)
+    LAST_CONV_FLOPS = flops
     check(_lib.load().rvc_conv1d(ctypes.byref(a), _stream()), "conv1d")
     return out
 
@@ -199,6 +218,76 @@ def sine_source(f0, noise, har, work, B, T, upp, sr, lin_w, lin_b):
     check(_lib.load().rvc_sine_source(_p(f0), _p(noise), _p(har), _p(work), B, T, upp, sr, lin_w, lin_b, _stream()),
           "sine_source")
     return har
+
+
+def stft_frames(x, win, out, N, F, nfft, hop):
+    if x.numel() < N or win.numel() < nfft or out.numel() < nfft * F:
+        raise ValueError("stft_frames: size mismatch")
+    check(_lib.load().rvc_stft_frames(_p(x), _p(win), _p(out), N, F, nfft, hop, _stream()), "stft_frames")
+    return out
+
+
+def spec_mag(spec, mag, K, F):
+    if spec.numel() < 2 * K * F or mag.numel() < K * F:
+        raise ValueError("spec_mag: size mismatch")
+    check(_lib.load().rvc_spec_mag(_p(spec), _p(mag), K, F, _stream()), "spec_mag")
+    return mag
+
+
+def mel_image(mel, img, M, F, Tp, scale, shift):
+    if mel.numel() < M * F or img.numel() < (Tp + 2) * (M + 2):
+        raise ValueError("mel_image: size mismatch")
+    check(_lib.load().rvc_mel_image(_p(mel), _p(img), M, F, Tp, scale, shift, _stream()), "mel_image")
+    return img
+
+
+def avgpool2(x, out, C, H, W):
+    if x.numel() < C * (H + 2) * (W + 2) or out.numel() < C * (H // 2 + 2) * (W // 2 + 2):
+        raise ValueError("avgpool2: size mismatch")
+    check(_lib.load().rvc_avgpool2(_p(x), _p(out), C, H, W, _stream()), "avgpool2")
+    return out
+
+
+def interleave4(phases, out, C, H, W):
+    if phases.numel() < 4 * C * (H + 2) * (W + 2) or out.numel() < C * (2 * H + 2) * (2 * W + 2):
+        raise ValueError("interleave4: size mismatch")
+    check(_lib.load().rvc_interleave4(_p(phases), _p(out), C, H, W, _stream()), "interleave4")
+    return out
+
+
+def img_to_seq(img, x, C, H, W):
+    if img.numel() < C * (H + 2) * (W + 2) or x.numel() < C * W * H:
+        raise ValueError("img_to_seq: size mismatch")
+    check(_lib.load().rvc_img_to_seq(_p(img), _p(x), C, H, W, _stream()), "img_to_seq")
+    return x
+
+
+def bigru(gi, whh, bhh, y, gran, err, T):
+    if gi.numel() < 2 * 768 * T or whh.numel() < 2 * 768 * 256 or y.numel() < 512 * T or gran.numel() < 1024:
+        raise ValueError("bigru: size mismatch")
+    check(_lib.load().rvc_bigru(_p(gi), _p(whh), _p(bhh), _p(y), _p(gran), _p(err), T, _stream()), "bigru")
+    return y
+
+
+def rmvpe_decode(sal, ld, F, thred, shift, f0, coarse, pitchf):
+    if sal.numel() < 360 * ld or coarse.numel() < F or pitchf.numel() < F or (f0 is not None and f0.numel() < F):
+        raise ValueError("rmvpe_decode: size mismatch")
+    f0p = ctypes.c_void_p(f0.data_ptr()) if f0 is not None else None
+    check(_lib.load().rvc_rmvpe_decode(_p(sal), ld, F, thred, shift, f0p, _p(coarse), _p(pitchf), _stream()),
+          "rmvpe_decode")
+
+
+def phone_upsample(feats, feats0, pitchf, out, C, Tf, T, protect):
+    if feats.numel() < C * Tf or out.numel() < C * T or T > 2 * Tf or (pitchf is not None and pitchf.numel() < T):
+        raise ValueError("phone_upsample: size mismatch")
+    check(_lib.load().rvc_phone_upsample(_p(feats), _p(feats0), _p(pitchf), _p(out), C, Tf, T, protect, _stream()),
+          "phone_upsample")
+    return out
+
+
+def peak_normalize(x, ws, scale_out=None):
+    check(_lib.load().rvc_peak_normalize(_p(x), x.numel(), _p(ws), _p(scale_out), _stream()), "peak_normalize")
+    return x
 
 
 SQRT = math.sqrt

@@ -1,0 +1,158 @@
+"""MI355X ``VC`` -- drop-in for ``main/inference/convert.py:VC`` (:181-458).
+
+``VC(tgt_sr, config).pipeline(model, net_g, sid, audio, pitch, f0_method, file_index, index_rate,
+pitch_guidance, filter_radius, volume_envelope, version, protect, hop_length, f0_autotune,
+f0_autotune_strength, suffix, embed_suffix, f0_file=None, f0_onnx=False, pbar=None)`` keeps the
+reference signature and returns float32 numpy audio at tgt_sr.  ``model`` is a
+``ContentVecAMD`` (``.pt`` embedder), ``net_g`` a ``SynthesizerAMD`` (``.pth``); f0 is RMVPE
+(``self.rmvpe``, loaded once from ``assets/models/predictors/rmvpe.pt`` or injected).
+
+Host side (as the reference): scipy filtfilt (f64), the quiet-point segmentation for inputs
+> x_max, reflect padding.  Everything else runs on the device, in the order of
+convert.py:388-458; the segment loop keeps all tensors in HBM and only the final waveform
+is copied back.  ``pipeline_device`` is the HBM-resident form the bench times.
+
+Not on this path (raise): FAISS retrieval (index_rate > 0 with an index: §8(f) next row),
+f0 methods other than rmvpe, f0 files, autotune, volume_envelope != 1, ONNX models.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+from scipy import signal
+
+from . import contentvec as cvm
+from . import ops
+
+BH, AH = signal.butter(N=5, Wn=48, btype="high", fs=16000)  # convert.py:30
+
+
+class Config:
+    """The fields of main/configs/config.py:Config that VC reads (fp32 windows, config.py:83)."""
+
+    def __init__(self, device="cuda:0", is_half=False):
+        self.device = device
+        self.is_half = is_half
+        self.x_pad, self.x_query, self.x_center, self.x_max = (3, 10, 60, 65) if is_half else (1, 6, 38, 41)
+
+
+class VC:
+    def __init__(self, tgt_sr, config, rmvpe=None):
+        self.x_pad = config.x_pad
+        self.x_query = config.x_query
+        self.x_center = config.x_center
+        self.x_max = config.x_max
+        self.sample_rate = 16000
+        self.window = 160
+        self.t_pad = self.sample_rate * self.x_pad
+        self.t_pad_tgt = tgt_sr * self.x_pad
+        self.t_pad2 = self.t_pad * 2
+        self.t_query = self.sample_rate * self.x_query
+        self.t_center = self.sample_rate * self.x_center
+        self.t_max = self.sample_rate * self.x_max
+        self.f0_min, self.f0_max = 50, 1100
+        self.device = config.device
+        self.is_half = config.is_half
+        self.rmvpe = rmvpe
+        self.noise_fn = None  # parity hook: noise_fn(seg, "z"|"sine", shape) -> device tensor
+        self.seed = 0
+        self._ws = None
+
+    # ------------------------------------------------------------------ host-side pieces
+    def segment_points(self, audio: np.ndarray):
+        """convert.py:404-412."""
+        opt_ts = []
+        audio_pad = np.pad(audio, (self.window // 2, self.window // 2), mode="reflect")
+        if audio_pad.shape[0] > self.t_max:
+            audio_sum = np.zeros_like(audio)
+            for i in range(self.window):
+                audio_sum += audio_pad[i: i - self.window]
+            for t in range(self.t_center, audio.shape[0], self.t_center):
+                seg = np.abs(audio_sum[t - self.t_query: t + self.t_query])
+                opt_ts.append(t - self.t_query + np.where(seg == seg.min())[0][0])
+        return opt_ts
+
+    def _rmvpe(self):
+        if self.rmvpe is None:
+            from .rmvpe import RMVPEAMD
+            self.rmvpe = RMVPEAMD.from_file(os.path.join("assets", "models", "predictors", "rmvpe.pt"), self.device)
+        return self.rmvpe
+
+    # ------------------------------------------------------------------ device pieces
+    def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg):
+        """VC.voice_conversion (convert.py:328-386) on a device segment a0 [N] -> waveform [T*upp]."""
+        N = a0.numel()
+        feats = model.features_cf(a0, 9 if version == "v1" else 12)
+        if version == "v1":
+            feats = model.final_proj.conv(feats)
+        E, Tf = feats.shape
+        p_len = N // self.window
+        T = min(2 * Tf, p_len)  # convert.py:364-370
+        if 2 * Tf > p_len:
+            raise NotImplementedError("phone longer than p_len (x_mask padding) never occurs in VC.pipeline")
+        pitch, pitchf = pitch[:T], pitchf[:T]
+        if pitch.numel() < T:
+            raise ValueError("pitch shorter than the phone sequence")
+        phone = torch.empty(E, T, device=a0.device)
+        blend = protect < 0.5
+        ops.phone_upsample(feats, feats, pitchf if blend else None, phone, E, Tf, T, float(protect))
+        zn = self.noise_fn(seg, "z", (1, net_g.inter, T)) if self.noise_fn else None
+        sn = self.noise_fn(seg, "sine", (1, T * net_g.upp, 1)) if self.noise_fn else None
+        o, *_ = net_g.infer_cf(phone, pitch.contiguous(), pitchf.contiguous(), sid, zn, sn, self.seed + seg)
+        return o
+
+    def pipeline_device(self, model, net_g, sid, audio_f64: np.ndarray, pitch, version, protect):
+        """The hot path with the waveform left in HBM: returns a device f32 tensor at tgt_sr."""
+        audio = signal.filtfilt(BH, AH, audio_f64)
+        opt_ts = self.segment_points(audio)
+        audio_pad = np.pad(audio, (self.t_pad, self.t_pad), mode="reflect")
+        p_len = audio_pad.shape[0] // self.window
+        dev = self.device
+        xp = torch.from_numpy(audio_pad.astype(np.float32)).to(dev)
+        return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect)
+
+    def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect):
+        coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch))
+        coarse, pitchf = coarse[:p_len], pitchf[:p_len]
+        outs = []
+        s, t, seg = 0, None, 0
+        w, tp = self.window, self.t_pad_tgt
+        for t in opt_ts:
+            t = t // w * w
+            o = self.voice_conversion_device(model, net_g, sid, xp[s: t + self.t_pad2 + w],
+                                             coarse[s // w: (t + self.t_pad2) // w],
+                                             pitchf[s // w: (t + self.t_pad2) // w], version, protect, seg)
+            outs.append(o[tp: o.numel() - tp])
+            s = t
+            seg += 1
+        o = self.voice_conversion_device(model, net_g, sid, xp[t:] if t is not None else xp,
+                                         coarse[t // w:] if t is not None else coarse,
+                                         pitchf[t // w:] if t is not None else pitchf, version, protect, seg)
+        outs.append(o[tp: o.numel() - tp])
+        out = torch.cat(outs) if len(outs) > 1 else outs[0].contiguous()
+        if self._ws is None:
+            self._ws = torch.zeros(4, dtype=torch.int32, device=xp.device)
+        ops.peak_normalize(out, self._ws)
+        self._rmvpe().check_error() if os.environ.get("RVC_AMD_CHECK") else None
+        return out
+
+    # ------------------------------------------------------------------ reference signature
+    def pipeline(self, model, net_g, sid, audio, pitch, f0_method, file_index, index_rate, pitch_guidance,
+                 filter_radius, volume_envelope, version, protect, hop_length, f0_autotune, f0_autotune_strength,
+                 suffix, embed_suffix, f0_file=None, f0_onnx=False, pbar=None):
+        if f0_method != "rmvpe" or f0_onnx:
+            raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe is on the MI355X hot path")
+        if file_index and os.path.exists(file_index) and index_rate != 0:
+            raise NotImplementedError("FAISS retrieval is a SURVEY §8(f) next row, not built yet")
+        if not pitch_guidance or f0_autotune or volume_envelope != 1 or hasattr(f0_file, "name"):
+            raise NotImplementedError("only the default f0 path (no autotune / f0 file / volume envelope)")
+        if suffix != ".pth" or embed_suffix != ".pt":
+            raise NotImplementedError("ONNX / safetensors models are not on the MI355X path")
+        if pbar is not None:
+            pbar.update(1)
+        out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio), pitch, version, protect)
+        if pbar is not None:
+            pbar.update(3)
+        return out.cpu().numpy()

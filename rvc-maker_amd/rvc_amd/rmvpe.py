@@ -1,0 +1,227 @@
+"""MI355X RMVPE f0 estimator: drop-in for ``RMVPE(model_path, is_half, device).infer_from_audio``
+(main/library/predictors/RMVPE.py:183-226) as ``VC.get_f0_rmvpe`` uses it (convert.py:248-255).
+
+Loaded once from an ``E2E(4, 1, (2, 2))`` state dict (the reference reloads ``rmvpe.pt`` on
+every ``pipeline`` call, convert.py:251 -- this build keeps it resident).  BatchNorm is folded
+into the convolutions on the host at load.  On the device:
+
+  mel       stft_frames (reflect centre, Hann) -> DFT as a K=1 MFMA GEMM (1024 -> 2x513)
+            -> spec_mag -> mel GEMM (513 -> 128) with log(clamp 1e-5) fused
+  U-Net     images kept zero-bordered [C][H+2][W+2]; every 3x3 / 1x1 conv is the MFMA
+            implicit-GEMM engine in 2-D mode (tap offsets + border masking), ReLU and the
+            residual add fused; encoder skips are written straight into the decoder's concat
+            buffers; ConvTranspose2d = 4 phase convs + interleave4
+  head      cnn conv -> img_to_seq -> W_ih GEMM (both directions) -> bigru recurrence
+            -> Linear 512->360 + sigmoid -> f64 decode + coarse pitch (rmvpe_decode)
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import melbasis, ops
+from .ops import ACT_LOGCLAMP, ACT_RELU, ACT_SIGMOID, pack_km
+
+N_MELS, N_CLASS, NFFT, HOP = 128, 360, 1024, 160
+EPS = 1e-5
+
+
+def _fold_bn(sd, name):
+    g, b = sd[name + ".weight"].double(), sd[name + ".bias"].double()
+    m, v = sd[name + ".running_mean"].double(), sd[name + ".running_var"].double()
+    s = g / torch.sqrt(v + EPS)
+    return s, b - m * s
+
+
+class _Conv2d:
+    """3x3 (pad 1) or 1x1 conv on bordered images through the conv1d engine (2-D mode)."""
+
+    def __init__(self, w, b, device):
+        Co, Ci, kh, kw = w.shape
+        self.Co, self.Ci, self.k = Co, Ci, kh
+        self.w = pack_km(w.reshape(Co, Ci, kh * kw).float()).to(device)
+        self.b = b.float().to(device) if b is not None else None
+
+    def __call__(self, x, H, W, out, **kw):
+        wrap = W + 2
+        L = (H + 2) * wrap
+        if self.k == 3:
+            toff = [dy * wrap + dx for dy in range(3) for dx in range(3)]
+            pad = wrap + 1
+        else:
+            toff, pad = [0], 0
+        return ops.conv1d(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L, B=1,
+                          out=out, toff=toff, wrap=wrap, **kw)
+
+
+class _ConvT2d:
+    """ConvTranspose2d(Ci, Co, 3, stride 2, padding 1, output_padding 1) + folded BN + ReLU as 4 phase convs."""
+
+    # per output parity: list of (kernel index, source offset on the input grid)
+    TAPS = {0: [(1, 0)], 1: [(0, 1), (2, 0)]}
+
+    def __init__(self, w, scale, shift, device):
+        Ci, Co = w.shape[0], w.shape[1]
+        self.Ci, self.Co = Ci, Co
+        wf = w.double() * scale.view(1, Co, 1, 1)
+        self.bias = shift.float().to(device)
+        self.phases = []
+        for py in (0, 1):
+            for px in (0, 1):
+                taps = [(ky, kx, dy, dx) for ky, dy in self.TAPS[py] for kx, dx in self.TAPS[px]]
+                wp = torch.stack([wf[:, :, ky, kx].t() for ky, kx, _, _ in taps], dim=-1)  # [Co, Ci, ntap]
+                self.phases.append((pack_km(wp.float()).to(device), [(dy, dx) for _, _, dy, dx in taps]))
+
+    def __call__(self, x, H, W, out_cat):
+        """x bordered [Ci][H+2][W+2] -> first Co channels of bordered out_cat [*][2H+2][2W+2]."""
+        wrap = W + 2
+        L = (H + 2) * wrap
+        ph = torch.zeros(4, self.Co, H + 2, W + 2, device=x.device)
+        for i, (wp, taps) in enumerate(self.phases):
+            toff = [dy * wrap + dx for dy, dx in taps]
+            ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, B=1, out=ph[i],
+                       toff=toff, wrap=wrap, out_act=ACT_RELU)
+        ops.interleave4(ph, out_cat, self.Co, H, W)
+
+
+class RMVPEAMD:
+    def __init__(self, sd: dict, device: str = "cuda", n_blocks: int = 4):
+        dev = device
+        self.device = dev
+        self.nb = n_blocks
+        self.mel_basis = torch.from_numpy(melbasis.mel_filterbank(16000, NFFT, N_MELS, 30, 8000))
+        self.window = torch.hann_window(NFFT).to(dev)  # float32 periodic, as RMVPE.py:166
+        n = np.arange(NFFT)
+        k = np.arange(NFFT // 2 + 1)
+        ang = 2 * np.pi * np.outer(k, n) / NFFT
+        dft = np.concatenate([np.cos(ang), -np.sin(ang)], 0)  # [1026, 1024]
+        self.dft = ops.Conv(torch.from_numpy(dft).float().unsqueeze(-1), None, device=dev)
+        self.mel = ops.Conv(self.mel_basis.unsqueeze(-1), None, device=dev)
+        s, t = _fold_bn(sd, "unet.encoder.bn")
+        self.in_scale, self.in_shift = float(s[0]), float(t[0])
+
+        def cbr(p):
+            out = {}
+            for conv, bn in (("conv.0", "conv.1"), ("conv.3", "conv.4")):
+                sc, sh = _fold_bn(sd, f"{p}.{bn}")
+                w = sd[f"{p}.{conv}.weight"].double() * sc.view(-1, 1, 1, 1)
+                out[conv] = _Conv2d(w.float(), sh.float(), dev)
+            if f"{p}.shortcut.weight" in sd:
+                out["sc"] = _Conv2d(sd[f"{p}.shortcut.weight"].float(), sd[f"{p}.shortcut.bias"].float(), dev)
+            return out
+
+        self.enc = [[cbr(f"unet.encoder.layers.{l}.conv.{b}") for b in range(n_blocks)] for l in range(5)]
+        self.inter = [[cbr(f"unet.intermediate.layers.{l}.conv.{b}") for b in range(n_blocks)]
+                      for l in range(4)]
+        self.dec = []
+        for l in range(5):
+            p = f"unet.decoder.layers.{l}"
+            sc, sh = _fold_bn(sd, p + ".conv1.1")
+            self.dec.append((_ConvT2d(sd[p + ".conv1.0.weight"], sc, sh, dev),
+                             [cbr(f"{p}.conv2.{b}") for b in range(n_blocks)]))
+        self.cnn = _Conv2d(sd["cnn.weight"].float(), sd["cnn.bias"].float(), dev)
+        g = "fc.0.gru."
+        self.w_ih = ops.Conv(torch.cat([sd[g + "weight_ih_l0"], sd[g + "weight_ih_l0_reverse"]], 0).float().unsqueeze(-1),
+                             torch.cat([sd[g + "bias_ih_l0"], sd[g + "bias_ih_l0_reverse"]], 0).float(), device=dev)
+        self.w_hh = torch.stack([sd[g + "weight_hh_l0"], sd[g + "weight_hh_l0_reverse"]], 0).float().contiguous().to(dev)
+        self.b_hh = torch.stack([sd[g + "bias_hh_l0"], sd[g + "bias_hh_l0_reverse"]], 0).float().contiguous().to(dev)
+        self.fc = ops.Conv(sd["fc.1.weight"].float().unsqueeze(-1), sd["fc.1.bias"].float(), device=dev)
+        self.gran = torch.zeros(1024, dtype=torch.int64, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    @classmethod
+    def from_file(cls, path, device="cuda"):
+        return cls(torch.load(path, map_location="cpu", weights_only=True), device)
+
+    # ------------------------------------------------------------------ pieces
+    def mel_spectrogram(self, audio: torch.Tensor) -> torch.Tensor:
+        """MelSpectrogram.forward (RMVPE.py:162-181): audio [N] f32 -> log-mel [128][F]."""
+        N = audio.numel()
+        F = 1 + N // HOP
+        dev = audio.device
+        frames = torch.empty(NFFT, F, device=dev)
+        ops.stft_frames(audio, self.window, frames, N, F, NFFT, HOP)
+        # algorithmic count of the reference's FFT-based stft (5 N log2 N / 2 per real frame)
+        spec = self.dft(frames, flops=2.5 * NFFT * math.log2(NFFT) * F)
+        mag = torch.empty(NFFT // 2 + 1, F, device=dev)
+        ops.spec_mag(spec, mag, NFFT // 2 + 1, F)
+        return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
+
+    def _cbr(self, blk, x, H, W, out):
+        dev = x.device
+        Co = blk["conv.0"].Co
+        h = torch.zeros(Co, H + 2, W + 2, device=dev)
+        blk["conv.0"](x, H, W, h, out_act=ACT_RELU)
+        if "sc" in blk:
+            sc = torch.zeros(Co, H + 2, W + 2, device=dev)
+            blk["sc"](x, H, W, sc)
+            res = sc
+        else:
+            res = x
+        blk["conv.3"](h, H, W, out, out_act=ACT_RELU, res=res)
+        return out
+
+    def salience(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
+        """mel2hidden + E2E (RMVPE.py:210-215, 143-144): mel [128][F] -> salience [360][Tp] (Tp = F rounded up to 32)."""
+        dev = mel.device
+        F = mel.shape[-1]
+        Tp = 32 * ((F - 1) // 32 + 1)
+        H, W = Tp, N_MELS
+        x = torch.zeros(1, H + 2, W + 2, device=dev)
+        ops.mel_image(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
+        cats = []
+        C = 16
+        for l in range(5):
+            cat = torch.zeros(2 * C, H + 2, W + 2, device=dev)
+            for b, blk in enumerate(self.enc[l]):
+                out = cat[C:] if b == self.nb - 1 else torch.zeros(C, H + 2, W + 2, device=dev)
+                x = self._cbr(blk, x, H, W, out)
+            cats.append((cat, C, H, W))
+            pooled = torch.zeros(C, H // 2 + 2, W // 2 + 2, device=dev)
+            ops.avgpool2(x, pooled, C, H, W)
+            x, H, W = pooled, H // 2, W // 2
+            C *= 2
+        for layer in self.inter:
+            for blk in layer:
+                x = self._cbr(blk, x, H, W, torch.zeros(blk["conv.0"].Co, H + 2, W + 2, device=dev))
+        for i, (convt, blocks) in enumerate(self.dec):
+            cat, C, Ho, Wo = cats[-1 - i]
+            convt(x, H, W, cat)
+            x, H, W = cat, Ho, Wo
+            for blk in blocks:
+                x = self._cbr(blk, x, H, W, torch.zeros(blk["conv.0"].Co, H + 2, W + 2, device=dev))
+        img = torch.zeros(3, H + 2, W + 2, device=dev)
+        self.cnn(x, H, W, img)
+        seq = torch.empty(3 * W, H, device=dev)
+        ops.img_to_seq(img, seq, 3, H, W)
+        gi = self.w_ih(seq)  # [1536][Tp]
+        y = torch.empty(512, Tp, device=dev)
+        ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran, self.err, Tp)
+        return self.fc(y, out_act=ACT_SIGMOID), Tp
+
+    def f0_device(self, audio: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, want_f0=False):
+        """audio [N] f32 device -> (coarse int64 [F], pitchf f32 [F], f0 f64 [F] | None) on the device."""
+        mel = self.mel_spectrogram(audio)
+        F = mel.shape[-1]
+        sal, Tp = self.salience(mel)
+        dev = audio.device
+        coarse = torch.empty(F, dtype=torch.int64, device=dev)
+        pitchf = torch.empty(F, device=dev)
+        f0 = torch.empty(F, dtype=torch.float64, device=dev) if want_f0 else None
+        ops.rmvpe_decode(sal, Tp, F, thred, math.pow(2, pitch_shift / 12), f0, coarse, pitchf)
+        return coarse, pitchf, f0
+
+    def check_error(self):
+        if int(self.err.item()) != 0:
+            raise RuntimeError("rvc_amd: bigru recurrence timed out (granule hand-off stalled)")
+
+    # ------------------------------------------------------------------ reference API
+    def infer_from_audio(self, audio: np.ndarray, thred: float = 0.03) -> np.ndarray:
+        """RMVPE.infer_from_audio (RMVPE.py:223-226): f64 numpy [N] -> f64 numpy f0 [1 + N//160]."""
+        x = torch.from_numpy(np.asarray(audio)).float().to(self.device)
+        _, _, f0 = self.f0_device(x, thred, 0.0, want_f0=True)
+        out = f0.cpu().numpy()
+        self.check_error()
+        return out
