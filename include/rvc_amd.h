@@ -83,7 +83,10 @@ typedef struct rvc_conv1d_args {
     int toff[16];
 } rvc_conv1d_args;
 
-int rvc_conv1d(const rvc_conv1d_args* a, rvc_stream_t stream);
+/* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned
+ * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args). */
+int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a);
+int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ attention
  * Flash-style multi-head attention on f32 MFMA over channels-first Q/K/V
@@ -171,6 +174,12 @@ int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, doub
  * peak_normalize: x /= max|x|/0.99 when > 1 (convert.py:450-451); ws: 16 B scratch;
  *                 scale_out (optional device float) receives max|x|/0.99
  */
+/* filtfilt_pad: scipy.signal.filtfilt(b, a, x) (padtype odd, padlen 18; convert.py:403) in f64, then
+ *   reflect padding by tpad (convert.py:416): x f32 [N] -> out f32 [N + 2*tpad] (+ optional f64 copy).
+ *   b[6], a[6], zi[5] (= lfilter_zi) and Ac[25] (= A^chunk of the filter's state matrix) are HOST
+ *   arrays; work: device f64 [2*(N+36)]; chunk * 256 >= N + 36. */
+int rvc_filtfilt_pad(const float* x, int64_t N, const double* b, const double* a, const double* zi, const double* Ac,
+                     int64_t chunk, int64_t tpad, double* work, float* out, double* out64, rvc_stream_t stream);
 int rvc_phone_upsample(const float* feats, const float* feats0, const float* pitchf, float* out, int64_t C, int64_t Tf,
                        int64_t T, float protect, rvc_stream_t stream);
 int rvc_peak_normalize(float* x, int64_t n, void* ws, float* scale_out, rvc_stream_t stream);

@@ -148,34 +148,43 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnParams p) {
 }
 
 // out[c][q] += sum_{|j-q|<=W} softmax_p(q, j) * Ev[j-q+W][c]   (synthesizers.py:250, heads_share)
-// p recomputed from scale*Q.K + Rk with the forward's saved (max, sum).
-__global__ void attn_relv_band_kernel(AttnParams p, const float* ev, int D) {
+// p recomputed from scale*Q.K + Rk with the forward's saved (max, sum).  A block owns 32 queries:
+// phase 1 computes the 32 x (2W+1) band probabilities (one dot product per thread-slot) into LDS,
+// phase 2 applies them to Ev for the 32 x D outputs.
+__global__ __launch_bounds__(256) void attn_relv_band_kernel(AttnParams p, const float* ev, int D) {
+    constexpr int QB = 32;
+    __shared__ float pb[QB][32];
+    __shared__ float evs[31 * 96];
     const int h = blockIdx.y, b = blockIdx.z;
     const int64_t T = p.T;
-    const int64_t qa = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (qa >= T) return;
+    const int64_t q0 = (int64_t)blockIdx.x * QB;
+    const int tid = threadIdx.x;
+    const int nb = 2 * p.W + 1;
     const float* Q = p.q + b * p.q_bs + h * p.q_hs;
     const float* K = p.k + b * p.k_bs + h * p.k_hs;
-    const float* RK = p.rk + ((int64_t)b * p.H + h) * (2 * p.W + 1) * T;
+    const float* RK = p.rk + ((int64_t)b * p.H + h) * nb * T;
     const float* ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;
     float* O = p.o + b * p.o_bs + h * p.o_hs;
-    const float m = ML[qa], inv = 1.f / ML[T + qa];
-    float pr[32];
-    const int nb = 2 * p.W + 1;
-    for (int r = 0; r < nb; ++r) {
-        int64_t j = qa + r - p.W;
+    for (int i = tid; i < nb * D; i += 256) evs[i] = ev[i];
+    for (int i = tid; i < QB * nb; i += 256) {
+        const int qi = i % QB, r = i / QB;
+        const int64_t qa = q0 + qi, j = qa + r - p.W;
         float pv = 0.f;
-        if (j >= 0 && j < T) {
+        if (qa < T && j >= 0 && j < T) {
             float sc = 0.f;
             for (int c = 0; c < D; ++c) sc += (Q[(int64_t)c * p.ldc + qa] * p.scale) * K[(int64_t)c * p.ldc + j];
             sc += RK[(int64_t)r * T + qa];
-            pv = expf(sc - m) * inv;
+            pv = expf(sc - ML[qa]) / ML[T + qa];
         }
-        pr[r] = pv;
+        pb[qi][r] = pv;
     }
-    for (int c = 0; c < D; ++c) {
+    __syncthreads();
+    for (int i = tid; i < QB * D; i += 256) {
+        const int qi = i % QB, c = i / QB;
+        const int64_t qa = q0 + qi;
+        if (qa >= T) continue;
         float acc = 0.f;
-        for (int r = 0; r < nb; ++r) acc += pr[r] * ev[r * D + c];
+        for (int r = 0; r < nb; ++r) acc += pb[qi][r] * evs[r * D + c];
         O[(int64_t)c * p.ldc + qa] += acc;
     }
 }
@@ -186,6 +195,7 @@ extern "C" int rvc_attention(const rvc_attn_args* a, rvc_stream_t stream) {
     RVC_CHECK_ARG(a && a->q && a->k && a->v && a->o && a->T > 0 && a->H > 0 && a->B > 0, "attention: bad args");
     RVC_CHECK_ARG(a->D == 64 || a->D == 96, "attention: head dim %d unsupported (64, 96)", a->D);
     RVC_CHECK_ARG(!a->rk || (a->ml && a->W >= 0 && a->W <= 15), "attention: rel band needs ml and W <= 15");
+    RVC_CHECK_ARG(!a->ev || (a->rk && (2 * a->W + 1) * a->D <= 31 * 96), "attention: ev band too large");
     AttnParams p;
     p.q = a->q; p.k = a->k; p.v = a->v; p.o = a->o; p.rk = a->rk; p.ml = a->ml;
     p.T = a->T; p.ldc = a->ldc ? a->ldc : a->T;
@@ -198,8 +208,8 @@ extern "C" int rvc_attention(const rvc_attn_args* a, rvc_stream_t stream) {
     else hipLaunchKernelGGL(attn_fwd_kernel<96>, grid, dim3(256), 0, s, p);
     RVC_HIP(hipGetLastError());
     if (a->rk && a->ev) {
-        hipLaunchKernelGGL(attn_relv_band_kernel, dim3(cdiv(a->T, 64), (unsigned)a->H, (unsigned)a->B), dim3(64), 0, s,
-                           p, a->ev, a->D);
+        hipLaunchKernelGGL(attn_relv_band_kernel, dim3(cdiv(a->T, 32), (unsigned)a->H, (unsigned)a->B), dim3(256), 0,
+                           s, p, a->ev, a->D);
         RVC_HIP(hipGetLastError());
     }
     return RVC_OK;

@@ -1,18 +1,24 @@
-// Implicit-GEMM conv1d on f32 MFMA for gfx950.
+// Implicit-GEMM convolution engine on f32 MFMA for gfx950 (v_mfma_f32_16x16x4_f32).
 //
 // GEMM view per (batch, phase, group):  Y[m][n] = sum_k A[k][m] * B[k][n]
-//   m = output channel, n = output column, k = (input channel c, tap t) -> c*K + t
-//   A = packed weights (KM layout, k-major, m contiguous), B = im2col of x (never
-//   materialised: x rows are staged once per channel chunk into LDS with their halo,
-//   and B[k][n] is read at koff[k] + n*stride).
-// Block = 256 threads = 4 wave64s arranged WAVES_M x WAVES_N; each wave owns a
-// (16*FM) x (16*FN) output tile held in FM*FN MFMA accumulators (4 VGPRs each).
-// The input transform (scale + leaky-relu, i.e. the reference's F.leaky_relu in
-// front of every HiFiGAN conv) is applied once when the tile is staged, and the
-// epilogue fuses bias, activation, residual add and accumulate.
+//   m = output channel, n = output column, k = c*K + tap (flattened input channel x tap)
+//   A = packed weights (KM layout: k-major, m contiguous),
+//   B = im2col of x, never materialised: for each 32-deep k chunk the <= ceil(32/K)+1 input rows it
+//       touches are staged into LDS once with their halo (pre-activation applied on staging),
+//       and B[k][n] is read at koff[k] + n*stride.
+// Block = 256 threads = 4 wave64s (WM x WN); a wave owns a (16*FM) x (16*FN) tile in FM*FN
+// accumulators.  Chunks are software-pipelined through registers: chunk i+1's global loads are
+// issued before chunk i's MFMAs and written to LDS after them (one LDS buffer, two barriers).
+// Small grids split the k range over blockIdx.z (split-K); partial tiles go to a workspace and
+// conv_splitk_reduce applies the epilogue.  The epilogue fuses bias, a second bias (speaker
+// conditioning), activation, residual add, accumulate, polyphase/strided stores (ConvTranspose)
+// and border masking (2-D mode).
 #include "rvc_common.h"
 
 namespace {
+
+constexpr int KCH = 32;     // flattened k per chunk
+constexpr int NB_MAX = 16;  // staged B elements per thread (rows * span <= 256 * NB_MAX)
 
 struct ConvParams {
     const float* x;
@@ -21,51 +27,155 @@ struct ConvParams {
     const float* bias2;
     const float* res;
     float* y;
-    int64_t Ci, Co, Lin, Lout, ncols;
+    float* ws;  // split-K partials [ksplit][B*nphase][Co][ncols]
+    int64_t B, Ci, Co, Lin, Lout, ncols;
     int64_t x_bstride, y_bstride, res_bstride, w_bstride;
     int K, stride, dil, pad, groups;
     int nphase, ostride, ooffset;
     int in_act, out_act, accumulate;
     float in_scale, in_slope, out_slope, out_scale;
-    int CK, KC, span, span_s;  // channels per chunk, padded k per chunk, staged row length / stride
-    int mtiles_per_group;
+    int span, span_s, rows_max;
+    float inv_span;
+    int mtiles_per_group, ksplit, chunks_per_split, avec;
     int ntoff, wrap;
     int toff[16];
 };
+
+__device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
+
+__device__ __forceinline__ void epilogue_store(const ConvParams& p, float acc, int b, int phase, int64_t m, int64_t n) {
+    if (n >= p.ncols) return;
+    const int64_t t = n * p.ostride + p.ooffset + phase;
+    if (t < 0 || t >= p.Lout) return;
+    if (p.wrap) {
+        const int64_t row = t / p.wrap, col = t - row * p.wrap;
+        if (col == 0 || col == p.wrap - 1 || row == 0 || row == p.Lout / p.wrap - 1) return;
+    }
+    float v = acc;
+    if (p.bias) v += p.bias[m];
+    if (p.bias2) v += p.bias2[m];
+    v = act_apply(v, p.out_act, p.out_slope) * p.out_scale;
+    const int64_t o = m * p.Lout + t;
+    if (p.res) v += p.res[b * p.res_bstride + o];
+    float* yb = p.y + b * p.y_bstride;
+    if (p.accumulate) yb[o] += v;
+    else yb[o] = v;
+}
 
 template <int FM, int FN, int WM, int WN>
 __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
-    constexpr int WS = BM + 16;  // A row stride (== 16 mod 32 -> conflict-free 2-row reads)
+    constexpr int WS = (BM / 32) * 32 + 16 + ((BM % 32) ? 32 : 0);  // == 16 mod 32, >= BM
+    constexpr int NA = KCH * BM / 256;                                // A elements per thread
+    constexpr bool AVEC_OK = (NA % 4) == 0 && (BM % 4) == 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* Ws = smem;                          // [KC][WS]
-    float* Xs = smem + p.KC * WS;              // [CK][span_s]
-    int* koff = (int*)(Xs + p.CK * p.span_s);  // [KC]
+    float* Ws = smem;                     // [KCH][WS]
+    int* koff = (int*)(smem + KCH * WS);  // [KCH]
+    float* Xs = smem + KCH * WS + KCH;    // [rows_max][span_s]
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
-
-    const int zb = blockIdx.z;
-    const int b = zb / p.nphase;
+    int zb = blockIdx.z;
+    const int split = zb % p.ksplit;
+    zb /= p.ksplit;
     const int phase = zb % p.nphase;
+    const int b = zb / p.nphase;
     const int g = blockIdx.y / p.mtiles_per_group;
     const int Cog = (int)(p.Co / p.groups);
     const int Cig = (int)(p.Ci / p.groups);
-    const int m0g = (blockIdx.y % p.mtiles_per_group) * BM;  // within group
+    const int m0g = (blockIdx.y % p.mtiles_per_group) * BM;
     const int64_t n0 = (int64_t)blockIdx.x * BN;
 
     const float* xb = p.x + b * p.x_bstride + (int64_t)g * Cig * p.Lin;
     const float* wg = p.w + b * p.w_bstride + ((int64_t)phase * p.groups + g) * (int64_t)Cig * p.K * Cog;
     const int64_t base = n0 * p.stride - p.pad;
-    const int kreal = p.CK * p.K;
+    const int kmax = Cig * p.K;
+    const int nch = (kmax + KCH - 1) / KCH;
+    const int ch_beg = split * p.chunks_per_split;
+    const int ch_end = min(nch, ch_beg + p.chunks_per_split);
 
-    for (int i = tid; i < p.KC; i += 256) {
-        int c = i / p.K, t = i - c * p.K;
-        koff[i] = (i < kreal) ? c * p.span_s + (p.ntoff ? p.toff[t] : t * p.dil) : 0;
-    }
+    float ra[NA];
+    float rb[NB_MAX];
+
+    auto gload = [&](int ch) {
+        const int k0 = ch * KCH;
+        if (AVEC_OK && p.avec) {
+#pragma unroll
+            for (int i = 0; i < NA / 4; ++i) {
+                const int idx = tid + 256 * i;
+                const int kk = idx / (BM / 4);
+                const int m = (idx % (BM / 4)) * 4;
+                const int kr = k0 + kk;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (kr < kmax && m0g + m < Cog) v = *reinterpret_cast<const float4*>(wg + kr * Cog + m0g + m);
+                ra[4 * i] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int idx = tid + 256 * i;
+                const int kk = idx / BM, m = idx % BM;
+                const int kr = k0 + kk;
+                ra[i] = (kr < kmax && m0g + m < Cog) ? wg[kr * Cog + m0g + m] : 0.f;
+            }
+        }
+        const int c_lo = k0 / p.K;
+        const int c_hi = min((k0 + KCH - 1) / p.K, Cig - 1);
+        const int n = (c_hi - c_lo + 1) * p.span;
+#pragma unroll
+        for (int i = 0; i < NB_MAX; ++i) {
+            const int idx = tid + 256 * i;
+            float v = 0.f;
+            if (idx < n) {
+                int r = (int)((float)idx * p.inv_span);
+                if (r * p.span > idx) --r;
+                if ((r + 1) * p.span <= idx) ++r;
+                const int pos = (int)base + idx - r * p.span;
+                if (pos >= 0 && pos < p.Lin) {
+                    v = xb[(c_lo + r) * (int)p.Lin + pos] * p.in_scale;
+                    if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
+                }
+            }
+            rb[i] = v;
+        }
+    };
+    auto sstore = [&](int ch) {
+        const int k0 = ch * KCH;
+        if (AVEC_OK && p.avec) {
+#pragma unroll
+            for (int i = 0; i < NA / 4; ++i) {
+                const int idx = tid + 256 * i;
+                const int kk = idx / (BM / 4);
+                const int m = (idx % (BM / 4)) * 4;
+                *reinterpret_cast<float4*>(Ws + kk * WS + m) = make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NA; ++i) {
+                const int idx = tid + 256 * i;
+                Ws[(idx / BM) * WS + idx % BM] = ra[i];
+            }
+        }
+        const int c_lo = k0 / p.K;
+        const int c_hi = min((k0 + KCH - 1) / p.K, Cig - 1);
+        const int n = (c_hi - c_lo + 1) * p.span;
+#pragma unroll
+        for (int i = 0; i < NB_MAX; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < n) {
+                int r = (int)((float)idx * p.inv_span);
+                if (r * p.span > idx) --r;
+                if ((r + 1) * p.span <= idx) ++r;
+                Xs[r * p.span_s + (idx - r * p.span)] = rb[i];
+            }
+        }
+        if (tid < KCH) {
+            const int kk = k0 + tid;
+            const int c = kk / p.K, t = kk - c * p.K;
+            koff[tid] = (kk < kmax) ? (c - c_lo) * p.span_s + tap_off(p, t) : 0;
+        }
+    };
 
     floatx4 acc[FM][FN];
 #pragma unroll
@@ -73,90 +183,78 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    const int nchunks = (Cig + p.CK - 1) / p.CK;
-    for (int ch = 0; ch < nchunks; ++ch) {
-        const int c0 = ch * p.CK;
-        __syncthreads();
-        // stage A: Ws[kk][m] = Wt[(c0*K + kk)][m0g + m]
-        {
-            const int64_t krow0 = (int64_t)c0 * p.K;
-            const int64_t kmax = (int64_t)Cig * p.K;
-            for (int i = tid; i < p.KC * BM; i += 256) {
-                int kk = i / BM, m = i - kk * BM;
-                int64_t kr = krow0 + kk;
-                float v = 0.f;
-                if (kk < kreal && kr < kmax && m0g + m < Cog) v = wg[kr * Cog + m0g + m];
-                Ws[kk * WS + m] = v;
-            }
-        }
-        // stage B source rows: Xs[c][j] = pre(x[c0+c][base + j])
-        {
-            const int rows = p.CK;
-            for (int i = tid; i < rows * p.span; i += 256) {
-                int c = i / p.span, j = i - c * p.span;
-                int64_t pos = base + j;
-                float v = 0.f;
-                if (c0 + c < Cig && pos >= 0 && pos < p.Lin) {
-                    v = xb[(int64_t)(c0 + c) * p.Lin + pos] * p.in_scale;
-                    if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
-                }
-                Xs[c * p.span_s + j] = v;
-            }
-        }
-        __syncthreads();
-        const int lk = lane >> 4;
-        const int ln = lane & 15;
-        const float* wa = Ws + wm * (16 * FM) + ln;
-        const int nb = (wn * 16 * FN + ln) * p.stride;
-        for (int k0 = 0; k0 < p.KC; k0 += 4) {
-            const int kk = k0 + lk;
+    const int lk = lane >> 4, ln = lane & 15;
+    const float* wa = Ws + wm * (16 * FM) + ln;
+    const int nb = (wn * 16 * FN + ln) * p.stride;
+    const int jstep = 16 * p.stride;
+
+    if (ch_beg < ch_end) {
+        gload(ch_beg);
+        sstore(ch_beg);
+    }
+    __syncthreads();
+    for (int ch = ch_beg; ch < ch_end; ++ch) {
+        const bool more = ch + 1 < ch_end;
+        if (more) gload(ch + 1);
+#pragma unroll
+        for (int ks = 0; ks < KCH / 4; ++ks) {
+            const int kk = ks * 4 + lk;
             float a[FM], bv[FN];
 #pragma unroll
             for (int i = 0; i < FM; ++i) a[i] = wa[kk * WS + i * 16];
             const float* xr = Xs + koff[kk] + nb;
 #pragma unroll
-            for (int j = 0; j < FN; ++j) bv[j] = xr[j * 16 * p.stride];
+            for (int j = 0; j < FN; ++j) bv[j] = xr[j * jstep];
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(a[i], bv[j], acc[i][j]);
         }
+        __syncthreads();
+        if (more) sstore(ch + 1);
+        __syncthreads();
     }
 
-    // epilogue
-    const int ln = lane & 15;
     const int lr = (lane >> 4) * 4;
-    float* yb = p.y + b * p.y_bstride;
-    const float* rb = p.res ? p.res + b * p.res_bstride : nullptr;
+    if (p.ksplit > 1) {
+        float* wsb = p.ws + (((int64_t)split * p.B * p.nphase + (int64_t)b * p.nphase + phase) * p.Co) * p.ncols;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
+                if (mg >= Cog) continue;
+                const int64_t m = (int64_t)g * Cog + mg;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
+                    if (n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
             if (mg >= Cog) continue;
             const int64_t m = (int64_t)g * Cog + mg;
-            const float bs = p.bias ? p.bias[m] : 0.f;
-            const float bs2 = p.bias2 ? p.bias2[m] : 0.f;
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
-                if (n >= p.ncols) continue;
-                const int64_t t = n * p.ostride + p.ooffset + phase;
-                if (t < 0 || t >= p.Lout) continue;
-                if (p.wrap) {
-                    const int64_t row = t / p.wrap, col = t - row * p.wrap;
-                    if (col == 0 || col == p.wrap - 1 || row == 0 || row == p.Lout / p.wrap - 1) continue;
-                }
-                float v = acc[i][j][r] + bs;
-                if (p.bias2) v += bs2;
-                v = act_apply(v, p.out_act, p.out_slope) * p.out_scale;
-                const int64_t o = m * p.Lout + t;
-                if (rb) v += rb[o];
-                if (p.accumulate) yb[o] += v;
-                else yb[o] = v;
-            }
+            for (int j = 0; j < FN; ++j) epilogue_store(p, acc[i][j][r], b, phase, m, n0 + wn * 16 * FN + j * 16 + ln);
         }
-    }
+}
+
+__global__ void conv_splitk_reduce(ConvParams p) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t m = blockIdx.y;
+    const int bp = blockIdx.z;
+    if (n >= p.ncols) return;
+    const int64_t sstride = p.B * p.nphase * p.Co * p.ncols;
+    const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + n;
+    float s = 0.f;
+    for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
+    epilogue_store(p, s, bp / p.nphase, bp % p.nphase, m, n);
 }
 
 struct Cfg {
@@ -165,19 +263,11 @@ struct Cfg {
 
 template <int FM, int FN, int WM, int WN>
 hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv1d_mfma_kernel<FM, FN, WM, WN>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
     hipLaunchKernelGGL((conv1d_mfma_kernel<FM, FN, WM, WN>), grid, dim3(256), lds, s, p);
     return hipGetLastError();
 }
 
-}  // namespace
-
-extern "C" int rvc_conv1d(const rvc_conv1d_args* a, rvc_stream_t stream) {
+int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& lds) {
     RVC_CHECK_ARG(a && a->x && a->w && a->y, "conv1d: null pointer");
     RVC_CHECK_ARG(a->B > 0 && a->Ci > 0 && a->Co > 0 && a->K > 0 && a->Lin > 0 && a->Lout > 0,
                   "conv1d: bad sizes B=%lld Ci=%lld Co=%lld K=%d Lin=%lld Lout=%lld", (long long)a->B,
@@ -185,74 +275,118 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, rvc_stream_t stream) {
     RVC_CHECK_ARG(a->groups >= 1 && a->Ci % a->groups == 0 && a->Co % a->groups == 0, "conv1d: bad groups");
     RVC_CHECK_ARG(a->stride >= 1 && a->dil >= 1 && a->nphase >= 1 && a->ostride >= 1, "conv1d: bad stride/dil");
     const int64_t Cog = a->Co / a->groups;
+    const int64_t Cig = a->Ci / a->groups;
     const int64_t ncols = a->ncols > 0 ? a->ncols : a->Lout;
 
-    // tile config by output-channel count and column count
-    Cfg cfg;
-    if (Cog % 48 == 0 && Cog % 64 != 0) cfg = {3, 1, 1, 4};        // 48 x 64 (ContentVec pos_conv)
-    else if (Cog <= 16) cfg = {1, 4, 1, 4};                         // 16 x 256
-    else if (Cog <= 32) cfg = {2, 4, 1, 4};                         // 32 x 256
-    else if (Cog <= 64) cfg = {2, 4, 2, 2};                         // 64 x 128
-    else {
-        int64_t tiles128 = ((Cog + 127) / 128) * a->groups * ((ncols + 127) / 128) * a->B * a->nphase;
-        cfg = tiles128 >= 480 ? Cfg{4, 4, 2, 2} : Cfg{2, 2, 2, 2};  // 128x128 or 64x64
-    }
-    const int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
-    const int WS = BM + 16;
+    if (Cog % 48 == 0 && Cog % 64 != 0) cfg = {3, 1, 1, 4};  // 48 x 64 (ContentVec pos_conv groups)
+    else if (Cog <= 16) cfg = {1, 4, 1, 4};                  // 16 x 256
+    else if (Cog <= 32) cfg = {2, 4, 1, 4};                  // 32 x 256
+    else if (Cog <= 64) cfg = {2, 4, 2, 2};                  // 64 x 128
+    else cfg = {4, 4, 2, 2};                                 // 128 x 128
+    int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
 
-    ConvParams p;
-    p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y;
-    p.w_bstride = a->w_bstride;
-    p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout; p.ncols = ncols;
-    p.x_bstride = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
-    p.y_bstride = a->y_bstride ? a->y_bstride : a->Co * a->Lout;
-    p.res_bstride = a->res_bstride ? a->res_bstride : a->Co * a->Lout;
-    p.K = a->K; p.stride = a->stride; p.dil = a->dil; p.pad = a->pad; p.groups = a->groups;
-    p.nphase = a->nphase; p.ostride = a->ostride; p.ooffset = a->ooffset;
-    p.in_act = a->in_act; p.out_act = a->out_act; p.accumulate = a->accumulate;
-    p.in_scale = a->in_scale; p.in_slope = a->in_slope; p.out_slope = a->out_slope; p.out_scale = a->out_scale;
     int maxoff = (a->K - 1) * a->dil;
-    p.ntoff = a->ntoff;
-    p.wrap = a->wrap;
     if (a->ntoff) {
         RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
         maxoff = 0;
         for (int i = 0; i < a->K; ++i) {
             RVC_CHECK_ARG(a->toff[i] >= 0, "conv1d: negative tap offset");
-            p.toff[i] = a->toff[i];
             if (a->toff[i] > maxoff) maxoff = a->toff[i];
         }
     }
-    p.span = (BN - 1) * a->stride + maxoff + 1;
-    p.span_s = p.span + 1;
-    const int Cig = (int)(a->Ci / a->groups);
-    // channels per chunk: aim for KC <= 128 and <= 56 KiB of LDS
-    int ck = 128 / a->K;
-    if (ck < 1) ck = 1;
-    if (ck > Cig) ck = Cig;
-    for (;;) {
-        int kc = ((ck * a->K + 3) / 4) * 4;
-        size_t lds = (size_t)kc * WS * 4 + (size_t)ck * p.span_s * 4 + (size_t)kc * 4;
-        if (lds <= 56 * 1024 || ck == 1) break;
-        --ck;
+    // rows touched by a chunk of KCH consecutive k starting at a multiple of KCH
+    int rows_max = (KCH % a->K == 0) ? KCH / a->K : (KCH - 1) / a->K + 2;
+    if (rows_max > Cig) rows_max = (int)Cig;
+    int span = (BN - 1) * a->stride + maxoff + 1;
+    // keep the staged B tile within the per-thread register budget by narrowing the N tile
+    while ((int64_t)rows_max * span > 256 * NB_MAX && cfg.FN > 2) {
+        cfg.FN /= 2;
+        BN = 16 * cfg.FN * cfg.WN;
+        span = (BN - 1) * a->stride + maxoff + 1;
     }
-    p.CK = ck;
-    p.KC = ((ck * a->K + 3) / 4) * 4;
-    size_t lds = (size_t)p.KC * WS * 4 + (size_t)p.CK * p.span_s * 4 + (size_t)p.KC * 4;
-    RVC_CHECK_ARG(lds <= 160 * 1024, "conv1d: LDS %zu too large (K=%d dil=%d stride=%d)", lds, a->K, a->dil,
-                  a->stride);
-    p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
-    dim3 grid(cdiv(ncols, BN), (unsigned)(p.mtiles_per_group * a->groups), (unsigned)(a->B * a->nphase));
-    RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
+    RVC_CHECK_ARG((int64_t)rows_max * span <= 256 * NB_MAX, "conv1d: staged tile too large (rows %d x span %d)",
+                  rows_max, span);
 
+    p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y; p.ws = nullptr;
+    p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout; p.ncols = ncols;
+    p.x_bstride = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
+    p.y_bstride = a->y_bstride ? a->y_bstride : a->Co * a->Lout;
+    p.res_bstride = a->res_bstride ? a->res_bstride : a->Co * a->Lout;
+    p.w_bstride = a->w_bstride;
+    p.K = a->K; p.stride = a->stride; p.dil = a->dil; p.pad = a->pad; p.groups = a->groups;
+    p.nphase = a->nphase; p.ostride = a->ostride; p.ooffset = a->ooffset;
+    p.in_act = a->in_act; p.out_act = a->out_act; p.accumulate = a->accumulate;
+    p.in_scale = a->in_scale; p.in_slope = a->in_slope; p.out_slope = a->out_slope; p.out_scale = a->out_scale;
+    p.ntoff = a->ntoff; p.wrap = a->wrap;
+    for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff ? a->toff[i] : 0;
+    p.span = span;
+    p.span_s = span + 1;
+    p.rows_max = rows_max;
+    p.inv_span = 1.0f / (float)span;
+    p.avec = (Cog % 4 == 0) && (((uintptr_t)a->w & 15) == 0) && (a->w_bstride % 4 == 0);
+    p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
+
+    const int64_t tiles = (int64_t)p.mtiles_per_group * a->groups * ((ncols + BN - 1) / BN) * a->B * a->nphase;
+    const int nch = (int)((Cig * a->K + KCH - 1) / KCH);
+    int ks = 1;
+    if (tiles < 512 && nch >= 4) {
+        ks = (int)((512 + tiles - 1) / tiles);
+        if (ks > 16) ks = 16;
+        if (ks > nch / 2) ks = nch / 2;
+        if (ks < 1) ks = 1;
+    }
+    p.chunks_per_split = (nch + ks - 1) / ks;
+    ks = (nch + p.chunks_per_split - 1) / p.chunks_per_split;
+    p.ksplit = ks;
+    const int WS = (BM / 32) * 32 + 16 + ((BM % 32) ? 32 : 0);
+    lds = (size_t)(KCH * WS + KCH) * 4 + (size_t)rows_max * p.span_s * 4;
+    RVC_CHECK_ARG(lds <= 160 * 1024, "conv1d: LDS %zu too large", lds);
+    grid = dim3(cdiv(ncols, BN), (unsigned)(p.mtiles_per_group * a->groups), (unsigned)(a->B * a->nphase * ks));
+    RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
+    return RVC_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {
+    ConvParams p;
+    Cfg cfg;
+    dim3 grid;
+    size_t lds;
+    if (plan(a, p, cfg, grid, lds) != RVC_OK) return -1;
+    if (p.ksplit <= 1) return 0;
+    return (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+}
+
+extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
+    ConvParams p;
+    Cfg cfg;
+    dim3 grid;
+    size_t lds;
+    int rc = plan(a, p, cfg, grid, lds);
+    if (rc != RVC_OK) return rc;
+    if (p.ksplit > 1) {
+        const int64_t need = (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+        RVC_CHECK_ARG(ws && ws_bytes >= need, "conv1d: split-K needs %lld B of workspace (got %lld)",
+                      (long long)need, (long long)ws_bytes);
+        p.ws = (float*)ws;
+    }
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     if (cfg.FM == 3) e = launch<3, 1, 1, 4>(p, grid, lds, s);
-    else if (cfg.FM == 1) e = launch<1, 4, 1, 4>(p, grid, lds, s);
-    else if (cfg.WM == 1) e = launch<2, 4, 1, 4>(p, grid, lds, s);
-    else if (cfg.FM == 4) e = launch<4, 4, 2, 2>(p, grid, lds, s);
+    else if (cfg.FM == 1 && cfg.FN == 4) e = launch<1, 4, 1, 4>(p, grid, lds, s);
+    else if (cfg.FM == 1) e = launch<1, 2, 1, 4>(p, grid, lds, s);
+    else if (cfg.WM == 1 && cfg.FN == 4) e = launch<2, 4, 1, 4>(p, grid, lds, s);
+    else if (cfg.WM == 1) e = launch<2, 2, 1, 4>(p, grid, lds, s);
+    else if (cfg.FM == 4 && cfg.FN == 4) e = launch<4, 4, 2, 2>(p, grid, lds, s);
+    else if (cfg.FM == 4) e = launch<4, 2, 2, 2>(p, grid, lds, s);
     else if (cfg.FN == 4) e = launch<2, 4, 2, 2>(p, grid, lds, s);
     else e = launch<2, 2, 2, 2>(p, grid, lds, s);
     RVC_HIP(e);
+    if (p.ksplit > 1) {
+        hipLaunchKernelGGL(conv_splitk_reduce, dim3(cdiv(p.ncols, 256), (unsigned)p.Co, (unsigned)(p.B * p.nphase)),
+                           dim3(256), 0, s, p);
+        RVC_HIP(hipGetLastError());
+    }
     return RVC_OK;
 }

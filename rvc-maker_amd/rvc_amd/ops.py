@@ -88,6 +88,17 @@ class ConvT:
 
 
 LAST_CONV_FLOPS = 0.0
+_WS = {}
+
+
+def _workspace(device, nbytes):
+    """Per-device split-K scratch, grown on demand (stream-ordered reuse is safe: one stream)."""
+    key = str(device)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() * 4 < nbytes:
+        buf = torch.empty((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
+        _WS[key] = buf
+    return buf
 
 
 def _shape3(x):
@@ -149,7 +160,12 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
         valid = (Lout // wrap - 2) * (wrap - 2) if wrap else (ncols or Lout) * nphase
         flops = 2.0 * B * Co * Cig * K * min(valid, Lout)
     LAST_CONV_FLOPS = flops
-    check(_lib.load().rvc_conv1d(ctypes.byref(a), _stream()), "conv1d")
+    lib = _lib.load()
+    need = lib.rvc_conv1d_workspace_bytes(ctypes.byref(a))
+    if need < 0:
+        raise RuntimeError(f"rvc_amd: conv1d plan failed: {lib.rvc_last_error().decode()}")
+    ws = _workspace(out.device, need) if need else None
+    check(lib.rvc_conv1d(ctypes.byref(a), _p(ws), need, _stream()), "conv1d")
     return out
 
 

@@ -35,7 +35,7 @@ def test_struct_layouts_match_header():
 def test_errors_are_reported_without_gpu():
     lib = _lib.load()
     a = _lib.Conv1dArgs()  # all-null -> EINVAL, no device touched
-    rc = lib.rvc_conv1d(ctypes.byref(a), None)
+    rc = lib.rvc_conv1d(ctypes.byref(a), None, 0, None)
     assert rc == -22
     assert b"null" in lib.rvc_last_error()
     assert lib.rvc_version() >= 1
