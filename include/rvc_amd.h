@@ -176,10 +176,9 @@ int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, doub
  */
 /* filtfilt_pad: scipy.signal.filtfilt(b, a, x) (padtype odd, padlen 18; convert.py:403) in f64, then
  *   reflect padding by tpad (convert.py:416): x f32 [N] -> out f32 [N + 2*tpad] (+ optional f64 copy).
- *   b[6], a[6], zi[5] (= lfilter_zi) and Ac[25] (= A^chunk of the filter's state matrix) are HOST
- *   arrays; work: device f64 [2*(N+36)]; chunk * 256 >= N + 36. */
-int rvc_filtfilt_pad(const float* x, int64_t N, const double* b, const double* a, const double* zi, const double* Ac,
-                     int64_t chunk, int64_t tpad, double* work, float* out, double* out64, rvc_stream_t stream);
+ *   b[6], a[6], zi[5] (= lfilter_zi(b, a)) are HOST arrays; work: device f64 [2*(N+36)]. */
+int rvc_filtfilt_pad(const float* x, int64_t N, const double* b, const double* a, const double* zi, int64_t tpad,
+                     double* work, float* out, double* out64, rvc_stream_t stream);
 int rvc_phone_upsample(const float* feats, const float* feats0, const float* pitchf, float* out, int64_t C, int64_t Tf,
                        int64_t T, float protect, rvc_stream_t stream);
 int rvc_peak_normalize(float* x, int64_t n, void* ws, float* scale_out, rvc_stream_t stream);

@@ -43,23 +43,42 @@ struct ConvParams {
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
 
-__device__ __forceinline__ void epilogue_store(const ConvParams& p, float acc, int b, int phase, int64_t m, int64_t n) {
-    if (n >= p.ncols) return;
-    const int64_t t = n * p.ostride + p.ooffset + phase;
-    if (t < 0 || t >= p.Lout) return;
+// Output column n -> store position t (or -1 when the column is not stored: beyond ncols / Lout,
+// or a border cell in 2-D mode).  32-bit math: every per-batch extent here is < 2^31.
+__device__ __forceinline__ int out_pos(const ConvParams& p, int64_t n, int phase) {
+    if (n >= p.ncols) return -1;
+    const int t = (int)n * p.ostride + p.ooffset + phase;
+    if (t < 0 || t >= (int)p.Lout) return -1;
     if (p.wrap) {
-        const int64_t row = t / p.wrap, col = t - row * p.wrap;
-        if (col == 0 || col == p.wrap - 1 || row == 0 || row == p.Lout / p.wrap - 1) return;
+        const int row = t / p.wrap, col = t - row * p.wrap;
+        if (col == 0 || col == p.wrap - 1 || row == 0 || row == (int)p.Lout / p.wrap - 1) return -1;
     }
+    return t;
+}
+
+// Branch-free epilogue for one element: every load is issued unconditionally from a clamped
+// address (a per-element guarded load makes hipcc branch and wait vmcnt(0) per element).
+__device__ __forceinline__ void epilogue_store(const ConvParams& p, float acc, int b, int64_t m, int t) {
+    const bool ok = t >= 0;
+    const int64_t o = m * p.Lout + (ok ? t : 0);
     float v = acc;
     if (p.bias) v += p.bias[m];
     if (p.bias2) v += p.bias2[m];
     v = act_apply(v, p.out_act, p.out_slope) * p.out_scale;
-    const int64_t o = m * p.Lout + t;
     if (p.res) v += p.res[b * p.res_bstride + o];
     float* yb = p.y + b * p.y_bstride;
-    if (p.accumulate) yb[o] += v;
-    else yb[o] = v;
+    if (p.accumulate) v += yb[o];
+    if (ok) yb[o] = v;
+}
+
+template <int ACT, int FM, int FN>
+__device__ __forceinline__ void apply_act(floatx4 (&acc)[FM][FN], float slope, float scale) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] = act_apply(acc[i][j][r], ACT, slope) * scale;
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -97,7 +116,29 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
 
     float ra[NA];
     float rb[NB_MAX];
+    // Per-thread B staging slots are the same for every chunk: slot i covers idx = tid + 256 i of the
+    // rows x span tile, i.e. (row, col) = divmod(idx, span).  Precompute them once, packed as
+    // row << 16 | col, plus a bitmask of slots whose input position base + col lies inside [0, Lin).
+    int bslot[NB_MAX];
+    unsigned bcolok = 0;
+    {
+        const int lin = (int)p.Lin;
+#pragma unroll
+        for (int i = 0; i < NB_MAX; ++i) {
+            const int idx = tid + 256 * i;
+            int r = (int)((float)idx * p.inv_span);
+            r -= (r * p.span > idx);
+            r += ((r + 1) * p.span <= idx);
+            const int j = idx - r * p.span;
+            bslot[i] = (r << 16) | j;
+            const int pos = (int)base + j;
+            bcolok |= (unsigned)(pos >= 0 && pos < lin) << i;
+        }
+    }
 
+    // gload issues raw loads only (clamped addresses, no arithmetic on the results), so the loads of
+    // chunk i+1 stay in flight across chunk i's MFMAs; sstore masks, pre-activates and writes LDS.
+    // Any use of a loaded value inside gload would make hipcc wait for it right there.
     auto gload = [&](int ch) {
         const int k0 = ch * KCH;
         if (AVEC_OK && p.avec) {
@@ -107,8 +148,8 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
                 const int kk = idx / (BM / 4);
                 const int m = (idx % (BM / 4)) * 4;
                 const int kr = k0 + kk;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (kr < kmax && m0g + m < Cog) v = *reinterpret_cast<const float4*>(wg + kr * Cog + m0g + m);
+                const bool ok = kr < kmax && m0g + m < Cog;
+                const float4 v = *reinterpret_cast<const float4*>(wg + (ok ? kr * Cog + m0g + m : 0));
                 ra[4 * i] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
             }
         } else {
@@ -117,27 +158,27 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
                 const int idx = tid + 256 * i;
                 const int kk = idx / BM, m = idx % BM;
                 const int kr = k0 + kk;
-                ra[i] = (kr < kmax && m0g + m < Cog) ? wg[kr * Cog + m0g + m] : 0.f;
+                const bool ok = kr < kmax && m0g + m < Cog;
+                ra[i] = wg[ok ? kr * Cog + m0g + m : 0];
             }
         }
         const int c_lo = k0 / p.K;
         const int c_hi = min((k0 + KCH - 1) / p.K, Cig - 1);
-        const int n = (c_hi - c_lo + 1) * p.span;
+        const int rows = c_hi - c_lo + 1;
+        const int n = rows * p.span;
+        const int lin = (int)p.Lin;
+        const int rbase = c_lo * lin + (int)base;
+        // groups of 4 loads behind a block-uniform bound check: only the groups the tile needs are issued
 #pragma unroll
-        for (int i = 0; i < NB_MAX; ++i) {
-            const int idx = tid + 256 * i;
-            float v = 0.f;
-            if (idx < n) {
-                int r = (int)((float)idx * p.inv_span);
-                if (r * p.span > idx) --r;
-                if ((r + 1) * p.span <= idx) ++r;
-                const int pos = (int)base + idx - r * p.span;
-                if (pos >= 0 && pos < p.Lin) {
-                    v = xb[(c_lo + r) * (int)p.Lin + pos] * p.in_scale;
-                    if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
+        for (int gi = 0; gi < NB_MAX; gi += 4) {
+            if (gi * 256 < n) {
+#pragma unroll
+                for (int i = gi; i < gi + 4; ++i) {
+                    const int r = bslot[i] >> 16, j = bslot[i] & 0xffff;
+                    const bool ok = r < rows && ((bcolok >> i) & 1u);
+                    rb[i] = xb[ok ? rbase + r * lin + j : 0];
                 }
             }
-            rb[i] = v;
         }
     };
     auto sstore = [&](int ch) {
@@ -148,26 +189,35 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
                 const int idx = tid + 256 * i;
                 const int kk = idx / (BM / 4);
                 const int m = (idx % (BM / 4)) * 4;
-                *reinterpret_cast<float4*>(Ws + kk * WS + m) = make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+                const bool ok = k0 + kk < kmax && m0g + m < Cog;
+                *reinterpret_cast<float4*>(Ws + kk * WS + m) =
+                    ok ? make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         } else {
 #pragma unroll
             for (int i = 0; i < NA; ++i) {
                 const int idx = tid + 256 * i;
-                Ws[(idx / BM) * WS + idx % BM] = ra[i];
+                const int kk = idx / BM, m = idx % BM;
+                const bool ok = k0 + kk < kmax && m0g + m < Cog;
+                Ws[kk * WS + m] = ok ? ra[i] : 0.f;
             }
         }
         const int c_lo = k0 / p.K;
         const int c_hi = min((k0 + KCH - 1) / p.K, Cig - 1);
-        const int n = (c_hi - c_lo + 1) * p.span;
+        const int rows = c_hi - c_lo + 1;
+        const int n = rows * p.span;
+        const int dump = p.rows_max * p.span_s;  // scratch slot after the tile for idx >= n
 #pragma unroll
-        for (int i = 0; i < NB_MAX; ++i) {
-            const int idx = tid + 256 * i;
-            if (idx < n) {
-                int r = (int)((float)idx * p.inv_span);
-                if (r * p.span > idx) --r;
-                if ((r + 1) * p.span <= idx) ++r;
-                Xs[r * p.span_s + (idx - r * p.span)] = rb[i];
+        for (int gi = 0; gi < NB_MAX; gi += 4) {
+            if (gi * 256 < n) {
+#pragma unroll
+                for (int i = gi; i < gi + 4; ++i) {
+                    const int r = bslot[i] >> 16, j = bslot[i] & 0xffff;
+                    const bool ok = r < rows && ((bcolok >> i) & 1u);
+                    float v = rb[i] * p.in_scale;
+                    if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
+                    Xs[tid + 256 * i < n ? r * p.span_s + j : dump] = ok ? v : 0.f;
+                }
             }
         }
         if (tid < KCH) {
@@ -223,26 +273,69 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
-                if (mg >= Cog) continue;
                 const int64_t m = (int64_t)g * Cog + mg;
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
                     const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
-                    if (n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
+                    if (mg < Cog && n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
                 }
             }
         return;
     }
+    // Epilogue one row fragment (16 channels x BN/WN columns) at a time, in passes so that hipcc
+    // issues each class of loads together: bias + activation + scale in registers (activation
+    // dispatched once per kernel, not per element), residual loads, accumulate loads -- all from
+    // clamped addresses -- then masked stores.  Per-fragment (not whole-tile) passes bound the
+    // epilogue's live registers, which would otherwise set the whole kernel's occupancy.
+    int tcol[FN];  // store position per column fragment (shared by all rows)
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int j = 0; j < FN; ++j) tcol[j] = out_pos(p, n0 + wn * 16 * FN + j * 16 + ln, phase);
+    float* yb = p.y + b * p.y_bstride;
+    const float* rb2 = p.res ? p.res + b * p.res_bstride : nullptr;
+    const int Lo = (int)p.Lout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        floatx4 (&av)[1][FN] = *reinterpret_cast<floatx4 (*)[1][FN]>(&acc[i][0]);
+        int mrow[4];  // channel index (clamped); m * Lout < 2^31 is checked on the host
+        bool mok[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
-            if (mg >= Cog) continue;
-            const int64_t m = (int64_t)g * Cog + mg;
+            mok[r] = mg < Cog;
+            mrow[r] = g * Cog + (mg < Cog ? mg : 0);
+            float bs = 0.f;
+            if (p.bias) bs = p.bias[mrow[r]];
+            if (p.bias2) bs += p.bias2[mrow[r]];
 #pragma unroll
-            for (int j = 0; j < FN; ++j) epilogue_store(p, acc[i][j][r], b, phase, m, n0 + wn * 16 * FN + j * 16 + ln);
+            for (int j = 0; j < FN; ++j) av[0][j][r] += bs;
         }
+        switch (p.out_act) {
+            case RVC_ACT_LRELU: apply_act<RVC_ACT_LRELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_RELU: apply_act<RVC_ACT_RELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_TANH: apply_act<RVC_ACT_TANH, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_GELU: apply_act<RVC_ACT_GELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_SIGMOID: apply_act<RVC_ACT_SIGMOID, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_LOGCLAMP: apply_act<RVC_ACT_LOGCLAMP, 1, FN>(av, p.out_slope, p.out_scale); break;
+            default: apply_act<RVC_ACT_NONE, 1, FN>(av, p.out_slope, p.out_scale); break;
+        }
+        if (rb2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) av[0][j][r] += rb2[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
+        }
+        if (p.accumulate) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) av[0][j][r] += yb[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                if (mok[r] && tcol[j] >= 0) yb[mrow[r] * Lo + tcol[j]] = av[0][j][r];
+    }
 }
 
 __global__ void conv_splitk_reduce(ConvParams p) {
@@ -254,7 +347,7 @@ __global__ void conv_splitk_reduce(ConvParams p) {
     const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + n;
     float s = 0.f;
     for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
-    epilogue_store(p, s, bp / p.nphase, bp % p.nphase, m, n);
+    epilogue_store(p, s, bp / p.nphase, m, out_pos(p, n, bp % p.nphase));
 }
 
 struct Cfg {
@@ -274,6 +367,8 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
                   (long long)a->Ci, (long long)a->Co, a->K, (long long)a->Lin, (long long)a->Lout);
     RVC_CHECK_ARG(a->groups >= 1 && a->Ci % a->groups == 0 && a->Co % a->groups == 0, "conv1d: bad groups");
     RVC_CHECK_ARG(a->stride >= 1 && a->dil >= 1 && a->nphase >= 1 && a->ostride >= 1, "conv1d: bad stride/dil");
+    RVC_CHECK_ARG(a->Co * a->Lout < (1ll << 31) && a->Ci * a->Lin < (1ll << 31) && a->Lin + a->pad < (1ll << 30),
+                  "conv1d: per-batch tensor exceeds 2^31 elements (use the batch dimension)");
     const int64_t Cog = a->Co / a->groups;
     const int64_t Cig = a->Ci / a->groups;
     const int64_t ncols = a->ncols > 0 ? a->ncols : a->Lout;
@@ -339,7 +434,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     ks = (nch + p.chunks_per_split - 1) / p.chunks_per_split;
     p.ksplit = ks;
     const int WS = (BM / 32) * 32 + 16 + ((BM % 32) ? 32 : 0);
-    lds = (size_t)(KCH * WS + KCH) * 4 + (size_t)rows_max * p.span_s * 4;
+    lds = (size_t)(KCH * WS + KCH) * 4 + ((size_t)rows_max * p.span_s + 4) * 4;  // +dump slot
     RVC_CHECK_ARG(lds <= 160 * 1024, "conv1d: LDS %zu too large", lds);
     grid = dim3(cdiv(ncols, BN), (unsigned)(p.mtiles_per_group * a->groups), (unsigned)(a->B * a->nphase * ks));
     RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");

@@ -10,7 +10,8 @@ import ctypes
 import os
 from ctypes import POINTER, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "librvc_amd.so")
+LIB_PATH = os.environ.get("RVC_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "librvc_amd.so")
 
 ACT_NONE, ACT_LRELU, ACT_RELU, ACT_TANH, ACT_GELU, ACT_SIGMOID, ACT_LOGCLAMP = 0, 1, 2, 3, 4, 5, 6
 
@@ -64,8 +65,8 @@ SIGNATURES = {
     "rvc_img_to_seq": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_bigru": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p],
-    "rvc_filtfilt_pad": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
-                         c_void_p, c_void_p, c_void_p],
+    "rvc_filtfilt_pad": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                         c_void_p],
     "rvc_phone_upsample": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_peak_normalize": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
 }

@@ -293,6 +293,33 @@ def rmvpe_decode(sal, ld, F, thred, shift, f0, coarse, pitchf):
           "rmvpe_decode")
 
 
+class FiltFilt:
+    """scipy.signal.filtfilt(b, a, .) + reflect padding on the device (filtfilt.hip); zi = lfilter_zi(b, a)
+    is computed once on the host like the filter design itself."""
+
+    def __init__(self, b, a):
+        from scipy import signal
+        import numpy as np
+        self.b = np.ascontiguousarray(b, dtype=np.float64)
+        self.a = np.ascontiguousarray(a, dtype=np.float64)
+        if self.b.size != 6 or self.a.size != 6 or self.a[0] != 1.0:
+            raise ValueError("FiltFilt: 5th-order filter with a[0] == 1 expected")
+        self.zi = np.ascontiguousarray(signal.lfilter_zi(self.b, self.a), dtype=np.float64)
+
+    def __call__(self, x, tpad, want_f64=False):
+        """x: device f32 [N] -> (reflect-padded filtered f32 [N + 2 tpad], f64 copy or None)."""
+        N = x.numel()
+        work = torch.empty(2 * (N + 36), dtype=torch.float64, device=x.device)
+        out = torch.empty(N + 2 * tpad, device=x.device)
+        out64 = torch.empty(N + 2 * tpad, dtype=torch.float64, device=x.device) if want_f64 else None
+        h = lambda arr: ctypes.c_void_p(arr.ctypes.data)  # noqa: E731
+        check(_lib.load().rvc_filtfilt_pad(_p(x), N, h(self.b), h(self.a), h(self.zi), tpad,
+                                           ctypes.c_void_p(work.data_ptr()), _p(out),
+                                           ctypes.c_void_p(out64.data_ptr()) if want_f64 else None, _stream()),
+              "filtfilt_pad")
+        return out, out64
+
+
 def phone_upsample(feats, feats0, pitchf, out, C, Tf, T, protect):
     if feats.numel() < C * Tf or out.numel() < C * T or T > 2 * Tf or (pitchf is not None and pitchf.numel() < T):
         raise ValueError("phone_upsample: size mismatch")

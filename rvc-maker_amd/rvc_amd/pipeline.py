@@ -7,10 +7,11 @@ reference signature and returns float32 numpy audio at tgt_sr.  ``model`` is a
 ``ContentVecAMD`` (``.pt`` embedder), ``net_g`` a ``SynthesizerAMD`` (``.pth``); f0 is RMVPE
 (``self.rmvpe``, loaded once from ``assets/models/predictors/rmvpe.pt`` or injected).
 
-Host side (as the reference): scipy filtfilt (f64), the quiet-point segmentation for inputs
-> x_max, reflect padding.  Everything else runs on the device, in the order of
-convert.py:388-458; the segment loop keeps all tensors in HBM and only the final waveform
-is copied back.  ``pipeline_device`` is the HBM-resident form the bench times.
+Everything runs on the device in the order of convert.py:388-458 -- the f64 filtfilt and
+reflect padding included (filtfilt.hip); only the quiet-point search for inputs > x_max stays
+on the host (it needs the filtered signal there, as the reference).  The segment loop keeps all
+tensors in HBM; ``pipeline_device`` is the HBM-resident form the bench times, ``pipeline`` adds
+the host copies of the reference signature.
 
 Not on this path (raise): FAISS retrieval (index_rate > 0 with an index: §8(f) next row),
 f0 methods other than rmvpe, f0 files, autotune, volume_envelope != 1, ONNX models.
@@ -59,6 +60,7 @@ class VC:
         self.noise_fn = None  # parity hook: noise_fn(seg, "z"|"sine", shape) -> device tensor
         self.seed = 0
         self._ws = None
+        self.filt = ops.FiltFilt(BH, AH)
 
     # ------------------------------------------------------------------ host-side pieces
     def segment_points(self, audio: np.ndarray):
@@ -103,14 +105,18 @@ class VC:
         o, *_ = net_g.infer_cf(phone, pitch.contiguous(), pitchf.contiguous(), sid, zn, sn, self.seed + seg)
         return o
 
-    def pipeline_device(self, model, net_g, sid, audio_f64: np.ndarray, pitch, version, protect):
-        """The hot path with the waveform left in HBM: returns a device f32 tensor at tgt_sr."""
-        audio = signal.filtfilt(BH, AH, audio_f64)
-        opt_ts = self.segment_points(audio)
-        audio_pad = np.pad(audio, (self.t_pad, self.t_pad), mode="reflect")
-        p_len = audio_pad.shape[0] // self.window
-        dev = self.device
-        xp = torch.from_numpy(audio_pad.astype(np.float32)).to(dev)
+    def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect):
+        """The hot path with inputs and output in HBM: audio device f32 [N] at 16 kHz (numpy accepted)
+        -> device f32 waveform at tgt_sr.  filtfilt + reflect padding run on the device (f64)."""
+        if not torch.is_tensor(audio):
+            audio = torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)).to(self.device)
+        N = audio.numel()
+        long_input = N + self.window > self.t_max  # convert.py:406 (audio padded by window/2 each side)
+        xp, xp64 = self.filt(audio.contiguous(), self.t_pad, want_f64=long_input)
+        opt_ts = []
+        if long_input:  # quiet-point search on the filtered f64 signal, host side as the reference
+            opt_ts = self.segment_points(xp64[self.t_pad: self.t_pad + N].cpu().numpy())
+        p_len = xp.numel() // self.window
         return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect)
 
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect):
@@ -152,7 +158,8 @@ class VC:
             raise NotImplementedError("ONNX / safetensors models are not on the MI355X path")
         if pbar is not None:
             pbar.update(1)
-        out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio), pitch, version, protect)
+        out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
+                                   protect)
         if pbar is not None:
             pbar.update(3)
         return out.cpu().numpy()

@@ -182,3 +182,32 @@ def test_randn_moments(ops):
     out2 = torch.empty(1 << 20, device=DEV)
     ops.randn(out2, seed=123)
     assert torch.equal(out.cpu(), out2.cpu())
+
+
+@pytest.mark.parametrize("N,tpad", [(480000, 16000), (3001, 1000), (40, 0)])
+def test_filtfilt_pad_matches_scipy(ops, N, tpad):
+    """convert.py:403,416: scipy filtfilt (f64, odd padding) + reflect pad, on the device.
+
+    Tolerance: the chunked recurrence reproduces scipy's sequential result up to rounding noise
+    amplified by the filter's 1.7e7 transient state gain (~1e-7 of full scale)."""
+    from scipy import signal
+    from rvc_amd.pipeline import AH, BH
+    x = (np.random.default_rng(N).standard_normal(N) * 0.3).astype(np.float32)
+    ref = np.pad(signal.filtfilt(BH, AH, x), (tpad, tpad), mode="reflect")
+    f = ops.FiltFilt(BH, AH)
+    out, out64 = f(torch.from_numpy(x).to(DEV), tpad, want_f64=True)
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(out64.cpu().numpy(), ref, rtol=0, atol=1e-6 * scale)
+    assert np.max(np.abs(out.cpu().numpy() - ref.astype(np.float32))) <= 1e-6 * scale
+    assert np.sqrt(np.mean((out64.cpu().numpy() - ref) ** 2)) < 1e-7 * scale
+
+
+def test_filtfilt_golden(ops, golden):
+    """The reference's own filtfilt output (tests/golden/filtfilt.npz, f64 input) -- via f32, as the pipeline."""
+    from scipy import signal
+    from rvc_amd.pipeline import AH, BH
+    g = golden("filtfilt")
+    np.testing.assert_allclose(signal.filtfilt(BH, AH, g["x"]), g["y"], rtol=0, atol=1e-12)
+    f = ops.FiltFilt(BH, AH)
+    _, out64 = f(torch.from_numpy(g["x"].astype(np.float32)).to(DEV), 0, want_f64=True)
+    np.testing.assert_allclose(out64.cpu().numpy(), g["y"], rtol=0, atol=1e-6)
