@@ -113,7 +113,10 @@ typedef struct rvc_attn_args {
     float scale, _pad1;
 } rvc_attn_args;
 
-int rvc_attention(const rvc_attn_args* a, rvc_stream_t stream);
+/* Long sequences are split over the keys (split-KV) to fill the chip; the partials need a
+ * workspace of rvc_attention_workspace_bytes(a) bytes (0 when not split). */
+int64_t rvc_attention_workspace_bytes(const rvc_attn_args* a);
+int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ elementwise
  * Memory-bound pieces of Synthesizer.infer (synthesizers.py:446-465).  All
@@ -176,7 +179,9 @@ int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, doub
  */
 /* filtfilt_pad: scipy.signal.filtfilt(b, a, x) (padtype odd, padlen 18; convert.py:403) in f64, then
  *   reflect padding by tpad (convert.py:416): x f32 [N] -> out f32 [N + 2*tpad] (+ optional f64 copy).
- *   b[6], a[6], zi[5] (= lfilter_zi(b, a)) are HOST arrays; work: device f64 [2*(N+36)]. */
+ *   b[6], a[6], zi[5] (= lfilter_zi(b, a)) are HOST arrays; work: device scratch of
+ *   rvc_filtfilt_work_bytes(N) bytes (8-byte aligned). */
+int64_t rvc_filtfilt_work_bytes(int64_t N);
 int rvc_filtfilt_pad(const float* x, int64_t N, const double* b, const double* a, const double* zi, int64_t tpad,
                      double* work, float* out, double* out64, rvc_stream_t stream);
 int rvc_phone_upsample(const float* feats, const float* feats0, const float* pitchf, float* out, int64_t C, int64_t Tf,

@@ -376,7 +376,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     if (Cog % 48 == 0 && Cog % 64 != 0) cfg = {3, 1, 1, 4};  // 48 x 64 (ContentVec pos_conv groups)
     else if (Cog <= 16) cfg = {1, 4, 1, 4};                  // 16 x 256
     else if (Cog <= 32) cfg = {2, 4, 1, 4};                  // 32 x 256
-    else if (Cog <= 64) cfg = {2, 4, 2, 2};                  // 64 x 128
+    else if (Cog <= 64 || Cog % 128 != 0) cfg = {2, 4, 2, 2}; // 64 x 128 (also 192: no half-empty M tile)
     else cfg = {4, 4, 2, 2};                                 // 128 x 128
     int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
 

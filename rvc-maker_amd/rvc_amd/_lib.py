@@ -44,7 +44,8 @@ SIGNATURES = {
     "rvc_version": [],
     "rvc_conv1d": [POINTER(Conv1dArgs), c_void_p, c_int64, c_void_p],
     "rvc_conv1d_workspace_bytes": [POINTER(Conv1dArgs)],
-    "rvc_attention": [POINTER(AttnArgs), c_void_p],
+    "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],
+    "rvc_attention": [POINTER(AttnArgs), c_void_p, c_int64, c_void_p],
     "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
                           c_void_p],
     "rvc_layernorm_cf": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
@@ -65,12 +66,14 @@ SIGNATURES = {
     "rvc_img_to_seq": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_bigru": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p],
+    "rvc_filtfilt_work_bytes": [c_int64],
     "rvc_filtfilt_pad": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                          c_void_p],
     "rvc_phone_upsample": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_peak_normalize": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
 }
-_RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64}
+_RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64,
+             "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64}
 
 _lib = None
 

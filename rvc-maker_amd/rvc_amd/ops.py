@@ -91,9 +91,10 @@ LAST_CONV_FLOPS = 0.0
 _WS = {}
 
 
-def _workspace(device, nbytes):
-    """Per-device split-K scratch, grown on demand (stream-ordered reuse is safe: one stream)."""
-    key = str(device)
+def _workspace(device, nbytes, kind="conv"):
+    """Split-K / split-KV scratch per (device, stream), grown on demand: reuse is stream-ordered, and
+    work running concurrently on another stream (VC's side stream) gets its own buffer."""
+    key = f"{device}/{kind}/{torch.cuda.current_stream(device).stream_id}"
     buf = _WS.get(key)
     if buf is None or buf.numel() * 4 < nbytes:
         buf = torch.empty((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
@@ -177,7 +178,12 @@ def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_b
     a.q_hs, a.k_hs, a.v_hs, a.o_hs = q_hs, k_hs, v_hs, o_hs
     a.q_bs, a.k_bs, a.v_bs, a.o_bs = q_bs, k_bs, v_bs, o_bs
     a.W, a.scale = W, scale
-    check(_lib.load().rvc_attention(ctypes.byref(a), _stream()), "attention")
+    lib = _lib.load()
+    need = lib.rvc_attention_workspace_bytes(ctypes.byref(a))
+    if need < 0:
+        raise ValueError(f"attention: unsupported shape H={H} D={D} T={T}")
+    ws = _workspace(o.device, need, "attn") if need else None
+    check(lib.rvc_attention(ctypes.byref(a), _p(ws), need, _stream()), "attention")
     return o
 
 
@@ -309,7 +315,10 @@ class FiltFilt:
     def __call__(self, x, tpad, want_f64=False):
         """x: device f32 [N] -> (reflect-padded filtered f32 [N + 2 tpad], f64 copy or None)."""
         N = x.numel()
-        work = torch.empty(2 * (N + 36), dtype=torch.float64, device=x.device)
+        nbytes = _lib.load().rvc_filtfilt_work_bytes(N)
+        if nbytes < 0:
+            raise ValueError(f"filtfilt: bad length {N}")
+        work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=x.device)
         out = torch.empty(N + 2 * tpad, device=x.device)
         out64 = torch.empty(N + 2 * tpad, dtype=torch.float64, device=x.device) if want_f64 else None
         h = lambda arr: ctypes.c_void_p(arr.ctypes.data)  # noqa: E731

@@ -83,12 +83,18 @@ class VC:
         return self.rmvpe
 
     # ------------------------------------------------------------------ device pieces
-    def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg):
-        """VC.voice_conversion (convert.py:328-386) on a device segment a0 [N] -> waveform [T*upp]."""
-        N = a0.numel()
+    def features_device(self, model, a0, version):
+        """convert.py:337-340: embedder features of segment a0 [N], channels-first [E][T_f]."""
         feats = model.features_cf(a0, 9 if version == "v1" else 12)
         if version == "v1":
             feats = model.final_proj.conv(feats)
+        return feats
+
+    def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats=None):
+        """VC.voice_conversion (convert.py:328-386) on a device segment a0 [N] -> waveform [T*upp]."""
+        N = a0.numel()
+        if feats is None:
+            feats = self.features_device(model, a0, version)
         E, Tf = feats.shape
         p_len = N // self.window
         T = min(2 * Tf, p_len)  # convert.py:364-370
@@ -119,24 +125,47 @@ class VC:
         p_len = xp.numel() // self.window
         return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect)
 
+    def _side_stream(self, device):
+        key = str(device)
+        if getattr(self, "_streams", None) is None:
+            self._streams = {}
+        if key not in self._streams:
+            self._streams[key] = torch.cuda.Stream(device=device)
+        return self._streams[key]
+
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect):
-        coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch))
-        coarse, pitchf = coarse[:p_len], pitchf[:p_len]
-        outs = []
-        s, t, seg = 0, None, 0
+        # Segments of convert.py:419-440: [s, t + t_pad2 + w) for each quiet point t, then [t, end).
         w, tp = self.window, self.t_pad_tgt
+        segs, s = [], 0
         for t in opt_ts:
             t = t // w * w
-            o = self.voice_conversion_device(model, net_g, sid, xp[s: t + self.t_pad2 + w],
-                                             coarse[s // w: (t + self.t_pad2) // w],
-                                             pitchf[s // w: (t + self.t_pad2) // w], version, protect, seg)
-            outs.append(o[tp: o.numel() - tp])
+            segs.append((s, t + self.t_pad2 + w, s // w, (t + self.t_pad2) // w))
             s = t
-            seg += 1
-        o = self.voice_conversion_device(model, net_g, sid, xp[t:] if t is not None else xp,
-                                         coarse[t // w:] if t is not None else coarse,
-                                         pitchf[t // w:] if t is not None else pitchf, version, protect, seg)
-        outs.append(o[tp: o.numel() - tp])
+        last = opt_ts[-1] // w * w if opt_ts else None
+        segs.append((last or 0, xp.numel(), (last or 0) // w, None))
+        # RMVPE (f0 over the whole padded signal) runs on a side stream, concurrently with the
+        # ContentVec features of every segment on the main stream: the two networks are independent
+        # until the synthesizer, and RMVPE's BiGRU recurrence occupies only 32 CUs.
+        main = torch.cuda.current_stream(xp.device)
+        side = self._side_stream(xp.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch))
+            f0_done = torch.cuda.Event()
+            f0_done.record(side)
+        feats = [self.features_device(model, xp[a:b], version) for a, b, _, _ in segs]
+        main.wait_event(f0_done)
+        coarse.record_stream(main)
+        pitchf.record_stream(main)
+        xp.record_stream(side)
+        coarse, pitchf = coarse[:p_len], pitchf[:p_len]
+        outs = []
+        for seg, ((a, b, fa, fb), fe) in enumerate(zip(segs, feats)):
+            o = self.voice_conversion_device(model, net_g, sid, xp[a:b], coarse[fa:fb], pitchf[fa:fb], version,
+                                             protect, seg, feats=fe)
+            outs.append(o[tp: o.numel() - tp])
         out = torch.cat(outs) if len(outs) > 1 else outs[0].contiguous()
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=xp.device)

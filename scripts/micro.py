@@ -1,0 +1,62 @@
+"""Micro-timings of the non-conv kernels at the bench's 30 s shapes (HIP events, torch stream).
+
+    python scripts/micro.py
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rvc-maker_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def timeit(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+def main():
+    from rvc_amd import ops
+    from rvc_amd.pipeline import AH, BH
+    dev = "cuda"
+    g = torch.Generator().manual_seed(0)
+    # filtfilt + reflect pad, 30 s at 16 kHz
+    f = ops.FiltFilt(BH, AH)
+    for n in (480000, 96000, 16000, 4000):
+        x = (torch.randn(n, generator=g) * 0.3).to(dev)
+        print(f"filtfilt_pad N={n}: {timeit(lambda: f(x, min(16000, n - 1))):9.1f} us")
+    # attention: TextEncoder (2 x 96, rel band W=10), ContentVec (12 x 64)
+    for H, D, T, rel in ((2, 96, 3200, True), (12, 64, 1600, False), (2, 96, 3200, False)):
+        qkv = torch.randn(3 * H * D, T, generator=g).to(dev)
+        o = torch.empty(H * D, T, device=dev)
+        kw = {}
+        if rel:
+            kw = dict(rk=torch.randn(H, 21, T, generator=g).to(dev) * 0.1, ev=torch.randn(21, D, generator=g).to(dev),
+                      ml=torch.empty(H, 2, T, device=dev), W=10)
+        C = H * D
+        fn = lambda: ops.attention(qkv, qkv[C:], qkv[2 * C:], o, B=1, H=H, D=D, T=T, ldc=T, q_hs=D * T,  # noqa: E731
+                                   k_hs=D * T, v_hs=D * T, o_hs=D * T, scale=D ** -0.5, **kw)
+        us = timeit(fn)
+        fl = 4.0 * T * T * D * H
+        print(f"attention H={H} D={D} T={T} rel={rel}: {us:9.1f} us  {fl / us / 1e6:6.1f} TFLOP/s")
+    # split-K reduce candidates: a flow-sized conv
+    for Ci, Co, K, L in ((192, 384, 5, 3200), (192, 192, 1, 3200), (192, 768, 3, 3200), (768, 192, 3, 3200)):
+        w = torch.randn(Co, Ci, K, generator=g) / np.sqrt(Ci * K)
+        c = ops.Conv(w, torch.zeros(Co), device=dev)
+        xi = torch.randn(Ci, L, generator=g).to(dev)
+        us = timeit(lambda: c(xi, pad=K // 2))
+        print(f"conv Ci={Ci} Co={Co} K={K} L={L}: {us:9.1f} us  {2.0 * Ci * Co * K * L / us / 1e6:6.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
