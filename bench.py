@@ -117,6 +117,7 @@ def main():
     torch.cuda.set_device(local)
 
     from rvc_amd import synthetic
+    from rvc_amd.shard import gather_waveforms
     vc, hub, net_g = build_models(dev)
     audio = synthetic.synthetic_audio(args.seconds, seed=1000 + rank)
     audio_dev = torch.from_numpy(audio).to(dev)  # input resident in HBM before the timed region
@@ -126,14 +127,7 @@ def main():
         out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33)
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
-            n = torch.tensor([out.numel()], device=dev, dtype=torch.int64)
-            sizes = [torch.zeros_like(n) for _ in range(world)]
-            dist.all_gather(sizes, n)
-            mx = int(max(int(s) for s in sizes))
-            buf = torch.zeros(mx, device=dev)
-            buf[: out.numel()] = out
-            gl = [torch.zeros(mx, device=dev) for _ in range(world)] if rank == 0 else None
-            dist.gather(buf, gl, dst=0)
+            gather_waveforms([out], dist, dst=0)
         return out
 
     for _ in range(args.warmup):

@@ -81,12 +81,22 @@ typedef struct rvc_conv1d_args {
        (t % wrap in {0, wrap-1}, or t / wrap in {0, Lout/wrap - 1}). */
     int ntoff, wrap;
     int toff[16];
+    /* Split-bf16 engine: wx = the same weights pre-split into bf16 h/m/l planes by
+       rvc_conv1d_pack_x6 (NULL = f32 MFMA engine).  Used for stride-1, ungrouped, 1-D convs;
+       other shapes ignore it.  wx_nmf = its padded 16-row fragment count. */
+    const void* wx;
+    int wx_nmf, _pad1;
 } rvc_conv1d_args;
 
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned
  * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args). */
 int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a);
 int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
+/* Pack KM weights [nphase][Ci*K][Co] (one group) for the split-bf16 engine: out must hold
+ * rvc_conv1d_x6_bytes(nphase, Ci, K, Co) bytes; *nmf_out receives wx_nmf. */
+int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co);
+int rvc_conv1d_pack_x6(const float* w_km, int64_t nphase, int64_t Ci, int K, int64_t Co, void* out, int* nmf_out,
+                       rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ attention
  * Flash-style multi-head attention on f32 MFMA over channels-first Q/K/V

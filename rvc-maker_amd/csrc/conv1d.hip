@@ -39,6 +39,8 @@ struct ConvParams {
     int mtiles_per_group, ksplit, chunks_per_split, avec;
     int ntoff, wrap;
     int toff[16];
+    const uint4* wx;  // split-bf16 packed weights (x6 engine) or null
+    int wx_nmf, wx_nch;
 };
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
@@ -79,6 +81,87 @@ __device__ __forceinline__ void apply_act(floatx4 (&acc)[FM][FN], float slope, f
         for (int j = 0; j < FN; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[i][j][r] = act_apply(acc[i][j][r], ACT, slope) * scale;
+}
+
+// Shared epilogue of the conv engines (both produce the MFMA 16x16 C layout: lane l holds column
+// l&15, rows (l>>4)*4 + r of each fragment).  Split-K partial tiles go to the workspace; otherwise
+// bias, 2nd bias, activation, scale, residual, accumulate and the (strided / polyphase / masked)
+// store are fused here.
+template <int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc)[FM][FN], int lane, int wm, int wn,
+                                              int split, int phase, int b, int g, int Cog, int m0g, int64_t n0) {
+    const int ln = lane & 15;
+    const int lr = (lane >> 4) * 4;
+    if (p.ksplit > 1) {
+        float* wsb = p.ws + (((int64_t)split * p.B * p.nphase + (int64_t)b * p.nphase + phase) * p.Co) * p.ncols;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
+                const int64_t m = (int64_t)g * Cog + mg;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
+                    if (mg < Cog && n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
+                }
+            }
+        return;
+    }
+    // Epilogue one row fragment (16 channels x BN/WN columns) at a time, in passes so that hipcc
+    // issues each class of loads together: bias + activation + scale in registers (activation
+    // dispatched once per kernel, not per element), residual loads, accumulate loads -- all from
+    // clamped addresses -- then masked stores.  Per-fragment (not whole-tile) passes bound the
+    // epilogue's live registers, which would otherwise set the whole kernel's occupancy.
+    int tcol[FN];  // store position per column fragment (shared by all rows)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) tcol[j] = out_pos(p, n0 + wn * 16 * FN + j * 16 + ln, phase);
+    float* yb = p.y + b * p.y_bstride;
+    const float* rb2 = p.res ? p.res + b * p.res_bstride : nullptr;
+    const int Lo = (int)p.Lout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        floatx4 (&av)[1][FN] = *reinterpret_cast<floatx4 (*)[1][FN]>(&acc[i][0]);
+        int mrow[4];  // channel index (clamped); m * Lout < 2^31 is checked on the host
+        bool mok[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
+            mok[r] = mg < Cog;
+            mrow[r] = g * Cog + (mg < Cog ? mg : 0);
+            float bs = 0.f;
+            if (p.bias) bs = p.bias[mrow[r]];
+            if (p.bias2) bs += p.bias2[mrow[r]];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) av[0][j][r] += bs;
+        }
+        switch (p.out_act) {
+            case RVC_ACT_LRELU: apply_act<RVC_ACT_LRELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_RELU: apply_act<RVC_ACT_RELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_TANH: apply_act<RVC_ACT_TANH, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_GELU: apply_act<RVC_ACT_GELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_SIGMOID: apply_act<RVC_ACT_SIGMOID, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_LOGCLAMP: apply_act<RVC_ACT_LOGCLAMP, 1, FN>(av, p.out_slope, p.out_scale); break;
+            default: apply_act<RVC_ACT_NONE, 1, FN>(av, p.out_slope, p.out_scale); break;
+        }
+        if (rb2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) av[0][j][r] += rb2[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
+        }
+        if (p.accumulate) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) av[0][j][r] += yb[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                if (mok[r] && tcol[j] >= 0) yb[mrow[r] * Lo + tcol[j]] = av[0][j][r];
+    }
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -265,77 +348,201 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
         __syncthreads();
     }
 
-    const int lr = (lane >> 4) * 4;
-    if (p.ksplit > 1) {
-        float* wsb = p.ws + (((int64_t)split * p.B * p.nphase + (int64_t)b * p.nphase + phase) * p.Co) * p.ncols;
+    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, g, Cog, m0g, n0);
+}
+
+// ------------------------------------------------------------------ split-bf16 ("x6") engine
+// f32 convolution on the bf16 matrix cores: every f32 operand is split exactly into three bf16
+// pieces (x = h + m + l, |x - (h+m+l)| <= 2^-27 |x|) and the product keeps the six terms down to
+// the 2^-24 level: hH + hM + mH + hL + mM + lH (v_mfma_f32_16x16x32_bf16, f32 accumulation).
+// That is f32-level accuracy at 6 x 16 cycles per 16x16x32 block against 8 x 32 for the f32 MFMA
+// (2.7x the f32 matrix rate).  Stride-1, ungrouped 1-D convs (everything hot in the generator,
+// flow, TextEncoder and the ContentVec linears).
+//
+// k-steps are (32-channel chunk, tap): a chunk's input rows are staged ONCE into LDS (split into
+// h/m/l planes, channel-contiguous [pos][32 ch] rows, 16-B groups XOR-swizzled by (pos>>2)&3 so
+// both the staging writes and the operand reads are conflict-free) and reused by all K taps.
+// B operands are one ds_read_b128 per plane per fragment; A operands (weights) come pre-split
+// and pre-arranged per lane from global memory (L2-resident), prefetched one k-step ahead.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+RVC_DEV floatx4 mfma_bf16(const uint4& a, const uint4& b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// v -> (h, m, l) bf16 bit patterns, v == h + m + (exactly representable rest), l = bf16(rest)
+RVC_DEV void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
+    const __bf16 bh = (__bf16)v;
+    const float r1 = v - (float)bh;  // exact (Sterbenz)
+    const __bf16 bm = (__bf16)r1;
+    const float r2 = r1 - (float)bm;  // exact
+    const __bf16 bl = (__bf16)r2;
+    h = __builtin_bit_cast(uint16_t, bh);
+    m = __builtin_bit_cast(uint16_t, bm);
+    l = __builtin_bit_cast(uint16_t, bl);
+}
+
+constexpr int X6_NI = 4;  // staged (position, 8-channel group) items per loader thread: 4 * span <= 1024
+
+// Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
+// own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
+// input prefetch never wait on each other.  One workgroup barrier per 32-channel chunk hands the
+// next staged X buffer (double-buffered in LDS) to the compute waves.
+template <int FM, int FN, int WM, int WN>
+__global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
+    static_assert(WM * WN == 4, "4 compute waves");
+    constexpr int BM = 16 * FM * WM;
+    constexpr int BN = 16 * FN * WN;
+    extern __shared__ uint4 xs[];  // [2 buffers][3 planes][span][4 x 16 B]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int zb = blockIdx.z;
+    const int split = zb % p.ksplit;
+    zb /= p.ksplit;
+    const int phase = zb % p.nphase;
+    const int b = zb / p.nphase;
+    const int Cog = (int)p.Co;
+    const int Cig = (int)p.Ci;
+    const int m0g = blockIdx.y * BM;
+    const int64_t n0 = (int64_t)blockIdx.x * BN;
+    const int K = p.K, span = p.span;
+    const int nch = p.wx_nch, nmf = p.wx_nmf;
+    const int ch_beg = split * p.chunks_per_split;
+    const int ch_end = min(nch, ch_beg + p.chunks_per_split);
+    const int nck = ch_end - ch_beg;
+    const int bufsz = 3 * span * 4;  // uint4 per buffer
+
+    if (wave >= 4) {
+        // ---------------- loader waves: chunk c+1 split into LDS while chunk c computes
+        const int ltid = tid - 256;
+        const int lin = (int)p.Lin;
+        const float* xb = p.x + b * p.x_bstride;
+        const int base = (int)(n0 - p.pad);
+        int ipos[X6_NI], ig8[X6_NI];
+        unsigned iok = 0;
+#pragma unroll
+        for (int it = 0; it < X6_NI; ++it) {
+            const int idx = ltid + 256 * it;
+            const int g8 = idx / span;
+            ig8[it] = g8 < 4 ? g8 : 3;
+            ipos[it] = idx - g8 * span;
+            const int q = base + ipos[it];
+            iok |= (unsigned)(idx < 4 * span && q >= 0 && q < lin) << it;
+        }
+        float xr[2][X6_NI][8];
+        auto xload = [&](int ch, float (&r)[X6_NI][8]) __attribute__((always_inline)) {
+            // unconditional (clamped) loads so that the vmcnt bookkeeping is static
+#pragma unroll
+            for (int it = 0; it < X6_NI; ++it) {
+                const int q = base + ipos[it];
+                const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    int c = ch * 32 + ig8[it] * 8 + e;
+                    c = c < Cig ? c : Cig - 1;
+                    r[it][e] = xb[(int64_t)c * lin + qc];
+                }
+            }
+        };
+        auto xstore = [&](int ch, const float (&r)[X6_NI][8], uint4* dst) __attribute__((always_inline)) {
+#pragma unroll
+            for (int it = 0; it < X6_NI; ++it) {
+                if (ltid + 256 * it < 4 * span) {
+                    uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) {
+                        uint32_t h2[2], m2[2], l2[2];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const int e = 2 * e2 + u;
+                            const bool ok = ((iok >> it) & 1u) && ch * 32 + ig8[it] * 8 + e < Cig;
+                            float v = r[it][e] * p.in_scale;
+                            if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
+                            split3(ok ? v : 0.f, h2[u], m2[u], l2[u]);
+                        }
+                        hw[e2] = h2[0] | (h2[1] << 16);
+                        mw[e2] = m2[0] | (m2[1] << 16);
+                        lw[e2] = l2[0] | (l2[1] << 16);
+                    }
+                    const int pos = ipos[it];
+                    const int slot = pos * 4 + (ig8[it] ^ ((pos >> 2) & 3));
+                    dst[slot] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                    dst[span * 4 + slot] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+                    dst[2 * span * 4 + slot] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                }
+            }
+        };
+        // prologue: chunk 0 -> LDS buffer 0, chunk 1 in flight
+        xload(ch_beg, xr[0]);
+        xload(min(ch_beg + 1, nch - 1), xr[1]);
+        xstore(ch_beg, xr[0], xs);
+        __syncthreads();
+        // iteration i (chunk ch_beg + i computing): regs slot (i+1)&1 holds chunk i+1; slot i&1 is free
+        auto iter = [&](int i, float (&nxt)[X6_NI][8], float (&fre)[X6_NI][8]) __attribute__((always_inline)) {
+            xload(min(ch_beg + i + 2, nch - 1), fre);
+            if (i + 1 < nck) xstore(ch_beg + i + 1, nxt, xs + ((i + 1) & 1) * bufsz);
+            __syncthreads();
+        };
+        for (int i = 0; i < nck; i += 2) {
+            iter(i, xr[1], xr[0]);
+            if (i + 1 < nck) iter(i + 1, xr[0], xr[1]);
+        }
+        return;
+    }
+
+    // ---------------- compute waves
+    const int wm = wave / WN, wn = wave % WN;
+    const uint4* wxp = p.wx + (int64_t)phase * K * nch * nmf * 3 * 64;
+    const int mf0 = m0g / 16 + wm * FM;
+    auto aload = [&](int s, uint4 (&a)[3][FM]) __attribute__((always_inline)) {
+        const int ch = s / K, t = s - ch * K;
+        const uint4* src = wxp + ((int64_t)((t * nch + ch) * nmf + mf0) * 3) * 64 + lane;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
-                const int64_t m = (int64_t)g * Cog + mg;
+            for (int q = 0; q < 3; ++q) a[q][i] = src[(i * 3 + q) * 64];
+    };
+    floatx4 acc[FM][FN];
 #pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
-                    if (mg < Cog && n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
-                }
-            }
-        return;
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int ln = lane & 15, lg = lane >> 4;
+    const int pb = wn * 16 * FN + ln;
+    auto compute = [&](int t, const uint4* xbuf, const uint4 (&a)[3][FM]) __attribute__((always_inline)) {
+        uint4 bq[3][FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int pos = pb + 16 * j + t * p.dil;
+            const int slot = pos * 4 + (lg ^ ((pos >> 2) & 3));
+#pragma unroll
+            for (int q = 0; q < 3; ++q) bq[q][j] = xbuf[q * span * 4 + slot];
+        }
+        // six passes, each over all FM x FN accumulators (no back-to-back dependent MFMAs)
+        constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
+        constexpr int PB[6] = {0, 1, 0, 2, 1, 0};
+#pragma unroll
+        for (int ps = 0; ps < 6; ++ps)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]][j], acc[i][j]);
+    };
+    const int s_beg = ch_beg * K, s_end = ch_end * K;
+    uint4 a0[3][FM], a1[3][FM];
+    if (s_beg < s_end) aload(s_beg, a0);
+    __syncthreads();  // chunk 0 staged
+    auto step = [&](int s, const uint4 (&cur)[3][FM], uint4 (&nxt)[3][FM]) __attribute__((always_inline)) {
+        const int ch = s / K, t = s - ch * K;
+        if (s + 1 < s_end) aload(s + 1, nxt);
+        compute(t, xs + ((ch - ch_beg) & 1) * bufsz, cur);
+        if (t == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
+    };
+    for (int s = s_beg; s < s_end; s += 2) {
+        step(s, a0, a1);
+        if (s + 1 < s_end) step(s + 1, a1, a0);
     }
-    // Epilogue one row fragment (16 channels x BN/WN columns) at a time, in passes so that hipcc
-    // issues each class of loads together: bias + activation + scale in registers (activation
-    // dispatched once per kernel, not per element), residual loads, accumulate loads -- all from
-    // clamped addresses -- then masked stores.  Per-fragment (not whole-tile) passes bound the
-    // epilogue's live registers, which would otherwise set the whole kernel's occupancy.
-    int tcol[FN];  // store position per column fragment (shared by all rows)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) tcol[j] = out_pos(p, n0 + wn * 16 * FN + j * 16 + ln, phase);
-    float* yb = p.y + b * p.y_bstride;
-    const float* rb2 = p.res ? p.res + b * p.res_bstride : nullptr;
-    const int Lo = (int)p.Lout;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-        floatx4 (&av)[1][FN] = *reinterpret_cast<floatx4 (*)[1][FN]>(&acc[i][0]);
-        int mrow[4];  // channel index (clamped); m * Lout < 2^31 is checked on the host
-        bool mok[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
-            mok[r] = mg < Cog;
-            mrow[r] = g * Cog + (mg < Cog ? mg : 0);
-            float bs = 0.f;
-            if (p.bias) bs = p.bias[mrow[r]];
-            if (p.bias2) bs += p.bias2[mrow[r]];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) av[0][j][r] += bs;
-        }
-        switch (p.out_act) {
-            case RVC_ACT_LRELU: apply_act<RVC_ACT_LRELU, 1, FN>(av, p.out_slope, p.out_scale); break;
-            case RVC_ACT_RELU: apply_act<RVC_ACT_RELU, 1, FN>(av, p.out_slope, p.out_scale); break;
-            case RVC_ACT_TANH: apply_act<RVC_ACT_TANH, 1, FN>(av, p.out_slope, p.out_scale); break;
-            case RVC_ACT_GELU: apply_act<RVC_ACT_GELU, 1, FN>(av, p.out_slope, p.out_scale); break;
-            case RVC_ACT_SIGMOID: apply_act<RVC_ACT_SIGMOID, 1, FN>(av, p.out_slope, p.out_scale); break;
-            case RVC_ACT_LOGCLAMP: apply_act<RVC_ACT_LOGCLAMP, 1, FN>(av, p.out_slope, p.out_scale); break;
-            default: apply_act<RVC_ACT_NONE, 1, FN>(av, p.out_slope, p.out_scale); break;
-        }
-        if (rb2) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int j = 0; j < FN; ++j) av[0][j][r] += rb2[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
-        }
-        if (p.accumulate) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int j = 0; j < FN; ++j) av[0][j][r] += yb[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-                if (mok[r] && tcol[j] >= 0) yb[mrow[r] * Lo + tcol[j]] = av[0][j][r];
-    }
+    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
 }
 
 __global__ void conv_splitk_reduce(ConvParams p) {
@@ -352,12 +559,57 @@ __global__ void conv_splitk_reduce(ConvParams p) {
 
 struct Cfg {
     int FM, FN, WM, WN;
+    bool x6;
 };
 
 template <int FM, int FN, int WM, int WN>
 hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL((conv1d_mfma_kernel<FM, FN, WM, WN>), grid, dim3(256), lds, s, p);
     return hipGetLastError();
+}
+
+template <int FM, int FN, int WM, int WN>
+hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN>), grid, dim3(512), lds, s, p);
+    return hipGetLastError();
+}
+
+void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
+    p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y; p.ws = nullptr;
+    p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout;
+    p.ncols = a->ncols > 0 ? a->ncols : a->Lout;
+    p.x_bstride = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
+    p.y_bstride = a->y_bstride ? a->y_bstride : a->Co * a->Lout;
+    p.res_bstride = a->res_bstride ? a->res_bstride : a->Co * a->Lout;
+    p.w_bstride = a->w_bstride;
+    p.K = a->K; p.stride = a->stride; p.dil = a->dil; p.pad = a->pad; p.groups = a->groups;
+    p.nphase = a->nphase; p.ostride = a->ostride; p.ooffset = a->ooffset;
+    p.in_act = a->in_act; p.out_act = a->out_act; p.accumulate = a->accumulate;
+    p.in_scale = a->in_scale; p.in_slope = a->in_slope; p.out_slope = a->out_slope; p.out_scale = a->out_scale;
+    p.ntoff = a->ntoff; p.wrap = a->wrap;
+    for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff ? a->toff[i] : 0;
+    p.wx = nullptr;
+    p.wx_nmf = p.wx_nch = 0;
+}
+
+// split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
+void split_k(ConvParams& p, int64_t tiles, int nch) {
+    int ks = 1;
+    if (tiles < 512 && nch >= 4) {
+        ks = (int)((512 + tiles - 1) / tiles);
+        if (ks > 16) ks = 16;
+        if (ks > nch / 2) ks = nch / 2;
+        if (ks < 1) ks = 1;
+    }
+    p.chunks_per_split = (nch + ks - 1) / ks;
+    p.ksplit = (nch + p.chunks_per_split - 1) / p.chunks_per_split;
+}
+
+constexpr int X6_BN = 128;
+
+bool x6_eligible(const rvc_conv1d_args* a) {
+    return a->wx && a->stride == 1 && a->groups == 1 && a->ntoff == 0 && a->w_bstride == 0 &&
+           X6_BN + (a->K - 1) * a->dil <= 256 && a->wx_nmf % 8 == 0 && (int64_t)a->wx_nmf * 16 >= a->Co;
 }
 
 int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& lds) {
@@ -372,12 +624,37 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     const int64_t Cog = a->Co / a->groups;
     const int64_t Cig = a->Ci / a->groups;
     const int64_t ncols = a->ncols > 0 ? a->ncols : a->Lout;
+    fill_common(a, p);
 
-    if (Cog % 48 == 0 && Cog % 64 != 0) cfg = {3, 1, 1, 4};  // 48 x 64 (ContentVec pos_conv groups)
-    else if (Cog <= 16) cfg = {1, 4, 1, 4};                  // 16 x 256
-    else if (Cog <= 32) cfg = {2, 4, 1, 4};                  // 32 x 256
-    else if (Cog <= 64 || Cog % 128 != 0) cfg = {2, 4, 2, 2}; // 64 x 128 (also 192: no half-empty M tile)
-    else cfg = {4, 4, 2, 2};                                 // 128 x 128
+    if (x6_eligible(a)) {
+        cfg.x6 = true;
+        if (Cog > 64) cfg = {4, 4, 2, 2, true};        // 128 x 128
+        else if (Cog > 32) cfg = {2, 4, 2, 2, true};   // 64 x 128
+        else if (Cog > 16) cfg = {2, 2, 1, 4, true};   // 32 x 128
+        else cfg = {1, 2, 1, 4, true};                 // 16 x 128
+        const int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
+        p.span = BN + (a->K - 1) * a->dil;
+        p.span_s = p.span;
+        p.rows_max = 0;
+        p.inv_span = 1.0f / (float)p.span;
+        p.avec = 0;
+        p.wx = (const uint4*)a->wx;
+        p.wx_nmf = a->wx_nmf;
+        p.wx_nch = (int)((Cig + 31) / 32);
+        p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
+        const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
+        split_k(p, tiles, p.wx_nch);
+        lds = (size_t)2 * 3 * p.span * 64;
+        grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
+        RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
+        return RVC_OK;
+    }
+
+    if (Cog % 48 == 0 && Cog % 64 != 0) cfg = {3, 1, 1, 4, false};  // 48 x 64 (ContentVec pos_conv groups)
+    else if (Cog <= 16) cfg = {1, 4, 1, 4, false};                  // 16 x 256
+    else if (Cog <= 32) cfg = {2, 4, 1, 4, false};                  // 32 x 256
+    else if (Cog <= 64 || Cog % 128 != 0) cfg = {2, 4, 2, 2, false}; // 64 x 128 (also 192: no half-empty M tile)
+    else cfg = {4, 4, 2, 2, false};                                 // 128 x 128
     int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
 
     int maxoff = (a->K - 1) * a->dil;
@@ -401,47 +678,73 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     }
     RVC_CHECK_ARG((int64_t)rows_max * span <= 256 * NB_MAX, "conv1d: staged tile too large (rows %d x span %d)",
                   rows_max, span);
-
-    p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y; p.ws = nullptr;
-    p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout; p.ncols = ncols;
-    p.x_bstride = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
-    p.y_bstride = a->y_bstride ? a->y_bstride : a->Co * a->Lout;
-    p.res_bstride = a->res_bstride ? a->res_bstride : a->Co * a->Lout;
-    p.w_bstride = a->w_bstride;
-    p.K = a->K; p.stride = a->stride; p.dil = a->dil; p.pad = a->pad; p.groups = a->groups;
-    p.nphase = a->nphase; p.ostride = a->ostride; p.ooffset = a->ooffset;
-    p.in_act = a->in_act; p.out_act = a->out_act; p.accumulate = a->accumulate;
-    p.in_scale = a->in_scale; p.in_slope = a->in_slope; p.out_slope = a->out_slope; p.out_scale = a->out_scale;
-    p.ntoff = a->ntoff; p.wrap = a->wrap;
-    for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff ? a->toff[i] : 0;
     p.span = span;
     p.span_s = span + 1;
     p.rows_max = rows_max;
     p.inv_span = 1.0f / (float)span;
     p.avec = (Cog % 4 == 0) && (((uintptr_t)a->w & 15) == 0) && (a->w_bstride % 4 == 0);
     p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
-
     const int64_t tiles = (int64_t)p.mtiles_per_group * a->groups * ((ncols + BN - 1) / BN) * a->B * a->nphase;
-    const int nch = (int)((Cig * a->K + KCH - 1) / KCH);
-    int ks = 1;
-    if (tiles < 512 && nch >= 4) {
-        ks = (int)((512 + tiles - 1) / tiles);
-        if (ks > 16) ks = 16;
-        if (ks > nch / 2) ks = nch / 2;
-        if (ks < 1) ks = 1;
-    }
-    p.chunks_per_split = (nch + ks - 1) / ks;
-    ks = (nch + p.chunks_per_split - 1) / p.chunks_per_split;
-    p.ksplit = ks;
+    split_k(p, tiles, (int)((Cig * a->K + KCH - 1) / KCH));
     const int WS = (BM / 32) * 32 + 16 + ((BM % 32) ? 32 : 0);
     lds = (size_t)(KCH * WS + KCH) * 4 + ((size_t)rows_max * p.span_s + 4) * 4;  // +dump slot
     RVC_CHECK_ARG(lds <= 160 * 1024, "conv1d: LDS %zu too large", lds);
-    grid = dim3(cdiv(ncols, BN), (unsigned)(p.mtiles_per_group * a->groups), (unsigned)(a->B * a->nphase * ks));
+    grid = dim3(cdiv(ncols, BN), (unsigned)(p.mtiles_per_group * a->groups), (unsigned)(a->B * a->nphase * p.ksplit));
     RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
     return RVC_OK;
 }
 
+// KM weights [nphase][Ci*K][Co] -> per-lane split-bf16 fragments [nphase][K][nch][nmf][3][64] x 16 B:
+// lane l of (t, chunk, fragment mf, plane q) holds plane q of W[c = 32 chunk + 8 (l>>4) + e][m = 16 mf + (l&15)], e < 8.
+__global__ __launch_bounds__(256) void pack_x6_kernel(const float* w, int64_t total, int Ci, int K, int Co, int nch,
+                                                      int nmf, uint4* out) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    int64_t r = idx;
+    const int lane = (int)(r % 64); r /= 64;
+    const int q = (int)(r % 3); r /= 3;
+    const int mf = (int)(r % nmf); r /= nmf;
+    const int ch = (int)(r % nch); r /= nch;
+    const int t = (int)(r % K); r /= K;
+    const int64_t ph = r;
+    const int m = mf * 16 + (lane & 15);
+    uint32_t wd[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+        uint32_t hv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = ch * 32 + 8 * (lane >> 4) + 2 * e2 + u;
+            const float v = (c < Ci && m < Co) ? w[((ph * Ci + c) * K + t) * Co + m] : 0.f;
+            uint32_t h, mm, l;
+            split3(v, h, mm, l);
+            hv[u] = q == 0 ? h : (q == 1 ? mm : l);
+        }
+        wd[e2] = hv[0] | (hv[1] << 16);
+    }
+    out[idx] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+}
+
+int64_t x6_nmf(int64_t Co) { return (Co + 127) / 128 * 8; }
+
 }  // namespace
+
+extern "C" int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co) {
+    if (nphase <= 0 || Ci <= 0 || K <= 0 || Co <= 0) return -1;
+    return nphase * K * ((Ci + 31) / 32) * x6_nmf(Co) * 3 * 64 * 16;
+}
+
+extern "C" int rvc_conv1d_pack_x6(const float* w_km, int64_t nphase, int64_t Ci, int K, int64_t Co, void* out,
+                                  int* nmf_out, rvc_stream_t stream) {
+    RVC_CHECK_ARG(w_km && out && nmf_out && nphase > 0 && Ci > 0 && K > 0 && Co > 0, "pack_x6: bad args");
+    const int nch = (int)((Ci + 31) / 32), nmf = (int)x6_nmf(Co);
+    const int64_t total = nphase * K * nch * nmf * 3 * 64;
+    hipLaunchKernelGGL(pack_x6_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, w_km, total,
+                       (int)Ci, K, (int)Co, nch, nmf, (uint4*)out);
+    RVC_HIP(hipGetLastError());
+    *nmf_out = nmf;
+    return RVC_OK;
+}
 
 extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {
     ConvParams p;
@@ -468,7 +771,12 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     }
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
-    if (cfg.FM == 3) e = launch<3, 1, 1, 4>(p, grid, lds, s);
+    if (cfg.x6) {
+        if (cfg.FM == 4) e = launch_x6<4, 4, 2, 2>(p, grid, lds, s);
+        else if (cfg.WM == 2) e = launch_x6<2, 4, 2, 2>(p, grid, lds, s);
+        else if (cfg.FM == 2) e = launch_x6<2, 2, 1, 4>(p, grid, lds, s);
+        else e = launch_x6<1, 2, 1, 4>(p, grid, lds, s);
+    } else if (cfg.FM == 3) e = launch<3, 1, 1, 4>(p, grid, lds, s);
     else if (cfg.FM == 1 && cfg.FN == 4) e = launch<1, 4, 1, 4>(p, grid, lds, s);
     else if (cfg.FM == 1) e = launch<1, 2, 1, 4>(p, grid, lds, s);
     else if (cfg.WM == 1 && cfg.FN == 4) e = launch<2, 4, 1, 4>(p, grid, lds, s);

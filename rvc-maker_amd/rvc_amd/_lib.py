@@ -26,7 +26,8 @@ class Conv1dArgs(ctypes.Structure):
                 ("nphase", c_int), ("ostride", c_int), ("ooffset", c_int),
                 ("in_act", c_int), ("out_act", c_int), ("accumulate", c_int), ("_pad0", c_int),
                 ("in_scale", c_float), ("in_slope", c_float), ("out_slope", c_float), ("out_scale", c_float),
-                ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16)]
+                ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16),
+                ("wx", c_void_p), ("wx_nmf", c_int), ("_pad1", c_int)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -44,6 +45,8 @@ SIGNATURES = {
     "rvc_version": [],
     "rvc_conv1d": [POINTER(Conv1dArgs), c_void_p, c_int64, c_void_p],
     "rvc_conv1d_workspace_bytes": [POINTER(Conv1dArgs)],
+    "rvc_conv1d_x6_bytes": [c_int64, c_int64, c_int, c_int64],
+    "rvc_conv1d_pack_x6": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
     "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],
     "rvc_attention": [POINTER(AttnArgs), c_void_p, c_int64, c_void_p],
     "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
@@ -72,7 +75,7 @@ SIGNATURES = {
     "rvc_phone_upsample": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_peak_normalize": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
 }
-_RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64,
+_RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64}
 
 _lib = None

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -50,8 +51,29 @@ def pack_convT(w: torch.Tensor, u: int) -> tuple[torch.Tensor, int]:
     return out.reshape(u, Ci * T, Co).contiguous(), T
 
 
+# Split-bf16 engine switch (the f32-MFMA engine runs when off); RVC_AMD_X6=0 disables it.
+X6 = os.environ.get("RVC_AMD_X6", "1") != "0"
+
+
+def pack_x6(w_km: torch.Tensor, nphase: int, Ci: int, K: int, Co: int):
+    """Device KM weights [nphase][Ci*K][Co] -> split-bf16 fragment image for the x6 engine
+    (rvc_conv1d_pack_x6), or (None, 0) when the engine is off."""
+    if not X6:
+        return None, 0
+    lib = _lib.load()
+    nbytes = lib.rvc_conv1d_x6_bytes(nphase, Ci, K, Co)
+    if nbytes <= 0:
+        raise ValueError("pack_x6: bad shape")
+    out = torch.empty(nbytes, dtype=torch.uint8, device=w_km.device)
+    nmf = ctypes.c_int(0)
+    check(lib.rvc_conv1d_pack_x6(_p(w_km), nphase, Ci, K, Co, ctypes.c_void_p(out.data_ptr()), ctypes.byref(nmf),
+                                 _stream()), "conv1d_pack_x6")
+    return out, nmf.value
+
+
 class Conv:
-    """A packed Conv1d (weight [Co, Ci/g, K], bias [Co]) resident on the device."""
+    """A packed Conv1d (weight [Co, Ci/g, K], bias [Co]) resident on the device.  Ungrouped convs also
+    carry the split-bf16 image, which the library uses for stride-1 calls."""
 
     def __init__(self, w, b=None, groups=1, device="cuda"):
         self.Co, self.Cig, self.K = (int(s) for s in w.shape)
@@ -59,10 +81,11 @@ class Conv:
         self.Ci = self.Cig * groups
         self.w = pack_km(w.float(), groups).to(device)
         self.b = b.float().to(device) if b is not None else None
+        self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co) if groups == 1 else (None, 0)
 
     def __call__(self, x, Lout=None, stride=1, pad=0, dil=1, **kw):
         return conv1d(x, self.w, self.Ci, self.Co, self.K, bias=self.b, stride=stride, pad=pad, dil=dil,
-                      groups=self.groups, Lout=Lout, **kw)
+                      groups=self.groups, Lout=Lout, wx=self.wx, wx_nmf=self.wx_nmf, **kw)
 
 
 class ConvT:
@@ -74,6 +97,7 @@ class ConvT:
         wp, self.T = pack_convT(w.float(), u)
         self.w = wp.to(device)
         self.b = b.float().to(device)
+        self.wx, self.wx_nmf = pack_x6(self.w, u, self.Ci, self.T, self.Co)
 
     def out_len(self, Lin):
         return (Lin - 1) * self.u - 2 * self.pad + self.K
@@ -84,7 +108,7 @@ class ConvT:
         ncols = (Lout - 1 + self.pad) // self.u + 1
         return conv1d(x, self.w, Ci, self.Co, self.T, bias=self.b, stride=1, pad=self.T - 1, dil=1, Lout=Lout,
                       ncols=ncols, nphase=self.u, ostride=self.u, ooffset=-self.pad, out=out,
-                      flops=2.0 * B * Ci * self.Co * self.K * Lin, **kw)
+                      flops=2.0 * B * Ci * self.Co * self.K * Lin, wx=self.wx, wx_nmf=self.wx_nmf, **kw)
 
 
 LAST_CONV_FLOPS = 0.0
@@ -111,7 +135,7 @@ def _shape3(x):
 def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, groups=1, Lout=None, ncols=0,
            nphase=1, ostride=1, ooffset=0, out=None, res=None, in_act=ACT_NONE, in_slope=0.0, in_scale=1.0,
            out_act=ACT_NONE, out_slope=0.0, out_scale=1.0, accumulate=False, B=None, Lin=None, x_bstride=0,
-           w_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, flops=None):
+           w_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, flops=None, wx=None, wx_nmf=0):
     """y = conv(pre(x)) with fused epilogue.  x: [B][Ci][Lin] device f32 (t contiguous).
 
     ``flops`` is the launch's ALGORITHMIC FLOP count for roofline accounting (recorded in
@@ -157,6 +181,8 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
         for i, v in enumerate(toff):
             a.toff[i] = int(v)
     a.wrap = wrap
+    if wx is not None:
+        a.wx, a.wx_nmf = ctypes.c_void_p(wx.data_ptr()), wx_nmf
     if flops is None:
         valid = (Lout // wrap - 2) * (wrap - 2) if wrap else (ncols or Lout) * nphase
         flops = 2.0 * B * Co * Cig * K * min(valid, Lout)

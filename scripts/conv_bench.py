@@ -23,12 +23,14 @@ SHAPES = [  # C, K, dil, L
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", type=str, default="", help="comma list of shape indices")
     args = ap.parse_args()
     from rvc_amd import ops
     print("lib:", ops._lib.LIB_PATH)
     g = torch.Generator().manual_seed(0)
     tot_ms = tot_fl = 0.0
-    for C, K, d, L in SHAPES:
+    shapes = [SHAPES[int(i)] for i in args.only.split(",")] if args.only else SHAPES
+    for C, K, d, L in shapes:
         w = torch.randn(C, C, K, generator=g) / (C * K) ** 0.5
         conv = ops.Conv(w, torch.randn(C, generator=g), device="cuda")
         x = torch.randn(C, L, generator=g).cuda()

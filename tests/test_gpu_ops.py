@@ -31,6 +31,15 @@ def ops():
     return o
 
 
+@pytest.fixture(params=[False, True], ids=["f32mfma", "x6"])
+def engine(request, ops):
+    """Run a conv test on the f32-MFMA engine and on the split-bf16 (x6) engine."""
+    old = ops.X6
+    ops.X6 = request.param
+    yield request.param
+    ops.X6 = old
+
+
 CONV_CASES = [
     # Ci, Co, K, stride, dil, pad, groups, L
     (32, 32, 3, 1, 1, 1, 1, 5000),
@@ -47,11 +56,15 @@ CONV_CASES = [
     (32, 1, 7, 1, 1, 3, 1, 3000),
     (192, 21, 1, 1, 1, 0, 1, 500),
     (256, 4608, 1, 1, 1, 0, 1, 1),
+    (64, 64, 11, 1, 5, 25, 1, 4000),     # generator ResBlock shape (dilated)
+    (40, 72, 3, 1, 1, 1, 1, 777),        # ragged channel chunks / fragments
+    (768, 3072, 1, 1, 1, 0, 1, 1599),    # ContentVec fc1
+    (256, 256, 7, 1, 1, 3, 1, 300),      # ragged N tile
 ]
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv1d(ops, case):
+def test_conv1d(ops, engine, case):
     Ci, Co, K, s, d, p, g, L = case
     x = torch.randn(Ci, L, generator=gen(1))
     w = torch.randn(Co, Ci // g, K, generator=gen(2)) / math.sqrt(Ci // g * K)
@@ -62,7 +75,7 @@ def test_conv1d(ops, case):
     close(y, ref)
 
 
-def test_conv1d_fused_epilogue(ops):
+def test_conv1d_fused_epilogue(ops, engine):
     Ci, Co, K, L = 64, 64, 5, 3000
     x = torch.randn(Ci, L, generator=gen(4))
     w = torch.randn(Co, Ci, K, generator=gen(5)) / math.sqrt(Ci * K)
@@ -81,7 +94,7 @@ def test_conv1d_fused_epilogue(ops):
 
 @pytest.mark.parametrize("u,k,ci,co,L", [(12, 24, 64, 32, 300), (10, 20, 64, 32, 300), (10, 16, 64, 32, 200),
                                           (2, 4, 32, 16, 2000), (8, 16, 64, 32, 100)])
-def test_conv_transpose(ops, u, k, ci, co, L):
+def test_conv_transpose(ops, engine, u, k, ci, co, L):
     x = torch.randn(ci, L, generator=gen(10))
     w = torch.randn(ci, co, k, generator=gen(11)) / math.sqrt(ci * k / u)
     b = torch.randn(co, generator=gen(12))

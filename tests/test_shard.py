@@ -1,0 +1,64 @@
+"""Multi-rank utterance sharding + waveform gather, world_size 2 over gloo on CPU."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from rvc_amd.shard import gather_waveforms, shard_utterances
+
+
+def test_shard_longest_first_balances():
+    lengths = [30, 10, 25, 5, 20, 15]
+    shards = shard_utterances(lengths, 2)
+    assert sorted(sum(shards, [])) == list(range(6))
+    loads = [sum(lengths[i] for i in s) for s in shards]
+    assert abs(loads[0] - loads[1]) <= 5
+    assert shard_utterances(lengths, 2) == shards  # deterministic
+    assert shard_utterances([7], 4) == [[0], [], [], []]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, lengths, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = shard_utterances(lengths, world)[rank]
+        # each "utterance" output is a deterministic ramp identifying it
+        outs = [torch.arange(lengths[i], dtype=torch.float32) + 1000 * i for i in mine]
+        got = gather_waveforms(outs, dist, dst=0)
+        if rank == 0:
+            q.put([[(int(p[0]) // 1000 if p.numel() else -1, p.numel(), float(p.sum())) for p in parts]
+                   for parts in got])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gather_waveforms_world2_gloo():
+    lengths = [300, 120, 250, 7, 199]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lengths, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = shard_utterances(lengths, world)
+    for r in range(world):
+        assert len(res[r]) == len(shards[r])
+        for (uid, n, s), i in zip(res[r], shards[r]):
+            assert uid == i and n == lengths[i]
+            assert s == pytest.approx(sum(range(lengths[i])) + 1000 * i * lengths[i])
