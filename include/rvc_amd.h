@@ -91,6 +91,8 @@ typedef struct rvc_conv1d_args {
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned
  * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args). */
 int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a);
+/* Which engine a call would run on: 0 = f32 MFMA, 1 = split-bf16 (x6); -1 on bad args. */
+int rvc_conv1d_engine(const rvc_conv1d_args* a);
 int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* Pack KM weights [nphase][Ci*K][Co] (one group) for the split-bf16 engine: out must hold
  * rvc_conv1d_x6_bytes(nphase, Ci, K, Co) bytes; *nmf_out receives wx_nmf. */

@@ -383,18 +383,18 @@ RVC_DEV void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
     l = __builtin_bit_cast(uint16_t, bl);
 }
 
-constexpr int X6_NI = 4;  // staged (position, 8-channel group) items per loader thread: 4 * span <= 1024
+constexpr int X6_NI_MAX = 6;  // staged (position, 8-channel group) items per loader thread: 4 * span <= 256 NI
 
 // Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
 // input prefetch never wait on each other.  One workgroup barrier per 32-channel chunk hands the
 // next staged X buffer (double-buffered in LDS) to the compute waves.
-template <int FM, int FN, int WM, int WN>
+template <int FM, int FN, int WM, int WN, int X6_NI>
 __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4, "4 compute waves");
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
-    extern __shared__ uint4 xs[];  // [2 buffers][3 planes][span][4 x 16 B]
+    extern __shared__ uint4 xs[];  // [2 buffers][span][3 planes][4 x 16 B]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int zb = blockIdx.z;
     const int split = zb % p.ksplit;
@@ -465,10 +465,10 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
                         lw[e2] = l2[0] | (l2[1] << 16);
                     }
                     const int pos = ipos[it];
-                    const int slot = pos * 4 + (ig8[it] ^ ((pos >> 2) & 3));
+                    const int slot = pos * 12 + (ig8[it] ^ ((pos >> 2) & 3));
                     dst[slot] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-                    dst[span * 4 + slot] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
-                    dst[2 * span * 4 + slot] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                    dst[slot + 4] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+                    dst[slot + 8] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
                 }
             }
         };
@@ -495,12 +495,15 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
     const uint4* wxp = p.wx + (int64_t)phase * K * nch * nmf * 3 * 64;
     const int mf0 = m0g / 16 + wm * FM;
     auto aload = [&](int s, uint4 (&a)[3][FM]) __attribute__((always_inline)) {
+        // wave-uniform fragment base (scalar registers) + one per-lane offset: saddr loads, no
+        // per-fragment 64-bit address registers
         const int ch = s / K, t = s - ch * K;
-        const uint4* src = wxp + ((int64_t)((t * nch + ch) * nmf + mf0) * 3) * 64 + lane;
+        const int frag0 = __builtin_amdgcn_readfirstlane((t * nch + ch) * nmf + mf0);
+        const uint4* src = wxp + (int64_t)frag0 * 3 * 64;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) a[q][i] = src[(i * 3 + q) * 64];
+            for (int q = 0; q < 3; ++q) a[q][i] = src[(i * 3 + q) * 64 + lane];
     };
     floatx4 acc[FM][FN];
 #pragma unroll
@@ -513,10 +516,10 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
         uint4 bq[3][FN];
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-            const int pos = pb + 16 * j + t * p.dil;
-            const int slot = pos * 4 + (lg ^ ((pos >> 2) & 3));
+            const int pos = pb + 16 * j + tap_off(p, t);
+            const int slot = pos * 12 + (lg ^ ((pos >> 2) & 3));
 #pragma unroll
-            for (int q = 0; q < 3; ++q) bq[q][j] = xbuf[q * span * 4 + slot];
+            for (int q = 0; q < 3; ++q) bq[q][j] = xbuf[slot + 4 * q];
         }
         // six passes, each over all FM x FN accumulators (no back-to-back dependent MFMAs)
         constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
@@ -570,7 +573,9 @@ hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
 
 template <int FM, int FN, int WM, int WN>
 hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN>), grid, dim3(512), lds, s, p);
+    // loader items per thread sized to the staged span (unused items would still issue loads)
+    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3>), grid, dim3(512), lds, s, p);
+    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6>), grid, dim3(512), lds, s, p);
     return hipGetLastError();
 }
 
@@ -607,9 +612,17 @@ void split_k(ConvParams& p, int64_t tiles, int nch) {
 
 constexpr int X6_BN = 128;
 
+int max_tap_off(const rvc_conv1d_args* a) {
+    if (!a->ntoff) return (a->K - 1) * a->dil;
+    int m = 0;
+    for (int i = 0; i < a->ntoff && i < 16; ++i) m = a->toff[i] > m ? a->toff[i] : m;
+    return m;
+}
+
 bool x6_eligible(const rvc_conv1d_args* a) {
-    return a->wx && a->stride == 1 && a->groups == 1 && a->ntoff == 0 && a->w_bstride == 0 &&
-           X6_BN + (a->K - 1) * a->dil <= 256 && a->wx_nmf % 8 == 0 && (int64_t)a->wx_nmf * 16 >= a->Co;
+    return a->wx && a->stride == 1 && a->groups == 1 && a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) &&
+           a->K <= 16 && X6_BN + max_tap_off(a) <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
+           (int64_t)a->wx_nmf * 16 >= a->Co;
 }
 
 int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& lds) {
@@ -625,6 +638,10 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     const int64_t Cig = a->Ci / a->groups;
     const int64_t ncols = a->ncols > 0 ? a->ncols : a->Lout;
     fill_common(a, p);
+    if (a->ntoff) {
+        RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
+        for (int i = 0; i < a->K; ++i) RVC_CHECK_ARG(a->toff[i] >= 0, "conv1d: negative tap offset");
+    }
 
     if (x6_eligible(a)) {
         cfg.x6 = true;
@@ -633,7 +650,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         else if (Cog > 16) cfg = {2, 2, 1, 4, true};   // 32 x 128
         else cfg = {1, 2, 1, 4, true};                 // 16 x 128
         const int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
-        p.span = BN + (a->K - 1) * a->dil;
+        p.span = BN + max_tap_off(a);
         p.span_s = p.span;
         p.rows_max = 0;
         p.inv_span = 1.0f / (float)p.span;
@@ -657,15 +674,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     else cfg = {4, 4, 2, 2, false};                                 // 128 x 128
     int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
 
-    int maxoff = (a->K - 1) * a->dil;
-    if (a->ntoff) {
-        RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
-        maxoff = 0;
-        for (int i = 0; i < a->K; ++i) {
-            RVC_CHECK_ARG(a->toff[i] >= 0, "conv1d: negative tap offset");
-            if (a->toff[i] > maxoff) maxoff = a->toff[i];
-        }
-    }
+    const int maxoff = max_tap_off(a);
     // rows touched by a chunk of KCH consecutive k starting at a multiple of KCH
     int rows_max = (KCH % a->K == 0) ? KCH / a->K : (KCH - 1) / a->K + 2;
     if (rows_max > Cig) rows_max = (int)Cig;
@@ -744,6 +753,15 @@ extern "C" int rvc_conv1d_pack_x6(const float* w_km, int64_t nphase, int64_t Ci,
     RVC_HIP(hipGetLastError());
     *nmf_out = nmf;
     return RVC_OK;
+}
+
+extern "C" int rvc_conv1d_engine(const rvc_conv1d_args* a) {
+    ConvParams p;
+    Cfg cfg;
+    dim3 grid;
+    size_t lds;
+    if (plan(a, p, cfg, grid, lds) != RVC_OK) return -1;
+    return cfg.x6 ? 1 : 0;
 }
 
 extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {

@@ -45,6 +45,7 @@ SIGNATURES = {
     "rvc_version": [],
     "rvc_conv1d": [POINTER(Conv1dArgs), c_void_p, c_int64, c_void_p],
     "rvc_conv1d_workspace_bytes": [POINTER(Conv1dArgs)],
+    "rvc_conv1d_engine": [POINTER(Conv1dArgs)],
     "rvc_conv1d_x6_bytes": [c_int64, c_int64, c_int, c_int64],
     "rvc_conv1d_pack_x6": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
     "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],

@@ -112,6 +112,7 @@ class ConvT:
 
 
 LAST_CONV_FLOPS = 0.0
+LAST_CONV_ENGINE = 0  # 0 = f32 MFMA engine, 1 = split-bf16 (x6) engine
 _WS = {}
 
 
@@ -140,7 +141,7 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
 
     ``flops`` is the launch's ALGORITHMIC FLOP count for roofline accounting (recorded in
     LAST_CONV_FLOPS); the default is 2*B*Co*(Ci/g)*K*(valid outputs)."""
-    global LAST_CONV_FLOPS
+    global LAST_CONV_FLOPS, LAST_CONV_ENGINE
     if B is None:
         B, Cx, Lx = _shape3(x)
         if Lin is None:
@@ -192,6 +193,7 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
     if need < 0:
         raise RuntimeError(f"rvc_amd: conv1d plan failed: {lib.rvc_last_error().decode()}")
     ws = _workspace(out.device, need) if need else None
+    LAST_CONV_ENGINE = lib.rvc_conv1d_engine(ctypes.byref(a))
     check(lib.rvc_conv1d(ctypes.byref(a), _p(ws), need, _stream()), "conv1d")
     return out
 

@@ -43,6 +43,7 @@ class _Conv2d:
         self.Co, self.Ci, self.k = Co, Ci, kh
         self.w = pack_km(w.reshape(Co, Ci, kh * kw).float()).to(device)
         self.b = b.float().to(device) if b is not None else None
+        self.wx, self.wx_nmf = ops.pack_x6(self.w, 1, Ci, kh * kw, Co)
 
     def __call__(self, x, H, W, out, **kw):
         wrap = W + 2
@@ -53,7 +54,7 @@ class _Conv2d:
         else:
             toff, pad = [0], 0
         return ops.conv1d(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L, B=1,
-                          out=out, toff=toff, wrap=wrap, **kw)
+                          out=out, toff=toff, wrap=wrap, wx=self.wx, wx_nmf=self.wx_nmf, **kw)
 
 
 class _ConvT2d:
@@ -72,17 +73,18 @@ class _ConvT2d:
             for px in (0, 1):
                 taps = [(ky, kx, dy, dx) for ky, dy in self.TAPS[py] for kx, dx in self.TAPS[px]]
                 wp = torch.stack([wf[:, :, ky, kx].t() for ky, kx, _, _ in taps], dim=-1)  # [Co, Ci, ntap]
-                self.phases.append((pack_km(wp.float()).to(device), [(dy, dx) for _, _, dy, dx in taps]))
+                wkm = pack_km(wp.float()).to(device)
+                self.phases.append((wkm, [(dy, dx) for _, _, dy, dx in taps]) + ops.pack_x6(wkm, 1, Ci, len(taps), Co))
 
     def __call__(self, x, H, W, out_cat):
         """x bordered [Ci][H+2][W+2] -> first Co channels of bordered out_cat [*][2H+2][2W+2]."""
         wrap = W + 2
         L = (H + 2) * wrap
         ph = torch.zeros(4, self.Co, H + 2, W + 2, device=x.device)
-        for i, (wp, taps) in enumerate(self.phases):
+        for i, (wp, taps, wx, wx_nmf) in enumerate(self.phases):
             toff = [dy * wrap + dx for dy, dx in taps]
             ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, B=1, out=ph[i],
-                       toff=toff, wrap=wrap, out_act=ACT_RELU)
+                       toff=toff, wrap=wrap, out_act=ACT_RELU, wx=wx, wx_nmf=wx_nmf)
         ops.interleave4(ph, out_cat, self.Co, H, W)
 
 

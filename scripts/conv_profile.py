@@ -23,7 +23,7 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=30.0)
-    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--top", type=int, default=60)
     args = ap.parse_args()
     from rvc_amd import ops, synthetic
     dev = "cuda:0"
@@ -44,7 +44,7 @@ def main():
         Lin = kw.get("Lin") or x.shape[-1]
         key = (B, Ci, Co, K, kw.get("stride", 1), kw.get("dil", 1), kw.get("groups", 1), Lin,
                kw.get("nphase", 1), "2d" if kw.get("wrap") else "", "res" if kw.get("res") is not None else "",
-               "acc" if kw.get("accumulate") else "")
+               "acc" if kw.get("accumulate") else "", "x6" if ops.LAST_CONV_ENGINE == 1 else "f32")
         rec.append((key, e0, e1, ops.LAST_CONV_FLOPS))
         return out
 
@@ -61,12 +61,12 @@ def main():
     tot_ms = sum(a[1] for a in agg.values())
     tot_fl = sum(a[2] for a in agg.values())
     print(f"{len(rec)} launches, {tot_ms:.2f} ms, {tot_fl / 1e9:.1f} GFLOP, {tot_fl / tot_ms / 1e9:.1f} TFLOP/s")
-    print(f"{'B':>3} {'Ci':>5} {'Co':>5} {'K':>3} {'s':>2} {'d':>2} {'g':>3} {'Lin':>8} {'ph':>2} {'flags':>10} "
+    print(f"{'B':>3} {'Ci':>5} {'Co':>5} {'K':>3} {'s':>2} {'d':>2} {'g':>3} {'Lin':>8} {'ph':>2} {'flags':>14} "
           f"{'calls':>5} {'ms':>8} {'us/call':>8} {'GFLOP':>8} {'TF/s':>6} {'%time':>6}")
     for key, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: args.top]:
-        B, Ci, Co, K, s, d, g, Lin, ph, f2d, fres, facc = key
-        flags = ",".join(x for x in (f2d, fres, facc) if x)
-        print(f"{B:>3} {Ci:>5} {Co:>5} {K:>3} {s:>2} {d:>2} {g:>3} {Lin:>8} {ph:>2} {flags:>10} {n:>5} {ms:>8.3f} "
+        B, Ci, Co, K, s, d, g, Lin, ph, f2d, fres, facc, eng = key
+        flags = ",".join(x for x in (eng, f2d, fres, facc) if x)
+        print(f"{B:>3} {Ci:>5} {Co:>5} {K:>3} {s:>2} {d:>2} {g:>3} {Lin:>8} {ph:>2} {flags:>14} {n:>5} {ms:>8.3f} "
               f"{ms / n * 1e3:>8.1f} {fl / 1e9:>8.2f} {fl / ms / 1e9:>6.1f} {100 * ms / tot_ms:>6.1f}")
 
 

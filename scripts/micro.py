@@ -7,6 +7,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rvc-maker_amd"))
+sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -58,5 +59,27 @@ def main():
         print(f"conv Ci={Ci} Co={Co} K={K} L={L}: {us:9.1f} us  {2.0 * Ci * Co * K * L / us / 1e6:6.1f} TFLOP/s")
 
 
+def branches():
+    """Critical-path pieces of one 30 s pipeline step, each timed alone."""
+    import bench
+    from rvc_amd import synthetic
+    vc, hub, net_g = bench.build_models("cuda:0")
+    audio = torch.from_numpy(synthetic.synthetic_audio(30.0, seed=1000)).cuda()
+    xp, _ = vc.filt(audio, vc.t_pad)
+    print(f"filtfilt+pad:      {timeit(lambda: vc.filt(audio, vc.t_pad), 5):9.1f} us")
+    print(f"ContentVec feats:  {timeit(lambda: vc.features_device(hub, xp, 'v2'), 5):9.1f} us")
+    print(f"RMVPE f0:          {timeit(lambda: vc._rmvpe().f0_device(xp, 0.03, 0.0), 5):9.1f} us")
+    feats = vc.features_device(hub, xp, "v2")
+    coarse, pitchf, _ = vc._rmvpe().f0_device(xp, 0.03, 0.0)
+    p_len = xp.numel() // 160
+    fn = lambda: vc.voice_conversion_device(hub, net_g, 0, xp, coarse[:p_len], pitchf[:p_len], "v2", 0.33, 0,  # noqa
+                                            feats=feats)
+    print(f"synth (enc+flow+gen): {timeit(fn, 3):9.1f} us")
+    print(f"full pipeline_device: {timeit(lambda: vc.pipeline_device(hub, net_g, 0, audio, 0, 'v2', 0.33), 3):9.1f} us")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "branches":
+        branches()
+        sys.exit(0)
     main()
