@@ -200,6 +200,23 @@ int rvc_phone_upsample(const float* feats, const float* feats0, const float* pit
                        int64_t T, float protect, rvc_stream_t stream);
 int rvc_peak_normalize(float* x, int64_t n, void* ws, float* scale_out, rvc_stream_t stream);
 
+/* ------------------------------------------------------------------ FAISS IVF-Flat retrieval
+ * Replaces faiss IndexIVFFlat(L2).search(feats, k=8) + the blend of convert.py:349-359.
+ * Queries (query i, dim c) live at q[c*cs + i*qs] (channels-first [d][nq]: cs = nq, qs = 1).
+ * centT: centroids transposed [d][nlist]; inverted lists in CSR form: list_off [nlist+1],
+ * codes [ntotal][d] (list-major), ids [ntotal].  Distances are computed in f64; results are
+ * D f32 [nq][k] (squared L2), I int64 [nq][k], missing results (FLT_MAX, -1) as in faiss.
+ * ws: rvc_ivf_coarse_ws_bytes(nq, nlist) bytes; probes: int64 [nq][nprobe] scratch/out. */
+int64_t rvc_ivf_coarse_ws_bytes(int64_t nq, int64_t nlist);
+int rvc_ivf_search(const float* q, int64_t nq, int64_t d, int64_t cs, int64_t qs, const float* centT, int64_t nlist,
+                   int nprobe, const int64_t* list_off, const float* codes, const int64_t* ids, int k, void* ws,
+                   int64_t ws_bytes, int64_t* probes, float* D, int64_t* I, rvc_stream_t stream);
+/* out = (sum_j big[I_j] * w_j / sum w) * index_rate + (1 - index_rate) * feats, w = (1/D)^2, in the
+ * f32 operation order of the reference's numpy/torch code; big = reconstruct_n(0, ntotal) [ntotal][d]. */
+int rvc_ivf_blend(const float* feats, int64_t nq, int64_t d, int64_t fcs, int64_t fqs, const float* D, const int64_t* I,
+                  int k, const float* big, int64_t ntotal, double index_rate, float* out, int64_t ocs, int64_t oqs,
+                  rvc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

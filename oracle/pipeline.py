@@ -1,8 +1,9 @@
 """Oracle: ``VC.pipeline`` (main/inference/convert.py:388-458) on torch-CPU / numpy / scipy.
 
-TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  f0 method "rmvpe", no
-FAISS index (retrieval is a §8(f) "next" row), volume_envelope = 1, no f0
-file, no autotune.  Noise is injected through ``noise(seg, name, shape)``.
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  f0 method "rmvpe", optional
+IVF-Flat retrieval through oracle.ivf (faiss itself is absent: parity unpinned),
+volume_envelope = 1, no f0 file, no autotune.  Noise is injected through
+``noise(seg, name, shape)``.
 """
 from __future__ import annotations
 
@@ -59,8 +60,10 @@ def segment_points(audio: np.ndarray, c: Consts):
     return opt_ts
 
 
-def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, z_noise, sine_noise, trace=None):
-    """VC.voice_conversion (convert.py:328-386), ``.pt`` embedder, ``.pth`` model, no index."""
+def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, z_noise, sine_noise, trace=None,
+                     index=None, big_npy=None, index_rate=0.0):
+    """VC.voice_conversion (convert.py:328-386), ``.pt`` embedder, ``.pth`` model; ``index`` is an
+    ``IVFFlatIndex`` searched by the numpy restatement in ``oracle.ivf`` (convert.py:349-359)."""
     window = 160
     feats = torch.from_numpy(audio0).float().view(1, -1)
     with torch.no_grad():
@@ -70,6 +73,13 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
             trace["feats"] = feats.clone()
         if protect < 0.5:
             feats0 = feats.clone()
+        if index is not None and big_npy is not None and index_rate != 0:
+            from . import ivf
+            npy = feats[0].cpu().numpy()
+            D, I = ivf.search(index, npy, k=8)
+            feats = torch.from_numpy(ivf.blend(npy, D, I, big_npy, index_rate)).unsqueeze(0)
+            if trace is not None:
+                trace.update(ivf_D=D, ivf_I=I)
         feats = F.interpolate(feats.permute(0, 2, 1), scale_factor=2).permute(0, 2, 1)
         if protect < 0.5:
             feats0 = F.interpolate(feats0.permute(0, 2, 1), scale_factor=2).permute(0, 2, 1)
@@ -92,7 +102,8 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
     return o[0, 0].numpy()
 
 
-def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None):
+def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None, index=None,
+             index_rate=0.0):
     """VC.pipeline (convert.py:388-458): f0 = rmvpe, no index, volume_envelope = 1.
 
     noise(seg_index, name, shape) -> torch tensor for "z" [1, 192, T] and "sine" [1, T*upp, 1]."""
@@ -106,6 +117,7 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
     audio_opt = []
     audio_pad = np.pad(audio, (c.t_pad, c.t_pad), mode="reflect")
     sid_t = torch.tensor(sid).unsqueeze(0).long()
+    big_npy = index.reconstruct_n(0, index.ntotal) if index is not None and index_rate != 0 else None
     p_len = audio_pad.shape[0] // c.window
     f0 = rm.infer_from_audio(Wr, mel_basis, audio_pad, thred=0.03)
     pitch_c, pitchf = coarse_f0(f0, pitch, c)
@@ -120,7 +132,8 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
         T = min(a0.shape[0] // c.window, 2 * cv.frames(a0.shape[0]))
         tr = {} if trace is not None else None
         out = voice_conversion(Wc, Ws, cfg, sid_t, a0, pch, pchf, version, protect,
-                               noise(seg, "z", (1, cfg[2], T)), noise(seg, "sine", (1, T * upp, 1)), tr)
+                               noise(seg, "z", (1, cfg[2], T)), noise(seg, "sine", (1, T * upp, 1)), tr,
+                               index=index, big_npy=big_npy, index_rate=index_rate)
         if trace is not None:
             trace.setdefault("segments", []).append(tr)
         return out[c.t_pad_tgt: -c.t_pad_tgt]

@@ -1,0 +1,245 @@
+// FAISS IVF-Flat (L2) search + the reference's retrieval blend (convert.py:349-359, 392-399;
+// index built by create_index.py:66-83 as IVF{n},Flat with nprobe 1, searched with k = 8).
+//
+//   ivf_coarse_kernel   exact (f64) squared distances of every query to every centroid,
+//                       written to a [nq][nlist] workspace
+//   ivf_select_kernel   per query (one wave): the nprobe nearest lists, ties by list id
+//   ivf_scan_kernel     per query (one wave): exhaustive L2 scan of the probed lists in f64,
+//                       top-k by (distance, id); missing results are (FLT_MAX, -1) as in faiss
+//   ivf_blend_kernel    weight = (1/D)^2 normalised (numpy's 8-way pairwise row sum), then
+//                       sum_j big[I_j] * w_j sequentially, times index_rate, plus (1 - rate) feats
+//                       -- f32, contraction off, the operation order of the numpy/torch code
+//
+// Queries and features are addressed (query i, dim c) at base[c * cs + i * qs], so the
+// channels-first [C][T] activations of the pipeline are read in place.
+#include <float.h>
+
+#include "rvc_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+constexpr int KMAX = 16;
+constexpr int QB = 8;  // queries per coarse block
+
+// grid (cdiv(nq, QB), cdiv(nlist, 256)); centT is [d][nlist] (transposed centroids, coalesced)
+__global__ __launch_bounds__(256) void ivf_coarse_kernel(const float* q, int64_t nq, int d, int64_t cs, int64_t qs,
+                                                         const float* centT, int64_t nlist, double* dist) {
+    extern __shared__ float qsh[];  // [QB][d]
+    const int64_t q0 = (int64_t)blockIdx.x * QB;
+    for (int i = threadIdx.x; i < QB * d; i += 256) {
+        const int qi = i / d, c = i - qi * d;
+        const int64_t qq = q0 + qi < nq ? q0 + qi : nq - 1;
+        qsh[i] = q[c * cs + qq * qs];
+    }
+    __syncthreads();
+    const int64_t l = (int64_t)blockIdx.y * 256 + threadIdx.x;
+    if (l >= nlist) return;
+    double acc[QB];
+#pragma unroll
+    for (int i = 0; i < QB; ++i) acc[i] = 0.0;
+    for (int c = 0; c < d; ++c) {
+        const double x = (double)centT[(int64_t)c * nlist + l];
+#pragma unroll
+        for (int i = 0; i < QB; ++i) {
+            const double t = (double)qsh[i * d + c] - x;
+            acc[i] = fma(t, t, acc[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < QB; ++i)
+        if (q0 + i < nq) dist[(q0 + i) * nlist + l] = acc[i];
+}
+
+// (d, id) lexicographic "a before b"
+__device__ __forceinline__ bool before(double da, int64_t ia, double db, int64_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+// one wave per query: nprobe passes of a wave-wide argmin over the lists not yet taken
+__global__ __launch_bounds__(64) void ivf_select_kernel(const double* dist, int64_t nq, int64_t nlist, int nprobe,
+                                                        int64_t* probes) {
+    const int64_t qi = blockIdx.x;
+    const int lane = threadIdx.x;
+    const double* row = dist + qi * nlist;
+    double taken_d = -1.0;
+    int64_t taken_i = -1;
+    for (int p = 0; p < nprobe; ++p) {
+        double bd = INFINITY;
+        int64_t bi = INT64_MAX;
+        for (int64_t l = lane; l < nlist; l += 64) {
+            const double v = row[l];
+            // strictly after the last taken (d, id) pair
+            if (before(taken_d, taken_i, v, l) && before(v, l, bd, bi)) {
+                bd = v;
+                bi = l;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(bd, o, 64);
+            const int64_t oi = __shfl_xor(bi, o, 64);
+            if (before(od, oi, bd, bi)) {
+                bd = od;
+                bi = oi;
+            }
+        }
+        if (lane == 0) probes[qi * nprobe + p] = bi < nlist ? bi : -1;
+        taken_d = bd;
+        taken_i = bi;
+    }
+}
+
+// one wave per query; lanes split the dimensions, every lane keeps the same top-k list
+__global__ __launch_bounds__(64) void ivf_scan_kernel(const float* q, int64_t nq, int d, int64_t cs, int64_t qs,
+                                                      const int64_t* probes, int nprobe, const int64_t* list_off,
+                                                      const float* codes, const int64_t* ids, int k, float* D,
+                                                      int64_t* I) {
+    const int64_t qi = blockIdx.x;
+    const int lane = threadIdx.x;
+    constexpr int DPL = 16;  // dims per lane (d <= 1024)
+    float qv[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) {
+        const int c = lane + 64 * j;
+        qv[j] = c < d ? q[c * cs + qi * qs] : 0.f;
+    }
+    double td[KMAX];
+    int64_t ti[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        td[j] = INFINITY;
+        ti[j] = -1;
+    }
+    for (int p = 0; p < nprobe; ++p) {
+        const int64_t li = probes[qi * nprobe + p];
+        if (li < 0) continue;
+        for (int64_t v = list_off[li]; v < list_off[li + 1]; ++v) {
+            const float* x = codes + v * d;
+            double part = 0.0;
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) {
+                const int c = lane + 64 * j;
+                if (c < d) {
+                    const double t = (double)qv[j] - (double)x[c];
+                    part = fma(t, t, part);
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            // every lane holds the same sum (xor butterfly): insert into the sorted top-k
+            const int64_t id = ids[v];
+            if (before(part, id, td[k - 1], ti[k - 1])) {
+                double cd = part;
+                int64_t ci = id;
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if (j < k && before(cd, ci, td[j], ti[j])) {
+                        const double sd = td[j];
+                        const int64_t si = ti[j];
+                        td[j] = cd;
+                        ti[j] = ci;
+                        cd = sd;
+                        ci = si;
+                    }
+                }
+            }
+        }
+    }
+    if (lane < k) {
+        double vd = 0.0;
+        int64_t vi = -1;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if (j == lane) {
+                vd = td[j];
+                vi = ti[j];
+            }
+        D[qi * k + lane] = vi < 0 ? FLT_MAX : (float)vd;
+        I[qi * k + lane] = vi;
+    }
+}
+
+// numpy add.reduce over a contiguous row of n <= 8 f32 (pairwise: 8-way blocks, else sequential)
+__device__ __forceinline__ float np_rowsum(const float* w, int n) {
+    if (n < 8) {
+        float s = 0.f;
+        for (int j = 0; j < n; ++j) s += w[j];
+        return s;
+    }
+    return ((w[0] + w[1]) + (w[2] + w[3])) + ((w[4] + w[5]) + (w[6] + w[7]));
+}
+
+// grid (cdiv(d, 256), nq): out[c][i] = (sum_j big[I_j][c] * wn_j) * rate + (1 - rate) * feats[c][i]
+__global__ __launch_bounds__(256) void ivf_blend_kernel(const float* feats, int d, int64_t fcs, int64_t fqs,
+                                                        const float* D, const int64_t* I, int k, const float* big,
+                                                        int64_t ntotal, float rate, float rate1, float* out,
+                                                        int64_t ocs, int64_t oqs) {
+    const int64_t qi = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    float w[8];
+    int64_t row[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j < k) {
+            const float inv = 1.0f / D[qi * k + j];
+            w[j] = inv * inv;
+            const int64_t ix = I[qi * k + j];
+            row[j] = ix < 0 ? ix + ntotal : ix;  // numpy negative indexing (-1 -> last row)
+        } else {
+            w[j] = 0.f;
+            row[j] = 0;
+        }
+    }
+    if (c >= d) return;
+    const float s = np_rowsum(w, k);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j < k) {
+            const float t = big[row[j] * d + c] * (w[j] / s);
+            acc = j == 0 ? t : acc + t;
+        }
+    }
+    out[c * ocs + qi * oqs] = acc * rate + rate1 * feats[c * fcs + qi * fqs];
+}
+}  // namespace
+
+extern "C" int64_t rvc_ivf_coarse_ws_bytes(int64_t nq, int64_t nlist) {
+    if (nq <= 0 || nlist <= 0) return -1;
+    return nq * nlist * (int64_t)sizeof(double);
+}
+
+extern "C" int rvc_ivf_search(const float* q, int64_t nq, int64_t d, int64_t cs, int64_t qs, const float* centT,
+                              int64_t nlist, int nprobe, const int64_t* list_off, const float* codes,
+                              const int64_t* ids, int k, void* ws, int64_t ws_bytes, int64_t* probes, float* D,
+                              int64_t* I, rvc_stream_t stream) {
+    RVC_CHECK_ARG(q && centT && list_off && codes && ids && ws && probes && D && I, "ivf_search: null pointer");
+    RVC_CHECK_ARG(nq > 0 && d > 0 && d <= 1024 && nlist > 0 && nprobe >= 1 && nprobe <= nlist && k >= 1 &&
+                      k <= KMAX, "ivf_search: bad sizes nq=%lld d=%lld nlist=%lld nprobe=%d k=%d", (long long)nq,
+                  (long long)d, (long long)nlist, nprobe, k);
+    RVC_CHECK_ARG(ws_bytes >= nq * nlist * (int64_t)sizeof(double), "ivf_search: workspace too small");
+    RVC_CHECK_ARG((size_t)QB * d * 4 <= 64 * 1024, "ivf_search: d too large");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(ivf_coarse_kernel, dim3(cdiv(nq, QB), cdiv(nlist, 256)), dim3(256), (size_t)QB * d * 4, s, q,
+                       nq, (int)d, cs, qs, centT, nlist, (double*)ws);
+    hipLaunchKernelGGL(ivf_select_kernel, dim3((unsigned)nq), dim3(64), 0, s, (const double*)ws, nq, nlist, nprobe,
+                       probes);
+    hipLaunchKernelGGL(ivf_scan_kernel, dim3((unsigned)nq), dim3(64), 0, s, q, nq, (int)d, cs, qs,
+                       (const int64_t*)probes, nprobe, list_off, codes, ids, k, D, I);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+extern "C" int rvc_ivf_blend(const float* feats, int64_t nq, int64_t d, int64_t fcs, int64_t fqs, const float* D,
+                             const int64_t* I, int k, const float* big, int64_t ntotal, double index_rate,
+                             float* out, int64_t ocs, int64_t oqs, rvc_stream_t stream) {
+    RVC_CHECK_ARG(feats && D && I && big && out, "ivf_blend: null pointer");
+    RVC_CHECK_ARG(nq > 0 && d > 0 && k >= 1 && k <= 8 && ntotal > 0 && nq < 65536 * 32768ll, "ivf_blend: bad sizes");
+    // torch: npy * index_rate + (1 - index_rate) * feats with the Python floats cast to f32
+    const float r = (float)index_rate, r1 = (float)(1.0 - index_rate);
+    hipLaunchKernelGGL(ivf_blend_kernel, dim3(cdiv(d, 256), (unsigned)nq), dim3(256), 0, (hipStream_t)stream, feats,
+                       (int)d, fcs, fqs, D, I, k, big, ntotal, r, r1, out, ocs, oqs);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}

@@ -357,6 +357,26 @@ class FiltFilt:
         return out, out64
 
 
+def ivf_search(q, nq, d, cs, qs, centT, nlist, nprobe, list_off, codes, ids, k, D, I, probes):
+    """FAISS IVF-Flat search (ivf.hip): see include/rvc_amd.h."""
+    if D.numel() < nq * k or I.numel() < nq * k or probes.numel() < nq * nprobe or centT.numel() < d * nlist:
+        raise ValueError("ivf_search: output / index buffers too small")
+    if q.numel() < (d - 1) * cs + (nq - 1) * qs + 1:
+        raise ValueError("ivf_search: query buffer too small")
+    lib = _lib.load()
+    need = lib.rvc_ivf_coarse_ws_bytes(nq, nlist)
+    ws = _workspace(q.device, need, "ivf")
+    check(lib.rvc_ivf_search(_p(q), nq, d, cs, qs, _p(centT), nlist, nprobe, _p(list_off), _p(codes), _p(ids), k,
+                             _p(ws), need, _p(probes), _p(D), _p(I), _stream()), "ivf_search")
+
+
+def ivf_blend(feats, nq, d, fcs, fqs, D, I, k, big, ntotal, index_rate, out, ocs, oqs):
+    if big.numel() < ntotal * d or D.numel() < nq * k or I.numel() < nq * k:
+        raise ValueError("ivf_blend: buffers too small")
+    check(_lib.load().rvc_ivf_blend(_p(feats), nq, d, fcs, fqs, _p(D), _p(I), k, _p(big), ntotal, float(index_rate),
+                                    _p(out), ocs, oqs, _stream()), "ivf_blend")
+
+
 def phone_upsample(feats, feats0, pitchf, out, C, Tf, T, protect):
     if feats.numel() < C * Tf or out.numel() < C * T or T > 2 * Tf or (pitchf is not None and pitchf.numel() < T):
         raise ValueError("phone_upsample: size mismatch")

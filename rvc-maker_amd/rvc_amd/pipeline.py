@@ -13,8 +13,11 @@ on the host (it needs the filtered signal there, as the reference).  The segment
 tensors in HBM; ``pipeline_device`` is the HBM-resident form the bench times, ``pipeline`` adds
 the host copies of the reference signature.
 
-Not on this path (raise): FAISS retrieval (index_rate > 0 with an index: §8(f) next row),
-f0 methods other than rmvpe, f0 files, autotune, volume_envelope != 1, ONNX models.
+FAISS retrieval (``file_index`` + ``index_rate``) runs on the device (retrieval.py / ivf.hip); the
+index file is read without faiss (faiss_index.py) and kept resident per path.
+
+Not on this path (raise): f0 methods other than rmvpe, f0 files, autotune, volume_envelope != 1,
+ONNX models.
 """
 from __future__ import annotations
 
@@ -90,11 +93,15 @@ class VC:
             feats = model.final_proj.conv(feats)
         return feats
 
-    def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats=None):
+    def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats=None,
+                                index=None, index_rate=0.0):
         """VC.voice_conversion (convert.py:328-386) on a device segment a0 [N] -> waveform [T*upp]."""
         N = a0.numel()
         if feats is None:
             feats = self.features_device(model, a0, version)
+        feats0 = feats  # convert.py:347: the protect blend uses the pre-retrieval features
+        if index is not None and index_rate != 0:
+            feats = index.retrieve_cf(feats, index_rate)
         E, Tf = feats.shape
         p_len = N // self.window
         T = min(2 * Tf, p_len)  # convert.py:364-370
@@ -105,13 +112,13 @@ class VC:
             raise ValueError("pitch shorter than the phone sequence")
         phone = torch.empty(E, T, device=a0.device)
         blend = protect < 0.5
-        ops.phone_upsample(feats, feats, pitchf if blend else None, phone, E, Tf, T, float(protect))
+        ops.phone_upsample(feats, feats0, pitchf if blend else None, phone, E, Tf, T, float(protect))
         zn = self.noise_fn(seg, "z", (1, net_g.inter, T)) if self.noise_fn else None
         sn = self.noise_fn(seg, "sine", (1, T * net_g.upp, 1)) if self.noise_fn else None
         o, *_ = net_g.infer_cf(phone, pitch.contiguous(), pitchf.contiguous(), sid, zn, sn, self.seed + seg)
         return o
 
-    def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect):
+    def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect, index=None, index_rate=0.0):
         """The hot path with inputs and output in HBM: audio device f32 [N] at 16 kHz (numpy accepted)
         -> device f32 waveform at tgt_sr.  filtfilt + reflect padding run on the device (f64)."""
         if not torch.is_tensor(audio):
@@ -123,7 +130,8 @@ class VC:
         if long_input:  # quiet-point search on the filtered f64 signal, host side as the reference
             opt_ts = self.segment_points(xp64[self.t_pad: self.t_pad + N].cpu().numpy())
         p_len = xp.numel() // self.window
-        return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect)
+        return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index,
+                                        index_rate)
 
     def _side_stream(self, device):
         key = str(device)
@@ -133,7 +141,8 @@ class VC:
             self._streams[key] = torch.cuda.Stream(device=device)
         return self._streams[key]
 
-    def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect):
+    def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index=None,
+                            index_rate=0.0):
         # Segments of convert.py:419-440: [s, t + t_pad2 + w) for each quiet point t, then [t, end).
         w, tp = self.window, self.t_pad_tgt
         segs, s = [], 0
@@ -164,7 +173,7 @@ class VC:
         outs = []
         for seg, ((a, b, fa, fb), fe) in enumerate(zip(segs, feats)):
             o = self.voice_conversion_device(model, net_g, sid, xp[a:b], coarse[fa:fb], pitchf[fa:fb], version,
-                                             protect, seg, feats=fe)
+                                             protect, seg, feats=fe, index=index, index_rate=index_rate)
             outs.append(o[tp: o.numel() - tp])
         out = torch.cat(outs) if len(outs) > 1 else outs[0].contiguous()
         if self._ws is None:
@@ -173,14 +182,23 @@ class VC:
         self._rmvpe().check_error() if os.environ.get("RVC_AMD_CHECK") else None
         return out
 
+    def _index(self, path):
+        """Device-resident IVF-Flat index per path (the reference re-reads it every call)."""
+        from .retrieval import IVFFlatDevice
+        cache = self.__dict__.setdefault("_indexes", {})
+        if path not in cache:
+            cache[path] = IVFFlatDevice.from_file(path, self.device)
+        return cache[path]
+
     # ------------------------------------------------------------------ reference signature
     def pipeline(self, model, net_g, sid, audio, pitch, f0_method, file_index, index_rate, pitch_guidance,
                  filter_radius, volume_envelope, version, protect, hop_length, f0_autotune, f0_autotune_strength,
                  suffix, embed_suffix, f0_file=None, f0_onnx=False, pbar=None):
         if f0_method != "rmvpe" or f0_onnx:
             raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe is on the MI355X hot path")
-        if file_index and os.path.exists(file_index) and index_rate != 0:
-            raise NotImplementedError("FAISS retrieval is a SURVEY §8(f) next row, not built yet")
+        index = None
+        if file_index != "" and os.path.exists(file_index) and index_rate != 0:  # convert.py:392-399
+            index = self._index(file_index)
         if not pitch_guidance or f0_autotune or volume_envelope != 1 or hasattr(f0_file, "name"):
             raise NotImplementedError("only the default f0 path (no autotune / f0 file / volume envelope)")
         if suffix != ".pth" or embed_suffix != ".pt":
@@ -188,7 +206,7 @@ class VC:
         if pbar is not None:
             pbar.update(1)
         out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
-                                   protect)
+                                   protect, index, index_rate)
         if pbar is not None:
             pbar.update(3)
         return out.cpu().numpy()

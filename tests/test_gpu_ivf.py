@@ -1,0 +1,91 @@
+"""FAISS IVF-Flat retrieval on the device (ivf.hip) vs the numpy oracle (oracle/ivf.py): identical
+neighbour indices, and the convert.py:349-359 blend; plus VC.pipeline with an index file vs the CPU
+oracle pipeline.  faiss is absent here, so faiss's own f32 rounding is "parity unpinned"."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ivf as oivf
+from rvc_amd.faiss_index import IVFFlatIndex
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def make(n, d, nlist, nprobe=1, seed=0, dups=0):
+    rng = np.random.default_rng(seed)
+    xb = rng.standard_normal((n, d)).astype(np.float32)
+    if dups:
+        xb[-dups:] = xb[:dups]  # exact duplicates: distance ties broken by id
+    cent = xb[rng.choice(n, nlist, replace=False)] + 0.01
+    return IVFFlatIndex.build(cent, xb, nprobe=nprobe), xb
+
+
+@pytest.mark.parametrize("n,d,nlist,nprobe,nq", [(6000, 768, 153, 1, 400), (3000, 256, 60, 3, 300),
+                                                 (500, 768, 64, 1, 200)])
+def test_search_matches_oracle(n, d, nlist, nprobe, nq):
+    from rvc_amd.retrieval import IVFFlatDevice
+    idx, xb = make(n, d, nlist, nprobe, dups=8)
+    rng = np.random.default_rng(7)
+    q = np.concatenate([xb[:20] + 0.0, rng.standard_normal((nq - 20, d)).astype(np.float32)])  # exact hits too
+    dev = IVFFlatDevice(idx, DEV)
+    Dg, Ig = dev.search_cf(torch.from_numpy(np.ascontiguousarray(q.T)).to(DEV), k=8)
+    Do, Io = oivf.search(idx, q, k=8)
+    np.testing.assert_array_equal(Ig.cpu().numpy(), Io)
+    np.testing.assert_allclose(Dg.cpu().numpy(), Do, rtol=1e-6, atol=1e-6)
+
+
+def test_blend_matches_oracle():
+    from rvc_amd.retrieval import IVFFlatDevice
+    idx, xb = make(4000, 768, 100)
+    rng = np.random.default_rng(3)
+    q = rng.standard_normal((321, 768)).astype(np.float32)
+    dev = IVFFlatDevice(idx, DEV)
+    qd = torch.from_numpy(np.ascontiguousarray(q.T)).to(DEV)
+    D, I = dev.search_cf(qd)
+    out = dev.blend_cf(qd, D, I, 0.75).cpu().numpy().T
+    ref = oivf.blend(q, D.cpu().numpy(), I.cpu().numpy(), idx.reconstruct_n(0, idx.ntotal), 0.75)
+    np.testing.assert_allclose(out, ref, rtol=0, atol=2e-6)
+
+
+def test_pipeline_with_index_vs_oracle(tmp_path):
+    """VC.pipeline(file_index=..., index_rate=0.75) end to end vs the CPU oracle with oracle.ivf."""
+    from oracle import contentvec as ocv
+    from oracle import pipeline as opl
+    from oracle import rmvpe as orm
+    from oracle import synth as osy
+    from rvc_amd import melbasis, synthetic
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD
+    sr, version, seed = 40000, "v2", 71
+    net_g = SynthesizerAMD(synthetic.make_synth_ckpt(sr, version, seed=seed), DEV)
+    hub = ContentVecAMD(synthetic.make_contentvec_ckpt(seed + 1), DEV)
+    vc = VC(sr, Config(DEV), rmvpe=RMVPEAMD(synthetic.rmvpe_state_dict(seed + 2), DEV))
+    audio = synthetic.synthetic_audio(3.0, seed=5)
+    # index over "training features": ContentVec outputs of another clip, as create_index.py builds it
+    feats = hub.features_cf(torch.from_numpy(synthetic.synthetic_audio(8.0, seed=6)).to(DEV)).t().cpu().numpy()
+    rng = np.random.default_rng(0)
+    idx = IVFFlatIndex.build(feats[rng.choice(len(feats), 16, replace=False)], feats)
+    path = tmp_path / "added_IVF16_Flat_nprobe_1_test_v2.index"
+    idx.write(str(path))
+    noises = {}
+
+    def noise(seg, kind, shape):
+        if (seg, kind) not in noises:
+            noises[(seg, kind)] = torch.randn(*shape, generator=torch.Generator().manual_seed(11 * seg + len(kind)))
+        return noises[(seg, kind)]
+
+    vc.noise_fn = lambda s, k, sh: noise(s, k, sh).to(DEV)
+    out = vc.pipeline(hub, net_g, 0, audio.copy(), 0, "rmvpe", str(path), 0.75, 1, 3, 1, version, 0.33, 64, False, 1,
+                      ".pth", ".pt")
+    ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
+    torch.set_num_threads(16)
+    ref = opl.pipeline(ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1)), osy.load_weights(ck["weight"]),
+                       orm.load_weights(synthetic.rmvpe_state_dict(seed + 2)),
+                       torch.from_numpy(melbasis.mel_filterbank()), ck["config"], 0, audio, 0.0, version, 0.33, noise,
+                       index=idx, index_rate=0.75)
+    assert out.shape == ref.shape
+    err = float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2)))
+    assert err < 1e-4, err
