@@ -217,6 +217,25 @@ int rvc_ivf_blend(const float* feats, int64_t nq, int64_t d, int64_t fcs, int64_
                   int k, const float* big, int64_t ntotal, double index_rate, float* out, int64_t ocs, int64_t oqs,
                   rvc_stream_t stream);
 
+/* ------------------------------------------------------------------ CREPE f0 (VC.get_f0_crepe, convert.py:230-237)
+ * crepe_frames: CREPE.py:151-171 framing (1024 @ hop, 512 zero pad) + per-frame zero-mean / unbiased-std
+ *   normalisation of frames [frame0, frame0 + nframes) -> out [nframes][1024].
+ * bn_maxpool: BatchNorm(eval, alpha/beta precomputed) + MaxPool(2) of y [B][C][L] into strided out.
+ * crepe_decode: probs [360][T] sigmoid outputs (masked in place to -inf outside [lo, hi)), softmax,
+ *   librosa Viterbi per sequence [seq_off[i], seq_off[i+1]) with log_trans[j][k] = log(A[k][j] + tiny),
+ *   bins -> Hz with dither cents [T], periodicity -> f0_raw [T], pd_raw [T].
+ * crepe_smooth_coarse: mean3(f0), median3(pd), f0[pd < 0.1] = 0, then get_f0's shift + coarse mel bins. */
+int rvc_crepe_frames(const float* audio, int64_t n, int hop, int64_t frame0, int64_t nframes, float* out,
+                     rvc_stream_t stream);
+int rvc_bn_maxpool(const float* y, int64_t B, int64_t C, int64_t L, const float* alpha, const float* beta, float* out,
+                   int64_t obs, int64_t ocs, int64_t ois, rvc_stream_t stream);
+int64_t rvc_crepe_decode_ws_bytes(int64_t T);
+int rvc_crepe_decode(float* probs, int64_t T, int lo, int hi, const int64_t* seq_off, int nseq, const double* log_trans,
+                     double log_off, double log_p_init, const float* dither, void* ws, int64_t ws_bytes, float* f0_raw,
+                     float* pd_raw, rvc_stream_t stream);
+int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T, float shift, double mel_min,
+                            double mel_max, int64_t* coarse, float* pitchf, rvc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,7 +103,7 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
 
 
 def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None, index=None,
-             index_rate=0.0):
+             index_rate=0.0, crepe=None):
     """VC.pipeline (convert.py:388-458): f0 = rmvpe, no index, volume_envelope = 1.
 
     noise(seg_index, name, shape) -> torch tensor for "z" [1, 192, T] and "sine" [1, T*upp, 1]."""
@@ -119,7 +119,12 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
     sid_t = torch.tensor(sid).unsqueeze(0).long()
     big_npy = index.reconstruct_n(0, index.ntotal) if index is not None and index_rate != 0 else None
     p_len = audio_pad.shape[0] // c.window
-    f0 = rm.infer_from_audio(Wr, mel_basis, audio_pad, thred=0.03)
+    if crepe is not None:  # f0_method "crepe-<capacity>": (state dict, capacity, dither cents [T])
+        from . import crepe as oc
+        csd, capacity, dither = crepe
+        f0 = oc.get_f0_crepe(csd, audio_pad, dither, capacity)
+    else:
+        f0 = rm.infer_from_audio(Wr, mel_basis, audio_pad, thred=0.03)
     pitch_c, pitchf = coarse_f0(f0, pitch, c)
     if trace is not None:
         trace["f0_raw"] = f0

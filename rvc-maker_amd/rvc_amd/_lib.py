@@ -78,12 +78,20 @@ SIGNATURES = {
                        c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
     "rvc_ivf_blend": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int, c_void_p, c_int64,
                       c_double, c_void_p, c_int64, c_int64, c_void_p],
+    "rvc_crepe_frames": [c_void_p, c_int64, c_int, c_int64, c_int64, c_void_p, c_void_p],
+    "rvc_bn_maxpool": [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                       c_void_p],
+    "rvc_crepe_decode_ws_bytes": [c_int64],
+    "rvc_crepe_decode": [c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_double, c_double, c_void_p,
+                         c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
+    "rvc_crepe_smooth_coarse": [c_void_p, c_void_p, c_int64, c_float, c_double, c_double, c_void_p, c_void_p,
+                                c_void_p],
     "rvc_phone_upsample": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_peak_normalize": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
-             "rvc_ivf_coarse_ws_bytes": c_int64}
+             "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64}
 
 _lib = None
 

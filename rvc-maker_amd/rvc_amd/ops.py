@@ -81,7 +81,9 @@ class Conv:
         self.Ci = self.Cig * groups
         self.w = pack_km(w.float(), groups).to(device)
         self.b = b.float().to(device) if b is not None else None
-        self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co) if groups == 1 else (None, 0)
+        # the split-bf16 engine takes ungrouped convs with <= 16 taps (see x6_eligible in conv1d.hip)
+        self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co) if groups == 1 and self.K <= 16 \
+            else (None, 0)
 
     def __call__(self, x, Lout=None, stride=1, pad=0, dil=1, **kw):
         return conv1d(x, self.w, self.Ci, self.Co, self.K, bias=self.b, stride=stride, pad=pad, dil=dil,

@@ -16,8 +16,9 @@ the host copies of the reference signature.
 FAISS retrieval (``file_index`` + ``index_rate``) runs on the device (retrieval.py / ivf.hip); the
 index file is read without faiss (faiss_index.py) and kept resident per path.
 
-Not on this path (raise): f0 methods other than rmvpe, f0 files, autotune, volume_envelope != 1,
-ONNX models.
+f0 methods: "rmvpe" and "crepe-{tiny,small,medium,large,full}" (crepe.py), both on the device.
+
+Not on this path (raise): other f0 methods, f0 files, autotune, volume_envelope != 1, ONNX models.
 """
 from __future__ import annotations
 
@@ -43,7 +44,9 @@ class Config:
 
 
 class VC:
-    def __init__(self, tgt_sr, config, rmvpe=None):
+    CREPE_METHODS = {f"crepe-{c}": c for c in ("tiny", "small", "medium", "large", "full")}
+
+    def __init__(self, tgt_sr, config, rmvpe=None, crepe=None):
         self.x_pad = config.x_pad
         self.x_query = config.x_query
         self.x_center = config.x_center
@@ -60,6 +63,7 @@ class VC:
         self.device = config.device
         self.is_half = config.is_half
         self.rmvpe = rmvpe
+        self.crepe = dict(crepe or {})  # capacity -> CrepeAMD (loaded on first use otherwise)
         self.noise_fn = None  # parity hook: noise_fn(seg, "z"|"sine", shape) -> device tensor
         self.seed = 0
         self._ws = None
@@ -84,6 +88,22 @@ class VC:
             from .rmvpe import RMVPEAMD
             self.rmvpe = RMVPEAMD.from_file(os.path.join("assets", "models", "predictors", "rmvpe.pt"), self.device)
         return self.rmvpe
+
+    def _crepe(self, capacity):
+        if capacity not in self.crepe:
+            from .crepe import CrepeAMD
+            self.crepe[capacity] = CrepeAMD.from_file(
+                os.path.join("assets", "models", "predictors", f"crepe_{capacity}.pth"), capacity, self.device)
+        return self.crepe[capacity]
+
+    def f0_device(self, xp, pitch, f0_method="rmvpe"):
+        """VC.get_f0 (convert.py:304-323) on the device: (coarse int64 [T], pitchf f32 [T])."""
+        if f0_method == "rmvpe":
+            coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch))
+            return coarse, pitchf
+        if f0_method in self.CREPE_METHODS:
+            return self._crepe(self.CREPE_METHODS[f0_method]).f0_device(xp, float(pitch))
+        raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe and crepe-* are on the MI355X hot path")
 
     # ------------------------------------------------------------------ device pieces
     def features_device(self, model, a0, version):
@@ -118,7 +138,8 @@ class VC:
         o, *_ = net_g.infer_cf(phone, pitch.contiguous(), pitchf.contiguous(), sid, zn, sn, self.seed + seg)
         return o
 
-    def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect, index=None, index_rate=0.0):
+    def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect, index=None, index_rate=0.0,
+                        f0_method="rmvpe"):
         """The hot path with inputs and output in HBM: audio device f32 [N] at 16 kHz (numpy accepted)
         -> device f32 waveform at tgt_sr.  filtfilt + reflect padding run on the device (f64)."""
         if not torch.is_tensor(audio):
@@ -131,7 +152,7 @@ class VC:
             opt_ts = self.segment_points(xp64[self.t_pad: self.t_pad + N].cpu().numpy())
         p_len = xp.numel() // self.window
         return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index,
-                                        index_rate)
+                                        index_rate, f0_method)
 
     def _side_stream(self, device):
         key = str(device)
@@ -142,7 +163,7 @@ class VC:
         return self._streams[key]
 
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index=None,
-                            index_rate=0.0):
+                            index_rate=0.0, f0_method="rmvpe"):
         # Segments of convert.py:419-440: [s, t + t_pad2 + w) for each quiet point t, then [t, end).
         w, tp = self.window, self.t_pad_tgt
         segs, s = [], 0
@@ -161,7 +182,7 @@ class VC:
         ready.record(main)
         with torch.cuda.stream(side):
             side.wait_event(ready)
-            coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch))
+            coarse, pitchf = self.f0_device(xp, pitch, f0_method)
             f0_done = torch.cuda.Event()
             f0_done.record(side)
         feats = [self.features_device(model, xp[a:b], version) for a, b, _, _ in segs]
@@ -179,7 +200,8 @@ class VC:
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=xp.device)
         ops.peak_normalize(out, self._ws)
-        self._rmvpe().check_error() if os.environ.get("RVC_AMD_CHECK") else None
+        if os.environ.get("RVC_AMD_CHECK") and f0_method == "rmvpe":
+            self._rmvpe().check_error()
         return out
 
     def _index(self, path):
@@ -194,8 +216,8 @@ class VC:
     def pipeline(self, model, net_g, sid, audio, pitch, f0_method, file_index, index_rate, pitch_guidance,
                  filter_radius, volume_envelope, version, protect, hop_length, f0_autotune, f0_autotune_strength,
                  suffix, embed_suffix, f0_file=None, f0_onnx=False, pbar=None):
-        if f0_method != "rmvpe" or f0_onnx:
-            raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe is on the MI355X hot path")
+        if (f0_method != "rmvpe" and f0_method not in self.CREPE_METHODS) or f0_onnx:
+            raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe and crepe-* are on the MI355X hot path")
         index = None
         if file_index != "" and os.path.exists(file_index) and index_rate != 0:  # convert.py:392-399
             index = self._index(file_index)
@@ -206,7 +228,7 @@ class VC:
         if pbar is not None:
             pbar.update(1)
         out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
-                                   protect, index, index_rate)
+                                   protect, index, index_rate, f0_method)
         if pbar is not None:
             pbar.update(3)
         return out.cpu().numpy()

@@ -271,6 +271,32 @@ def rmvpe_state_dict(seed: int = 777) -> "OrderedDict[str, torch.Tensor]":
     return sd
 
 
+# ---------------------------------------------------------------- CREPE
+CREPE_CAPACITY = {
+    "full": ([1, 1024, 128, 128, 128, 256], [1024, 128, 128, 128, 256, 512], 2048),
+    "large": ([1, 768, 96, 96, 96, 192], [768, 96, 96, 96, 192, 384], 1536),
+    "medium": ([1, 512, 64, 64, 64, 128], [512, 64, 64, 64, 128, 256], 1024),
+    "small": ([1, 256, 32, 32, 32, 64], [256, 32, 32, 32, 64, 128], 512),
+    "tiny": ([1, 128, 16, 16, 16, 32], [128, 16, 16, 16, 32, 64], 256),
+}
+
+
+def crepe_state_dict(seed: int = 999, capacity: str = "full") -> "OrderedDict[str, torch.Tensor]":
+    """fp32 ``Crepe(capacity)`` state dict (``CREPE.py:11-58``): conv{i} (k x 1 kernels), conv{i}_BN,
+    classifier."""
+    g = _Gen(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    cin, cout, nfeat = CREPE_CAPACITY[capacity]
+    for i in range(6):
+        k = 512 if i == 0 else 64
+        sd[f"conv{i + 1}.weight"] = g.normal((cout[i], cin[i], k, 1), math.sqrt(2.0 / (cin[i] * k)))
+        sd[f"conv{i + 1}.bias"] = g.normal((cout[i],), 0.02)
+        _bn(g, sd, f"conv{i + 1}_BN", cout[i])
+    sd["classifier.weight"] = g.normal((360, nfeat), 2.0 / math.sqrt(nfeat))
+    sd["classifier.bias"] = g.normal((360,), 0.5)
+    return sd
+
+
 # ---------------------------------------------------------------- audio
 def synthetic_audio(seconds: float, seed: int = 1000, sr: int = 16000) -> np.ndarray:
     """SURVEY §8(d) test signal: 3-harmonic glide (60-240 Hz) + 200 ms gaps every 5 s + noise, peak <= 0.9."""

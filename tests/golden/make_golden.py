@@ -46,8 +46,16 @@ def _stub_modules():
 
     filt.mel = mel
     lib.filters = filt
+    # librosa.sequence.viterbi (CREPE's decode): the oracle's restatement of librosa >= 0.10 --
+    # the CREPE golden therefore pins the network/preprocessing/postprocessing around it, not it
+    seq = types.ModuleType("librosa.sequence")
+    sys.path.insert(0, REPO)
+    from oracle.crepe import viterbi_librosa
+    seq.viterbi = viterbi_librosa
+    lib.sequence = seq
     sys.modules["librosa"] = lib
     sys.modules["librosa.filters"] = filt
+    sys.modules["librosa.sequence"] = seq
     om = types.ModuleType("omegaconf")
     om.DictConfig = dict
 
@@ -239,10 +247,47 @@ def gen_filtfilt(seed):
                         bh=conv.bh, ah=conv.ah)
 
 
+def gen_crepe(seconds, seed):
+    """VC.get_f0_crepe(x, "full") (convert.py:230-237) with synthetic Crepe-full weights; every
+    scipy.stats.triang.rvs dither draw and every batch's network output are recorded."""
+    import scipy.stats
+    import main.inference.convert as conv
+    from main.library.predictors import CREPE as RC
+    torch.save(synthetic.crepe_state_dict(seed), os.path.join("assets", "models", "predictors", "crepe_full.pth"))
+    vc = conv.VC(48000, conv.config)
+    audio = synthetic.synthetic_audio(seconds, seed=seed + 1).astype(np.float64)
+    draws, probs = [], []
+    rvs0, post0 = scipy.stats.triang.rvs, RC.postprocess
+
+    def rvs(*a, **k):
+        v = rvs0(*a, **k)
+        draws.append(np.asarray(v, dtype=np.float64).reshape(-1))
+        return v
+
+    def post(p, *a, **k):
+        probs.append(p[0].t().numpy().copy())  # [T_batch][360]
+        return post0(p, *a, **k)
+
+    scipy.stats.triang.rvs, RC.postprocess = rvs, post
+    np.random.seed(seed + 2)
+    try:
+        f0 = vc.get_f0_crepe(audio, "full")
+    finally:
+        scipy.stats.triang.rvs, RC.postprocess = rvs0, post0
+    frames = next(RC.preprocess(torch.tensor(np.copy(audio))[None].float(), 16000, 160, 512, "cpu", True))
+    np.savez_compressed(os.path.join(OUT, "crepe.npz"), seed=seed, audio=audio, f0=f0,
+                        probs=np.concatenate(probs), dither=np.concatenate(draws), frames_head=frames[:40].numpy(),
+                        batch_sizes=np.array([len(p) for p in probs]))
+    print("crepe", f0.shape, float(np.mean(f0)), [len(p) for p in probs])
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     setup_harness()
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "crepe":
+        gen_crepe(6.0, seed=81)
+        return
     gen_synth("synth_48k_v2", 48000, "v2", 120, seed=11)
     gen_synth("synth_40k_v2", 40000, "v2", 100, seed=12)
     gen_synth("synth_32k_v1", 32000, "v1", 100, seed=13)
@@ -251,6 +296,7 @@ def main():
     gen_filtfilt(seed=41)
     gen_pipeline("pipeline_48k_v2", 48000, "v2", 2.0, seed=51, pitch=0, protect=0.33)
     gen_pipeline("pipeline_32k_v1", 32000, "v1", 1.5, seed=52, pitch=3, protect=0.5)
+    gen_crepe(6.0, seed=81)
 
 
 if __name__ == "__main__":

@@ -111,3 +111,19 @@ def test_coarse_quantiser_sweep():
     # mute fixture semantics (assets/logs/mute/f0/mute.wav.npy): silence -> coarse 1
     z, _ = opl.coarse_f0(np.zeros(301), 0, c)
     assert np.all(z == 1)
+
+
+def test_crepe_oracle_matches_reference_golden(golden):
+    """VC.get_f0_crepe (convert.py:230-237, CREPE.py) -- network, per-batch viterbi, dither, mean/median."""
+    from oracle import crepe as oc
+    from rvc_amd import synthetic
+    g = golden("crepe")
+    sd = synthetic.crepe_state_dict(int(g["seed"]))
+    import torch
+    frames = oc.preprocess(torch.tensor(np.copy(g["audio"]))[None].float(), 160, 512)
+    np.testing.assert_allclose(frames[0][:40].numpy(), g["frames_head"], rtol=0, atol=1e-6)
+    tr = {}
+    f0 = oc.get_f0_crepe(sd, g["audio"], g["dither"], trace=tr)
+    np.testing.assert_allclose(tr["probs"], g["probs"], rtol=0, atol=2e-6)
+    assert f0.shape == g["f0"].shape
+    np.testing.assert_allclose(f0, g["f0"], rtol=1e-5, atol=1e-3)
