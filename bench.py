@@ -76,6 +76,26 @@ class ConvProbe:
         return len(ms), float(sum(ms)), float(sum(fl))
 
 
+def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
+    """SURVEY §8(d) cfg 3 index shape: IVF2564,Flat over 100k 768-d vectors, nprobe 1.  Vectors are drawn
+    around 2564 seeded centres (a trained IVF index has balanced lists; uniform Gaussians in 768-d would
+    pile most vectors onto a few "hub" centroids); the centres are the IVF centroids."""
+    from rvc_amd.faiss_index import IVFFlatIndex
+    from rvc_amd.retrieval import IVFFlatDevice
+    rng = np.random.default_rng(seed)
+    cent = rng.standard_normal((nlist, 768)).astype(np.float32)
+    xb = (cent[rng.integers(0, nlist, n)] + 0.35 * rng.standard_normal((n, 768))).astype(np.float32)
+    x = torch.from_numpy(xb).to(dev)
+    c = torch.from_numpy(cent).to(dev)
+    assign = torch.cdist(x, c).argmin(1).cpu().numpy()  # host-side index build (not timed)
+    order = np.argsort(assign, kind="stable")
+    sizes = np.bincount(assign, minlength=nlist)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    codes = [xb[order[off[i]:off[i + 1]]] for i in range(nlist)]
+    ids = [order[off[i]:off[i + 1]].astype(np.int64) for i in range(nlist)]
+    return IVFFlatDevice(IVFFlatIndex(768, cent, codes, ids, nprobe=1, ntotal=n), dev)
+
+
 def cpu_baseline(seconds=8.0):
     """The torch-CPU oracle (a restatement of the reference's CPU path) on a bounded clip."""
     from oracle import contentvec as ocv
@@ -106,6 +126,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # variants beyond the headline config (BASELINE configs 3/5 ingredients); defaults = configs[1]
+    ap.add_argument("--sr", type=int, default=48000, choices=[32000, 40000, 48000])
+    ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
+    ap.add_argument("--index-rate", type=float, default=0.0,
+                    help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -121,13 +146,20 @@ def main():
 
     from rvc_amd import synthetic
     from rvc_amd.shard import gather_waveforms
-    vc, hub, net_g = build_models(dev)
+    vc, hub, net_g = build_models(dev, sr=args.sr)
+    index = None
+    if args.index_rate > 0:
+        index = synthetic_index(dev)
+    if args.f0 != "rmvpe":
+        from rvc_amd.crepe import CrepeAMD
+        cap = args.f0.split("-", 1)[1]
+        vc.crepe[cap] = CrepeAMD(synthetic.crepe_state_dict(1240, cap), cap, dev)
     audio = synthetic.synthetic_audio(args.seconds, seed=1000 + rank)
     audio_dev = torch.from_numpy(audio).to(dev)  # input resident in HBM before the timed region
     vc.seed = 17 + rank
 
     def step():
-        out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33)
+        out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
             gather_waveforms([out], dist, dst=0)
@@ -151,7 +183,7 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
-    audio_s = out_len / 48000.0
+    audio_s = out_len / float(args.sr)
     value = world * args.steps * audio_s / dt
 
     roof = None
@@ -177,9 +209,12 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
                 "data": "synthetic 16 kHz audio (SURVEY §8d generator), random-init weights of the true shapes",
-                "config": {"workload": f"VC.pipeline 48k v2, ContentVec-768, RMVPE f0, one {args.seconds:g} s clip "
-                                       "per GPU per step, no index, protect 0.33",
-                           "model": "RVC v2 48k (NSF-HiFiGAN) + ContentVec + RMVPE", "global_batch": world,
+                "config": {"workload": f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, one "
+                                       f"{args.seconds:g} s clip per GPU per step, "
+                                       + (f"IVF-Flat index_rate {args.index_rate:g}" if index is not None else "no index")
+                                       + ", protect 0.33",
+                           "model": f"RVC v2 {args.sr // 1000}k (NSF-HiFiGAN) + ContentVec + {args.f0}",
+                           "global_batch": world,
                            "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",
                            "output_seconds_per_clip": round(audio_s, 4)},
                 "roofline": roof, "cpu_baseline": cpu}

@@ -90,18 +90,20 @@ __global__ __launch_bounds__(64) void ivf_select_kernel(const double* dist, int6
     }
 }
 
-// one wave per query; lanes split the dimensions, every lane keeps the same top-k list
+// one wave per query, four list vectors per iteration (16 lanes each, lanes split the dimensions);
+// every lane keeps the same top-k list.  Insertion by (distance, id) is order-independent.
 __global__ __launch_bounds__(64) void ivf_scan_kernel(const float* q, int64_t nq, int d, int64_t cs, int64_t qs,
                                                       const int64_t* probes, int nprobe, const int64_t* list_off,
                                                       const float* codes, const int64_t* ids, int k, float* D,
                                                       int64_t* I) {
     const int64_t qi = blockIdx.x;
     const int lane = threadIdx.x;
-    constexpr int DPL = 16;  // dims per lane (d <= 1024)
+    const int grp = lane >> 4, r = lane & 15;
+    constexpr int DPL = 64;  // dims per lane (d <= 1024)
     float qv[DPL];
 #pragma unroll
     for (int j = 0; j < DPL; ++j) {
-        const int c = lane + 64 * j;
+        const int c = r + 16 * j;
         qv[j] = c < d ? q[c * cs + qi * qs] : 0.f;
     }
     double td[KMAX];
@@ -111,38 +113,46 @@ __global__ __launch_bounds__(64) void ivf_scan_kernel(const float* q, int64_t nq
         td[j] = INFINITY;
         ti[j] = -1;
     }
+    auto insert = [&](double dv, int64_t id) {
+        if (!before(dv, id, td[k - 1], ti[k - 1])) return;
+        double cd = dv;
+        int64_t ci = id;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if (j < k && before(cd, ci, td[j], ti[j])) {
+                const double sd = td[j];
+                const int64_t si = ti[j];
+                td[j] = cd;
+                ti[j] = ci;
+                cd = sd;
+                ci = si;
+            }
+        }
+    };
     for (int p = 0; p < nprobe; ++p) {
         const int64_t li = probes[qi * nprobe + p];
         if (li < 0) continue;
-        for (int64_t v = list_off[li]; v < list_off[li + 1]; ++v) {
-            const float* x = codes + v * d;
+        const int64_t v0 = list_off[li], v1 = list_off[li + 1];
+        for (int64_t v = v0; v < v1; v += 4) {
+            const int64_t vv = v + grp < v1 ? v + grp : v1 - 1;
+            const float* x = codes + vv * d;
             double part = 0.0;
 #pragma unroll
             for (int j = 0; j < DPL; ++j) {
-                const int c = lane + 64 * j;
+                const int c = r + 16 * j;
                 if (c < d) {
                     const double t = (double)qv[j] - (double)x[c];
                     part = fma(t, t, part);
                 }
             }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-            // every lane holds the same sum (xor butterfly): insert into the sorted top-k
-            const int64_t id = ids[v];
-            if (before(part, id, td[k - 1], ti[k - 1])) {
-                double cd = part;
-                int64_t ci = id;
+            for (int o = 8; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            const int64_t myid = ids[vv];
 #pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    if (j < k && before(cd, ci, td[j], ti[j])) {
-                        const double sd = td[j];
-                        const int64_t si = ti[j];
-                        td[j] = cd;
-                        ti[j] = ci;
-                        cd = sd;
-                        ci = si;
-                    }
-                }
+            for (int g = 0; g < 4; ++g) {
+                const double dv = __shfl(part, 16 * g, 64);
+                const int64_t id = __shfl(myid, 16 * g, 64);
+                if (v + g < v1) insert(dv, id);
             }
         }
     }

@@ -78,8 +78,22 @@ def branches():
     print(f"full pipeline_device: {timeit(lambda: vc.pipeline_device(hub, net_g, 0, audio, 0, 'v2', 0.33), 3):9.1f} us")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] == "retrieval"):
     if len(sys.argv) > 1 and sys.argv[1] == "branches":
         branches()
         sys.exit(0)
     main()
+
+
+def retrieval():
+    """IVF-Flat search + blend at the cfg-3 index shape (100k x 768, IVF2564, nprobe 1), 1599 queries."""
+    import bench
+    idx = bench.synthetic_index("cuda")
+    q = torch.randn(768, 1599, device="cuda")
+    print(f"ivf search: {timeit(lambda: idx.search_cf(q), 5):9.1f} us")
+    D, I = idx.search_cf(q)
+    print(f"ivf blend:  {timeit(lambda: idx.blend_cf(q, D, I, 0.75), 5):9.1f} us")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "retrieval":
+    retrieval()
