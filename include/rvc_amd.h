@@ -181,8 +181,21 @@ int rvc_interleave4(const float* phases, float* out, int64_t C, int64_t H, int64
 int rvc_img_to_seq(const float* img, float* x, int64_t C, int64_t H, int64_t W, rvc_stream_t stream);
 int rvc_bigru(const float* gi, const float* whh, const float* bhh, float* y, void* gran_ws, int* err, int64_t T,
               rvc_stream_t stream);
-int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, double shift, double* f0, int64_t* coarse,
-                     float* pitchf, rvc_stream_t stream);
+/* Optional steps of VC.get_f0 between the raw f0 and the mel quantiser (convert.py:311-318), in
+ * the reference's order: autotune (Autotune.autotune_f0, convert.py:168-179: f += (nearest of the 54
+ * reference notes - f) * strength, first note on ties, unvoiced frames included) on the raw f0, then
+ * the pitch shift, then the f0-file override f0[rep_off + i] = rep[i] for i < rep_len (convert.py:314-318,
+ * rep = the host's np.interp of the file, f64).  NULL = none of them.  Arithmetic is f64 on the RMVPE
+ * path (its f0 is f64) and f32 on the CREPE path (its f0 is f32), as in NumPy 2. */
+typedef struct rvc_f0_post {
+    int autotune, _pad0;
+    double strength;
+    const double* rep; /* device f64 [rep_len] or NULL */
+    int64_t rep_off, rep_len;
+} rvc_f0_post;
+
+int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, double shift, const rvc_f0_post* post,
+                     double* f0, int64_t* coarse, float* pitchf, rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ VC.pipeline glue
  * phone_upsample: nearest x2 + protect blend (convert.py:361-378) -> phone [C][T]
@@ -199,6 +212,15 @@ int rvc_filtfilt_pad(const float* x, int64_t N, const double* b, const double* a
 int rvc_phone_upsample(const float* feats, const float* feats0, const float* pitchf, float* out, int64_t C, int64_t Tf,
                        int64_t T, float protect, rvc_stream_t stream);
 int rvc_peak_normalize(float* x, int64_t n, void* ws, float* scale_out, rvc_stream_t stream);
+/* change_rms (convert.py:150-152, VC.pipeline volume_envelope != 1, convert.py:449):
+ *   rms_frames: librosa.feature.rms(y, frame_length = 2*hop, hop_length = hop) (center, zero pad)
+ *     of y [n] (f64 when y64 != NULL, else f32 y32) -> out f32 [1 + n / hop] (mean square in f64).
+ *   rms_mix: y[i] *= r1(i)^(1 - rate) * max(r2(i), 1e-6)^(rate - 1), r(i) = F.interpolate(r, n,
+ *     "linear", align_corners=False) of the source (r1 [n1]) and output (r2 [n2]) envelopes, f32. */
+int64_t rvc_rms_frames_len(int64_t n, int64_t hop);
+int rvc_rms_frames(const double* y64, const float* y32, int64_t n, int64_t hop, float* out, rvc_stream_t stream);
+int rvc_rms_mix(float* y, int64_t n, const float* r1, int64_t n1, const float* r2, int64_t n2, double rate,
+                rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ FAISS IVF-Flat retrieval
  * Replaces faiss IndexIVFFlat(L2).search(feats, k=8) + the blend of convert.py:349-359.
@@ -234,7 +256,8 @@ int rvc_crepe_decode(float* probs, int64_t T, int lo, int hi, const int64_t* seq
                      double log_off, double log_p_init, const float* dither, void* ws, int64_t ws_bytes, float* f0_raw,
                      float* pd_raw, rvc_stream_t stream);
 int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T, float shift, double mel_min,
-                            double mel_max, int64_t* coarse, float* pitchf, rvc_stream_t stream);
+                            double mel_max, const rvc_f0_post* post, int64_t* coarse, float* pitchf,
+                            rvc_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,9 +1,9 @@
 """Oracle: ``VC.pipeline`` (main/inference/convert.py:388-458) on torch-CPU / numpy / scipy.
 
-TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  f0 method "rmvpe", optional
-IVF-Flat retrieval through oracle.ivf (faiss itself is absent: parity unpinned),
-volume_envelope = 1, no f0 file, no autotune.  Noise is injected through
-``noise(seg, name, shape)``.
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  f0 method "rmvpe" or crepe, optional
+IVF-Flat retrieval through oracle.ivf (faiss itself is absent: parity unpinned), f0
+autotune, f0 file and volume envelope (change_rms; its librosa RMS is restated, parity
+unpinned vs librosa).  Noise is injected through ``noise(seg, name, shape)``.
 """
 from __future__ import annotations
 
@@ -36,9 +36,60 @@ class Consts:
         self.f0_mel_max = 1127 * np.log(1 + self.f0_max / 700)
 
 
-def coarse_f0(f0: np.ndarray, pitch: float, c: Consts):
-    """VC.get_f0 tail (convert.py:311-323)."""
+REF_NOTES = [49.00, 51.91, 55.00, 58.27, 61.74, 65.41, 69.30, 73.42, 77.78, 82.41, 87.31, 92.50, 98.00, 103.83,
+             110.00, 116.54, 123.47, 130.81, 138.59, 146.83, 155.56, 164.81, 174.61, 185.00, 196.00, 207.65, 220.00,
+             233.08, 246.94, 261.63, 277.18, 293.66, 311.13, 329.63, 349.23, 369.99, 392.00, 415.30, 440.00, 466.16,
+             493.88, 523.25, 554.37, 587.33, 622.25, 659.25, 698.46, 739.99, 783.99, 830.61, 880.00, 932.33, 987.77,
+             1046.50]  # VC.__init__ ref_freqs (convert.py:198)
+
+
+def autotune_f0(f0: np.ndarray, strength: float) -> np.ndarray:
+    """Autotune.autotune_f0 (convert.py:172-179): each frame moves toward the nearest reference note
+    (first on ties), unvoiced frames included; arithmetic in the array's dtype (NumPy 2)."""
+    out = np.zeros_like(f0)
+    for i, freq in enumerate(f0):
+        out[i] = freq + (min(REF_NOTES, key=lambda x: abs(x - freq)) - freq) * strength
+    return out
+
+
+def f0_override(inp_f0: np.ndarray, x_pad: int, tf0: int = 100):
+    """convert.py:316-318: (np.interp of the f0 file at 100 frames/s, first frame index)."""
+    n = np.round((inp_f0[:, 0].max() - inp_f0[:, 0].min()) * tf0 + 1).astype(np.int16)
+    return np.interp(list(range(n)), inp_f0[:, 0] * 100, inp_f0[:, 1]), x_pad * tf0
+
+
+def rms_librosa(y: np.ndarray, frame_length: int, hop_length: int) -> np.ndarray:
+    """librosa.feature.rms(y=y, frame_length, hop_length) of librosa >= 0.10 (center=True,
+    pad_mode="constant", dtype=float32 squares) -> [1, 1 + len(y) // hop_length].  librosa is absent
+    here: this restatement is PARITY UNPINNED against librosa itself."""
+    yp = np.pad(y, (frame_length // 2, frame_length // 2), mode="constant")
+    n = 1 + (yp.shape[0] - frame_length) // hop_length
+    frames = np.lib.stride_tricks.as_strided(yp, shape=(frame_length, n),
+                                             strides=(yp.strides[0], hop_length * yp.strides[0]))
+    power = np.mean(np.power(frames, 2, dtype=np.float32), axis=-2, keepdims=True)
+    return np.sqrt(power)
+
+
+def change_rms(source_audio, source_rate, target_audio, target_rate, rate):
+    """change_rms (convert.py:150-152): torch linear interpolation of both RMS envelopes to the output
+    length, gain = rms1^(1-rate) * max(rms2, 1e-6)^(rate-1)."""
+    n = target_audio.shape[0]
+    r2 = F.interpolate(torch.from_numpy(rms_librosa(target_audio, target_rate // 2 * 2, target_rate // 2)).float()
+                       .unsqueeze(0), size=n, mode="linear").squeeze()
+    r1 = F.interpolate(torch.from_numpy(rms_librosa(source_audio, source_rate // 2 * 2, source_rate // 2)).float()
+                       .unsqueeze(0), size=n, mode="linear").squeeze()
+    return (target_audio * (torch.pow(r1, 1 - rate) * torch.pow(torch.maximum(r2, torch.zeros_like(r2) + 1e-6),
+                                                               rate - 1)).numpy())
+
+
+def coarse_f0(f0: np.ndarray, pitch: float, c: Consts, autotune_strength=None, inp_f0=None):
+    """VC.get_f0 tail (convert.py:311-323): optional autotune, shift, optional f0-file override, quantiser."""
+    if autotune_strength is not None:
+        f0 = autotune_f0(f0, autotune_strength)
     f0 = f0 * pow(2, pitch / 12)
+    if inp_f0 is not None:
+        rep, a = f0_override(inp_f0, c.x_pad)
+        f0[a: a + len(rep)] = rep[:f0[a: a + len(rep)].shape[0]]
     f0_mel = 1127 * np.log(1 + f0 / 700)
     f0_mel[f0_mel > 0] = (f0_mel[f0_mel > 0] - c.f0_mel_min) * 254 / (c.f0_mel_max - c.f0_mel_min) + 1
     f0_mel[f0_mel <= 1] = 1
@@ -103,8 +154,9 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
 
 
 def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None, index=None,
-             index_rate=0.0, crepe=None):
-    """VC.pipeline (convert.py:388-458): f0 = rmvpe, no index, volume_envelope = 1.
+             index_rate=0.0, crepe=None, autotune_strength=None, inp_f0=None, volume_envelope=1.0):
+    """VC.pipeline (convert.py:388-458): f0 = rmvpe (or crepe), optional index, autotune, f0 file
+    (``inp_f0`` [n][2] f32) and volume envelope.
 
     noise(seg_index, name, shape) -> torch tensor for "z" [1, 192, T] and "sine" [1, T*upp, 1]."""
     tgt_sr = cfg[-1]
@@ -125,7 +177,7 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
         f0 = oc.get_f0_crepe(csd, audio_pad, dither, capacity)
     else:
         f0 = rm.infer_from_audio(Wr, mel_basis, audio_pad, thred=0.03)
-    pitch_c, pitchf = coarse_f0(f0, pitch, c)
+    pitch_c, pitchf = coarse_f0(f0, pitch, c, autotune_strength, inp_f0)
     if trace is not None:
         trace["f0_raw"] = f0
         trace["coarse"] = pitch_c.copy()
@@ -155,6 +207,8 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
                          pitch_t[:, t // c.window:] if t is not None else pitch_t,
                          pitchf_t[:, t // c.window:] if t is not None else pitchf_t))
     audio_opt = np.concatenate(audio_opt)
+    if volume_envelope != 1:
+        audio_opt = change_rms(audio, c.sr, audio_opt, c.sr, volume_envelope)
     audio_max = np.abs(audio_opt).max() / 0.99
     if audio_max > 1:
         audio_opt /= audio_max

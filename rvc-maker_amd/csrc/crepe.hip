@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void crepe_freq_kernel(const int64_t* states, 
 // clamp [1, 255]; coarse = rint.
 __global__ __launch_bounds__(256) void crepe_smooth_coarse_kernel(const float* f0r, const float* pd, int64_t T,
                                                                   float shift, double mel_min, double mel_max,
-                                                                  int64_t* coarse, float* pitchf) {
+                                                                  rvc_f0_post post, int64_t* coarse, float* pitchf) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= T) return;
     const float a = t > 0 ? f0r[t - 1] : 0.f, c = t + 1 < T ? f0r[t + 1] : 0.f;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void crepe_smooth_coarse_kernel(const float* f
         med = fmaxf(fminf(x, y), fminf(fmaxf(x, y), z));
     }
     if (!isinf(med) && med < 0.1f) f = 0.f;  // an infinite median becomes NaN in the reference: kept
-    f = f * shift;
+    f = f0_post_apply<float>(f, t, shift, post);
     float mel = 1127.f * logf(1.f + f / 700.f);
     if (mel > 0.f) mel = (float)(((double)mel - mel_min) * 254.0 / (mel_max - mel_min) + 1.0);
     if (mel <= 1.f) mel = 1.f;
@@ -252,10 +252,13 @@ extern "C" int rvc_crepe_decode(float* probs, int64_t T, int lo, int hi, const i
 extern "C" int64_t rvc_crepe_decode_ws_bytes(int64_t T) { return T * NB * 4 + T * NB * 2 + T * 8 + 16; }
 
 extern "C" int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T, float shift, double mel_min,
-                                       double mel_max, int64_t* coarse, float* pitchf, rvc_stream_t stream) {
+                                       double mel_max, const rvc_f0_post* post, int64_t* coarse, float* pitchf,
+                                       rvc_stream_t stream) {
     RVC_CHECK_ARG(f0_raw && pd_raw && coarse && pitchf && T > 0, "crepe_smooth_coarse: bad args");
+    RVC_CHECK_ARG(!post || !post->rep || (post->rep_off >= 0 && post->rep_len >= 0), "crepe_smooth_coarse: bad f0 post");
+    const rvc_f0_post pp = f0_post_or_none(post);
     hipLaunchKernelGGL(crepe_smooth_coarse_kernel, dim3(cdiv(T, 256)), dim3(256), 0, (hipStream_t)stream, f0_raw,
-                       pd_raw, T, shift, mel_min, mel_max, coarse, pitchf);
+                       pd_raw, T, shift, mel_min, mel_max, pp, coarse, pitchf);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }

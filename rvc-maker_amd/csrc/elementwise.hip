@@ -225,3 +225,72 @@ extern "C" int rvc_sine_source(const float* f0, const float* noise, float* har, 
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }
+
+// ---------------------------------------------------------------- change_rms (convert.py:150-152)
+// librosa.feature.rms(y, frame_length = 2*hop, hop_length = hop): centered frames over the zero-padded
+// signal, mean of the f32 squares (librosa's abs2 dtype=float32), sqrt in f32.  One block per frame.
+namespace {
+__global__ __launch_bounds__(256) void rms_frames_kernel(const double* y64, const float* y32, int64_t n, int64_t hop,
+                                                         float* out) {
+    const int64_t f = blockIdx.x;
+    const int64_t lo = f * hop - hop, hi = lo + 2 * hop;  // original-index window [lo, hi)
+    const int64_t a = lo < 0 ? 0 : lo, b = hi > n ? n : hi;
+    double acc = 0.0;
+    for (int64_t i = a + threadIdx.x; i < b; i += 256) {
+        const float v = y64 ? (float)y64[i] : y32[i];
+        acc += (double)(v * v);
+    }
+    __shared__ double part[256];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[f] = sqrtf((float)(part[0] / (double)(2 * hop)));
+}
+
+// torch F.interpolate(mode="linear", align_corners=False) of r [m] to n points, at output index i.
+__device__ __forceinline__ float interp_linear(const float* r, int64_t m, int64_t n, int64_t i) {
+#pragma clang fp contract(off)
+    const float scale = (float)m / (float)n;
+    float src = scale * ((float)i + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    int64_t i0 = (int64_t)src;
+    if (i0 > m - 1) i0 = m - 1;
+    const int64_t i1 = i0 + (i0 < m - 1 ? 1 : 0);
+    const float l1 = src - (float)i0, l0 = 1.f - l1;
+    return l0 * r[i0] + l1 * r[i1];
+}
+
+__global__ __launch_bounds__(256) void rms_mix_kernel(float* y, int64_t n, const float* r1, int64_t n1, const float* r2,
+                                                      int64_t n2, float e1, float e2) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float a = interp_linear(r1, n1, n, i);
+    const float b = fmaxf(interp_linear(r2, n2, n, i), 1e-6f);
+    y[i] = y[i] * powf(a, e1) * powf(b, e2);
+}
+}  // namespace
+
+extern "C" int64_t rvc_rms_frames_len(int64_t n, int64_t hop) { return (n < 0 || hop <= 0) ? -1 : 1 + n / hop; }
+
+extern "C" int rvc_rms_frames(const double* y64, const float* y32, int64_t n, int64_t hop, float* out,
+                              rvc_stream_t stream) {
+    RVC_CHECK_ARG((y64 || y32) && out && n > 0 && hop > 0, "rms_frames: bad args");
+    hipLaunchKernelGGL(rms_frames_kernel, dim3((unsigned)(1 + n / hop)), dim3(256), 0, (hipStream_t)stream, y64, y32,
+                       n, hop, out);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+extern "C" int rvc_rms_mix(float* y, int64_t n, const float* r1, int64_t n1, const float* r2, int64_t n2, double rate,
+                           rvc_stream_t stream) {
+    RVC_CHECK_ARG(y && r1 && r2 && n > 0 && n1 > 0 && n2 > 0, "rms_mix: bad args");
+    // torch.pow(r, 1 - rate): the exponent is the python float 1 - rate, taken as f32 by the op
+    const double rd = rate;
+    hipLaunchKernelGGL(rms_mix_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, y, n, r1, n1, r2, n2,
+                       (float)(1.0 - rd), (float)(rd - 1.0));
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}

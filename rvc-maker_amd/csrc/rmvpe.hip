@@ -256,7 +256,8 @@ __device__ float np_pairwise9_f(const float* a) {
 }
 
 __global__ void rmvpe_decode_kernel(const float* sal, int64_t ld, int64_t F, double thred, double shift,
-                                    double mel_min, double mel_max, double* f0_out, int64_t* coarse, float* pitchf) {
+                                    double mel_min, double mel_max, rvc_f0_post post, double* f0_out, int64_t* coarse,
+                                    float* pitchf) {
     int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= F) return;
     int am = 0;
@@ -281,7 +282,7 @@ __global__ void rmvpe_decode_kernel(const float* sal, int64_t ld, int64_t F, dou
     if ((double)fmaxf(mx, 0.f) <= thred) dev = 0.0;
     double f0 = 10.0 * pow(2.0, dev / 1200.0);
     if (f0 == 10.0) f0 = 0.0;
-    f0 = f0 * shift;
+    f0 = f0_post_apply<double>(f0, t, shift, post);
     if (f0_out) f0_out[t] = f0;
     double fm = 1127.0 * log(1.0 + f0 / 700.0);
     if (fm > 0) fm = (fm - mel_min) * 254.0 / (mel_max - mel_min) + 1.0;
@@ -291,12 +292,15 @@ __global__ void rmvpe_decode_kernel(const float* sal, int64_t ld, int64_t F, dou
     pitchf[t] = (float)f0;
 }
 
-extern "C" int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, double shift, double* f0,
-                                int64_t* coarse, float* pitchf, rvc_stream_t stream) {
+extern "C" int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, double shift,
+                                const rvc_f0_post* post, double* f0, int64_t* coarse, float* pitchf,
+                                rvc_stream_t stream) {
     RVC_CHECK_ARG(sal && coarse && pitchf && F > 0 && ld >= F, "rmvpe_decode: bad args");
+    RVC_CHECK_ARG(!post || !post->rep || (post->rep_off >= 0 && post->rep_len >= 0), "rmvpe_decode: bad f0 post");
+    const rvc_f0_post pp = f0_post_or_none(post);
     const double mel_min = 1127.0 * log(1.0 + 50.0 / 700.0), mel_max = 1127.0 * log(1.0 + 1100.0 / 700.0);
     hipLaunchKernelGGL(rmvpe_decode_kernel, dim3(cdiv(F, 128)), dim3(128), 0, (hipStream_t)stream, sal, ld, F, thred,
-                       shift, mel_min, mel_max, f0, coarse, pitchf);
+                       shift, mel_min, mel_max, pp, f0, coarse, pitchf);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }

@@ -61,3 +61,44 @@ void rvc_set_error(const char* fmt, ...);
     } while (0)
 
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+// VC.get_f0's optional f0 steps (convert.py:311-318), shared by the RMVPE (f64) and CREPE (f32)
+// decoders.  The 54 reference notes of VC.__init__ (convert.py:198).
+static __device__ __constant__ double kRefNotes[54] = {
+    49.00,  51.91,  55.00,  58.27,  61.74,  65.41,  69.30,  73.42,  77.78,  82.41,  87.31,  92.50,  98.00,  103.83,
+    110.00, 116.54, 123.47, 130.81, 138.59, 146.83, 155.56, 164.81, 174.61, 185.00, 196.00, 207.65, 220.00, 233.08,
+    246.94, 261.63, 277.18, 293.66, 311.13, 329.63, 349.23, 369.99, 392.00, 415.30, 440.00, 466.16, 493.88, 523.25,
+    554.37, 587.33, 622.25, 659.25, 698.46, 739.99, 783.99, 830.61, 880.00, 932.33, 987.77, 1046.50};
+
+// Autotune.autotune_f0 (convert.py:172-179): min(notes, key=|x - f|) keeps the first note on ties;
+// F is the f0 array's dtype (NumPy 2: python-float note/strength operands take the array's dtype).
+template <typename F>
+RVC_DEV F autotune_note(F f, double strength) {
+#pragma clang fp contract(off)
+    F best = (F)kRefNotes[0];
+    F bd = (F)fabs((double)((F)kRefNotes[0] - f));
+    for (int i = 1; i < 54; ++i) {
+        F d = (F)kRefNotes[i] - f;
+        d = d < (F)0 ? -d : d;
+        if (d < bd) {
+            bd = d;
+            best = (F)kRefNotes[i];
+        }
+    }
+    return f + (best - f) * (F)strength;
+}
+
+// autotune -> * shift -> f0-file override, on frame t (kernels take the struct by value; the
+// C entry points turn a NULL post into a zeroed one).
+template <typename F>
+RVC_DEV F f0_post_apply(F f, int64_t t, F shift, const rvc_f0_post& post) {
+    if (post.autotune) f = autotune_note<F>(f, post.strength);
+    f = f * shift;
+    if (post.rep && t >= post.rep_off && t < post.rep_off + post.rep_len) f = (F)post.rep[t - post.rep_off];
+    return f;
+}
+
+static inline rvc_f0_post f0_post_or_none(const rvc_f0_post* p) {
+    rvc_f0_post z = {};
+    return p ? *p : z;
+}

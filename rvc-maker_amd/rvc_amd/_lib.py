@@ -39,6 +39,12 @@ class AttnArgs(ctypes.Structure):
                 ("W", c_int), ("_pad0", c_int), ("scale", c_float), ("_pad1", c_float)]
 
 
+class F0Post(ctypes.Structure):
+    """rvc_f0_post: autotune / f0-file steps of VC.get_f0 (convert.py:311-318)."""
+    _fields_ = [("autotune", c_int), ("_pad0", c_int), ("strength", c_double), ("rep", c_void_p),
+                ("rep_off", c_int64), ("rep_len", c_int64)]
+
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "rvc_last_error": [],
@@ -69,7 +75,8 @@ SIGNATURES = {
     "rvc_interleave4": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_img_to_seq": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_bigru": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
-    "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p],
+    "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, POINTER(F0Post), c_void_p, c_void_p,
+                         c_void_p, c_void_p],
     "rvc_filtfilt_work_bytes": [c_int64],
     "rvc_filtfilt_pad": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                          c_void_p],
@@ -84,14 +91,18 @@ SIGNATURES = {
     "rvc_crepe_decode_ws_bytes": [c_int64],
     "rvc_crepe_decode": [c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_void_p, c_double, c_double, c_void_p,
                          c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
-    "rvc_crepe_smooth_coarse": [c_void_p, c_void_p, c_int64, c_float, c_double, c_double, c_void_p, c_void_p,
-                                c_void_p],
+    "rvc_crepe_smooth_coarse": [c_void_p, c_void_p, c_int64, c_float, c_double, c_double, POINTER(F0Post), c_void_p,
+                                c_void_p, c_void_p],
     "rvc_phone_upsample": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_peak_normalize": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p],
+    "rvc_rms_frames_len": [c_int64, c_int64],
+    "rvc_rms_frames": [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
+    "rvc_rms_mix": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
-             "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64}
+             "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
+             "rvc_rms_frames_len": c_int64}
 
 _lib = None
 

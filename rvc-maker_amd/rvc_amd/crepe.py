@@ -98,7 +98,7 @@ class CrepeAMD:
         self.classifier(x, out=out, out_act=ACT_SIGMOID)
 
     # ------------------------------------------------------------------ f0
-    def f0_device(self, audio: torch.Tensor, pitch_shift: float = 0.0, trace=None):
+    def f0_device(self, audio: torch.Tensor, pitch_shift: float = 0.0, trace=None, post=None):
         """audio [N] device f32 (the padded 16 kHz signal) -> (coarse int64 [T], pitchf f32 [T]),
         T = 1 + N // 160."""
         dev = audio.device
@@ -131,7 +131,8 @@ class CrepeAMD:
         mel_min = 1127 * np.log(1 + 50 / 700)
         mel_max = 1127 * np.log(1 + 1100 / 700)
         check(lib.rvc_crepe_smooth_coarse(ops._p(f0r), ops._p(pdr), T, float(math.pow(2, pitch_shift / 12)),
-                                          float(mel_min), float(mel_max), ops._p(coarse), ops._p(pitchf),
+                                          float(mel_min), float(mel_max), ops._post_ref(post, T), ops._p(coarse),
+                                          ops._p(pitchf),
                                           ops._stream()), "crepe_smooth_coarse")
         if trace is not None:
             trace.update(f0_raw=f0r.cpu().numpy(), pd_raw=pdr.cpu().numpy())

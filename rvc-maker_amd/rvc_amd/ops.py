@@ -321,12 +321,40 @@ def bigru(gi, whh, bhh, y, gran, err, T):
     return y
 
 
-def rmvpe_decode(sal, ld, F, thred, shift, f0, coarse, pitchf):
+class F0Post:
+    """The optional steps of VC.get_f0 between the raw f0 and the quantiser (convert.py:311-318):
+    autotune strength (None = off) and the f0-file override ``rep`` (f64 values for frames
+    [rep_off, rep_off + len(rep)))."""
+
+    def __init__(self, autotune_strength=None, rep=None, rep_off=0, device=None):
+        self.autotune_strength = autotune_strength
+        self.rep = None
+        self.rep_off = int(rep_off)
+        if rep is not None and len(rep) > 0:
+            import numpy as np
+            self.rep = torch.from_numpy(np.ascontiguousarray(rep, dtype=np.float64)).to(device)
+
+    def struct(self, F):
+        """ctypes rvc_f0_post for an f0 track of F frames (the override is clipped to it)."""
+        s = _lib.F0Post()
+        if self.autotune_strength is not None:
+            s.autotune, s.strength = 1, float(self.autotune_strength)
+        if self.rep is not None and self.rep_off < F:
+            s.rep = ctypes.c_void_p(self.rep.data_ptr())
+            s.rep_off, s.rep_len = self.rep_off, min(self.rep.numel(), F - self.rep_off)
+        return s
+
+
+def _post_ref(post, F):
+    return ctypes.byref(post.struct(F)) if post is not None else None
+
+
+def rmvpe_decode(sal, ld, F, thred, shift, f0, coarse, pitchf, post=None):
     if sal.numel() < 360 * ld or coarse.numel() < F or pitchf.numel() < F or (f0 is not None and f0.numel() < F):
         raise ValueError("rmvpe_decode: size mismatch")
     f0p = ctypes.c_void_p(f0.data_ptr()) if f0 is not None else None
-    check(_lib.load().rvc_rmvpe_decode(_p(sal), ld, F, thred, shift, f0p, _p(coarse), _p(pitchf), _stream()),
-          "rmvpe_decode")
+    check(_lib.load().rvc_rmvpe_decode(_p(sal), ld, F, thred, shift, _post_ref(post, F), f0p, _p(coarse), _p(pitchf),
+                                       _stream()), "rmvpe_decode")
 
 
 class FiltFilt:
@@ -390,6 +418,23 @@ def phone_upsample(feats, feats0, pitchf, out, C, Tf, T, protect):
 def peak_normalize(x, ws, scale_out=None):
     check(_lib.load().rvc_peak_normalize(_p(x), x.numel(), _p(ws), _p(scale_out), _stream()), "peak_normalize")
     return x
+
+
+def change_rms(src, src64, out, hop, rate):
+    """change_rms(audio, 16000, audio_opt, 16000, rate) (convert.py:150-152, :449) in place on the device
+    output ``out`` [n]; src = the filtered 16 kHz input (f64 ``src64`` preferred, else f32 ``src``).
+    The reference passes 16000 as both rates, so both envelopes use hop = 8000 (``hop``)."""
+    lib = _lib.load()
+    n_src = (src64 if src64 is not None else src).numel()
+    n1, n2 = lib.rvc_rms_frames_len(n_src, hop), lib.rvc_rms_frames_len(out.numel(), hop)
+    r1 = torch.empty(n1, device=out.device)
+    r2 = torch.empty(n2, device=out.device)
+    s64 = ctypes.c_void_p(src64.data_ptr()) if src64 is not None else None
+    check(lib.rvc_rms_frames(s64, None if src64 is not None else _p(src), n_src, hop, _p(r1), _stream()),
+          "rms_frames")
+    check(lib.rvc_rms_frames(None, _p(out), out.numel(), hop, _p(r2), _stream()), "rms_frames")
+    check(lib.rvc_rms_mix(_p(out), out.numel(), _p(r1), n1, _p(r2), n2, float(rate), _stream()), "rms_mix")
+    return out
 
 
 SQRT = math.sqrt

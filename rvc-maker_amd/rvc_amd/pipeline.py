@@ -18,7 +18,9 @@ index file is read without faiss (faiss_index.py) and kept resident per path.
 
 f0 methods: "rmvpe" and "crepe-{tiny,small,medium,large,full}" (crepe.py), both on the device.
 
-Not on this path (raise): other f0 methods, f0 files, autotune, volume_envelope != 1, ONNX models.
+f0 autotune and f0 files run inside the f0 decode kernels; volume_envelope != 1 (change_rms) runs on
+the device after the segment loop.  Not on this path (raise): other f0 methods, ONNX/safetensors models,
+no-f0 models.
 """
 from __future__ import annotations
 
@@ -96,13 +98,18 @@ class VC:
                 os.path.join("assets", "models", "predictors", f"crepe_{capacity}.pth"), capacity, self.device)
         return self.crepe[capacity]
 
-    def f0_device(self, xp, pitch, f0_method="rmvpe"):
-        """VC.get_f0 (convert.py:304-323) on the device: (coarse int64 [T], pitchf f32 [T])."""
+    def f0_device(self, xp, pitch, f0_method="rmvpe", f0_autotune=False, f0_autotune_strength=1.0, inp_f0=None):
+        """VC.get_f0 (convert.py:304-323) on the device: (coarse int64 [T], pitchf f32 [T]).  Autotune
+        and the f0-file override run inside the decode kernels, in the reference's order."""
+        post = None
+        if f0_autotune or inp_f0 is not None:
+            rep, off = f0_override(inp_f0, self.x_pad) if inp_f0 is not None else (None, 0)
+            post = ops.F0Post(f0_autotune_strength if f0_autotune else None, rep, off, xp.device)
         if f0_method == "rmvpe":
-            coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch))
+            coarse, pitchf, _ = self._rmvpe().f0_device(xp, 0.03, float(pitch), post=post)
             return coarse, pitchf
         if f0_method in self.CREPE_METHODS:
-            return self._crepe(self.CREPE_METHODS[f0_method]).f0_device(xp, float(pitch))
+            return self._crepe(self.CREPE_METHODS[f0_method]).f0_device(xp, float(pitch), post=post)
         raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe and crepe-* are on the MI355X hot path")
 
     # ------------------------------------------------------------------ device pieces
@@ -139,20 +146,23 @@ class VC:
         return o
 
     def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect, index=None, index_rate=0.0,
-                        f0_method="rmvpe"):
+                        f0_method="rmvpe", f0_autotune=False, f0_autotune_strength=1.0, inp_f0=None,
+                        volume_envelope=1.0):
         """The hot path with inputs and output in HBM: audio device f32 [N] at 16 kHz (numpy accepted)
         -> device f32 waveform at tgt_sr.  filtfilt + reflect padding run on the device (f64)."""
         if not torch.is_tensor(audio):
             audio = torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)).to(self.device)
         N = audio.numel()
         long_input = N + self.window > self.t_max  # convert.py:406 (audio padded by window/2 each side)
-        xp, xp64 = self.filt(audio.contiguous(), self.t_pad, want_f64=long_input)
+        xp, xp64 = self.filt(audio.contiguous(), self.t_pad, want_f64=long_input or volume_envelope != 1)
         opt_ts = []
         if long_input:  # quiet-point search on the filtered f64 signal, host side as the reference
             opt_ts = self.segment_points(xp64[self.t_pad: self.t_pad + N].cpu().numpy())
         p_len = xp.numel() // self.window
+        f0_opts = dict(f0_autotune=f0_autotune, f0_autotune_strength=f0_autotune_strength, inp_f0=inp_f0)
+        src64 = xp64[self.t_pad: self.t_pad + N] if volume_envelope != 1 else None
         return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index,
-                                        index_rate, f0_method)
+                                        index_rate, f0_method, f0_opts, volume_envelope, src64)
 
     def _side_stream(self, device):
         key = str(device)
@@ -163,7 +173,7 @@ class VC:
         return self._streams[key]
 
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index=None,
-                            index_rate=0.0, f0_method="rmvpe"):
+                            index_rate=0.0, f0_method="rmvpe", f0_opts=None, volume_envelope=1.0, src64=None):
         # Segments of convert.py:419-440: [s, t + t_pad2 + w) for each quiet point t, then [t, end).
         w, tp = self.window, self.t_pad_tgt
         segs, s = [], 0
@@ -182,7 +192,7 @@ class VC:
         ready.record(main)
         with torch.cuda.stream(side):
             side.wait_event(ready)
-            coarse, pitchf = self.f0_device(xp, pitch, f0_method)
+            coarse, pitchf = self.f0_device(xp, pitch, f0_method, **(f0_opts or {}))
             f0_done = torch.cuda.Event()
             f0_done.record(side)
         feats = [self.features_device(model, xp[a:b], version) for a, b, _, _ in segs]
@@ -197,6 +207,8 @@ class VC:
                                              protect, seg, feats=fe, index=index, index_rate=index_rate)
             outs.append(o[tp: o.numel() - tp])
         out = torch.cat(outs) if len(outs) > 1 else outs[0].contiguous()
+        if volume_envelope != 1:  # convert.py:449: both envelopes at the 16 kHz rate (reference quirk)
+            ops.change_rms(None, src64, out, self.sample_rate // 2, volume_envelope)
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=xp.device)
         ops.peak_normalize(out, self._ws)
@@ -221,14 +233,44 @@ class VC:
         index = None
         if file_index != "" and os.path.exists(file_index) and index_rate != 0:  # convert.py:392-399
             index = self._index(file_index)
-        if not pitch_guidance or f0_autotune or volume_envelope != 1 or hasattr(f0_file, "name"):
-            raise NotImplementedError("only the default f0 path (no autotune / f0 file / volume envelope)")
+        if not pitch_guidance:
+            raise NotImplementedError("no-f0 models: the reference's no-f0 Generator is not buildable (SURVEY §0)")
         if suffix != ".pth" or embed_suffix != ".pt":
             raise NotImplementedError("ONNX / safetensors models are not on the MI355X path")
         if pbar is not None:
             pbar.update(1)
-        out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
-                                   protect, index, index_rate, f0_method)
+        inp_f0 = read_f0_file(f0_file)
         if pbar is not None:
-            pbar.update(3)
+            pbar.update(1)
+        out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
+                                   protect, index, index_rate, f0_method, bool(f0_autotune), f0_autotune_strength,
+                                   inp_f0, volume_envelope)
+        if pbar is not None:
+            pbar.update(2)
         return out.cpu().numpy()
+
+
+def read_f0_file(f0_file):
+    """convert.py:425-436: an object with ``.name`` naming a text file of "time,f0" lines -> f32 [n][2]
+    (None when absent, empty or unreadable; the reference logs and carries on)."""
+    if not hasattr(f0_file, "name"):
+        return None
+    try:
+        with open(f0_file.name, "r") as f:
+            raw = f.read()
+        if len(raw) == 0:
+            return None
+        return np.array([[float(v) for v in line.split(",")] for line in raw.strip("\n").split("\n")],
+                        dtype=np.float32)
+    except Exception as e:  # noqa: BLE001 -- the reference's bare except + log
+        import logging
+        logging.getLogger(__name__).error(f"f0 file: {e}")
+        return None
+
+
+def f0_override(inp_f0, x_pad, tf0=100):
+    """convert.py:316-318: the f0 file resampled to 100 frames/s by np.interp (f64), written over the
+    frames starting at x_pad * tf0.  Returns (values, first frame); the decode kernels clip it to the track."""
+    n = np.round((inp_f0[:, 0].max() - inp_f0[:, 0].min()) * tf0 + 1).astype(np.int16)
+    rep = np.interp(list(range(n)), inp_f0[:, 0] * 100, inp_f0[:, 1])
+    return rep, x_pad * tf0

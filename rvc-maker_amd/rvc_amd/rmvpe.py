@@ -203,8 +203,10 @@ class RMVPEAMD:
         ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran, self.err, Tp)
         return self.fc(y, out_act=ACT_SIGMOID), Tp
 
-    def f0_device(self, audio: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, want_f0=False):
-        """audio [N] f32 device -> (coarse int64 [F], pitchf f32 [F], f0 f64 [F] | None) on the device."""
+    def f0_device(self, audio: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, want_f0=False,
+                  post=None):
+        """audio [N] f32 device -> (coarse int64 [F], pitchf f32 [F], f0 f64 [F] | None) on the device;
+        ``post`` (ops.F0Post) adds get_f0's autotune / f0-file steps."""
         mel = self.mel_spectrogram(audio)
         F = mel.shape[-1]
         sal, Tp = self.salience(mel)
@@ -212,7 +214,7 @@ class RMVPEAMD:
         coarse = torch.empty(F, dtype=torch.int64, device=dev)
         pitchf = torch.empty(F, device=dev)
         f0 = torch.empty(F, dtype=torch.float64, device=dev) if want_f0 else None
-        ops.rmvpe_decode(sal, Tp, F, thred, math.pow(2, pitch_shift / 12), f0, coarse, pitchf)
+        ops.rmvpe_decode(sal, Tp, F, thred, math.pow(2, pitch_shift / 12), f0, coarse, pitchf, post)
         return coarse, pitchf, f0
 
     def check_error(self):

@@ -53,6 +53,16 @@ def _stub_modules():
     from oracle.crepe import viterbi_librosa
     seq.viterbi = viterbi_librosa
     lib.sequence = seq
+    # librosa.feature.rms (change_rms, convert.py:150-152): the oracle's restatement -- unpinned vs librosa
+    feat = types.ModuleType("librosa.feature")
+    from oracle.pipeline import rms_librosa
+
+    def rms(y=None, frame_length=2048, hop_length=512, **kw):
+        return rms_librosa(y, frame_length, hop_length)
+
+    feat.rms = rms
+    lib.feature = feat
+    sys.modules["librosa.feature"] = feat
     sys.modules["librosa"] = lib
     sys.modules["librosa.filters"] = filt
     sys.modules["librosa.sequence"] = seq
@@ -208,7 +218,8 @@ def gen_rmvpe(seconds, seed):
     print("rmvpe", tuple(mel.shape), tuple(hidden.shape), float(np.mean(f0)))
 
 
-def gen_pipeline(name, sr, version, seconds, seed, pitch, protect):
+def gen_pipeline(name, sr, version, seconds, seed, pitch, protect, f0_autotune=False, f0_autotune_strength=1,
+                 f0_lines=None, volume_envelope=1):
     import main.inference.convert as conv
     ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
     net_g = build_ref_synth(ck)
@@ -219,13 +230,18 @@ def gen_pipeline(name, sr, version, seconds, seed, pitch, protect):
     torch.save(synthetic.rmvpe_state_dict(seed + 2), os.path.join("assets", "models", "predictors", "rmvpe.pt"))
     vc = conv.VC(sr, conv.config)
     audio = synthetic.synthetic_audio(seconds, seed=seed + 3)
+    f0_file = None
+    if f0_lines is not None:  # the reference reads f0_file.name (a gradio upload object)
+        f0_file = types.SimpleNamespace(name=os.path.abspath(f"{name}_f0.txt"))
+        with open(f0_file.name, "w") as f:
+            f.write("\n".join(f0_lines) + "\n")
     torch.manual_seed(seed + 4)
     with NoiseRecorder() as rec:
         out = vc.pipeline(model=hub, net_g=net_g, sid=0, audio=audio.copy(), pitch=pitch, f0_method="rmvpe",
-                          file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3, volume_envelope=1,
-                          version=version, protect=protect, hop_length=64, f0_autotune=False,
-                          f0_autotune_strength=1, suffix=".pth", embed_suffix=".pt", f0_file=None, f0_onnx=False,
-                          pbar=Pbar())
+                          file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3,
+                          volume_envelope=volume_envelope, version=version, protect=protect, hop_length=64,
+                          f0_autotune=f0_autotune, f0_autotune_strength=f0_autotune_strength, suffix=".pth",
+                          embed_suffix=".pt", f0_file=f0_file, f0_onnx=False, pbar=Pbar())
     kinds = [k for k, _ in rec.draws]
     assert len(kinds) % 3 == 0 and kinds[:3] == ["randn_like", "rand", "randn_like"], kinds
     nseg = len(kinds) // 3
@@ -233,8 +249,15 @@ def gen_pipeline(name, sr, version, seconds, seed, pitch, protect):
     for s in range(nseg):
         arrs[f"z_noise_{s}"] = rec.draws[3 * s][1].numpy()
         arrs[f"sine_noise_{s}"] = rec.draws[3 * s + 2][1].numpy()
+    opts = {}
+    if f0_autotune:
+        opts["f0_autotune_strength"] = f0_autotune_strength
+    if f0_lines is not None:
+        opts["f0_lines"] = np.array(f0_lines)
+    if volume_envelope != 1:
+        opts["volume_envelope"] = volume_envelope
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), sr=sr, version=version, seed=seed, pitch=pitch,
-                        protect=protect, audio=audio, out=out, nseg=nseg, x_pad=conv.config.x_pad, **arrs)
+                        protect=protect, audio=audio, out=out, nseg=nseg, x_pad=conv.config.x_pad, **arrs, **opts)
     print(name, "out", out.shape, float(np.sqrt(np.mean(out ** 2))), "segments", nseg)
 
 
@@ -281,12 +304,44 @@ def gen_crepe(seconds, seed):
     print("crepe", f0.shape, float(np.mean(f0)), [len(p) for p in probs])
 
 
+def gen_f0_opts(seed):
+    """KATs of the reference's Autotune.autotune_f0 (f64 and f32 tracks, convert.py:168-179), get_f0's
+    f0-file override (convert.py:304-323 with a recorded f0 track) and change_rms (convert.py:150-152)."""
+    import main.inference.convert as conv
+    vc = conv.VC(48000, conv.config)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    f64 = rng.uniform(0, 1200, 997)
+    f64[::9] = 0.0
+    f64[5] = 50.455  # midway-ish between notes
+    f32 = f64.astype(np.float32)
+    at64 = conv.Autotune.autotune_f0(vc, f64.copy(), 0.75)
+    at32 = conv.Autotune.autotune_f0(vc, f32.copy(), 0.75)
+    # get_f0 with a stubbed method returning the recorded track (the f0 estimator is not under test)
+    inp_f0 = np.array([[0.0, 220.0], [0.31, 330.0], [0.77, 180.5], [1.204, 410.25]], dtype=np.float32)
+    x = np.zeros(16000 * 4)
+    track = rng.uniform(80, 700, 1 + x.shape[0] // 160)
+    vc.get_f0_rmvpe = lambda x, legacy=False, onnx=False: track.copy()
+    coarse, f0 = vc.get_f0(x, x.shape[0] // 160, 3, "rmvpe", 3, 64, True, 0.6, inp_f0.copy())
+    src = rng.standard_normal(16000 * 3) * np.linspace(0.01, 0.5, 16000 * 3)
+    tgt = (rng.standard_normal(16000 * 9) * 0.2).astype(np.float32)
+    cr = conv.change_rms(src, 16000, tgt.copy(), 16000, 0.35)
+    np.savez_compressed(os.path.join(OUT, "f0_opts.npz"), f64=f64, f32=f32, at64=at64, at32=at32, inp_f0=inp_f0,
+                        track=track, coarse=coarse, f0=f0, rms_src=src, rms_tgt=tgt, rms_out=cr)
+    print("f0_opts", float(np.abs(at64 - f64).max()), coarse[:5], float(np.abs(cr).mean()))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     setup_harness()
     torch.set_num_threads(8)
     if len(sys.argv) > 1 and sys.argv[1] == "crepe":
         gen_crepe(6.0, seed=81)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "opts":
+        gen_f0_opts(seed=91)
+        gen_pipeline("pipeline_48k_v2_opts", 48000, "v2", 2.5, seed=53, pitch=2, protect=0.33, f0_autotune=True,
+                     f0_autotune_strength=0.8, f0_lines=["0.0,200", "0.4,260.5", "0.9,150", "1.6,0", "2.0,310"],
+                     volume_envelope=0.6)
         return
     gen_synth("synth_48k_v2", 48000, "v2", 120, seed=11)
     gen_synth("synth_40k_v2", 40000, "v2", 100, seed=12)
@@ -297,6 +352,10 @@ def main():
     gen_pipeline("pipeline_48k_v2", 48000, "v2", 2.0, seed=51, pitch=0, protect=0.33)
     gen_pipeline("pipeline_32k_v1", 32000, "v1", 1.5, seed=52, pitch=3, protect=0.5)
     gen_crepe(6.0, seed=81)
+    gen_f0_opts(seed=91)
+    gen_pipeline("pipeline_48k_v2_opts", 48000, "v2", 2.5, seed=53, pitch=2, protect=0.33, f0_autotune=True,
+                 f0_autotune_strength=0.8, f0_lines=["0.0,200", "0.4,260.5", "0.9,150", "1.6,0", "2.0,310"],
+                 volume_envelope=0.6)
 
 
 if __name__ == "__main__":

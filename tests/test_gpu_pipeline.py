@@ -1,4 +1,6 @@
 """End-to-end VC.pipeline on the HIP path vs the reference's own outputs (golden vectors)."""
+import types
+
 import numpy as np
 import pytest
 import torch
@@ -27,8 +29,8 @@ class Pbar:
         self.n += k
 
 
-@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1"])
-def test_pipeline_matches_reference_golden(golden, name):
+@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1", "pipeline_48k_v2_opts"])
+def test_pipeline_matches_reference_golden(golden, name, tmp_path):
     g = golden(name)
     sr, version, seed = int(g["sr"]), str(g["version"]), int(g["seed"])
     vc, hub, net_g = build(sr, version, seed)
@@ -40,10 +42,17 @@ def test_pipeline_matches_reference_golden(golden, name):
 
     vc.noise_fn = noise
     pb = Pbar()
+    f0_file = None
+    if "f0_lines" in g:  # the reference reads f0_file.name (convert.py:427)
+        path = tmp_path / "f0.txt"
+        path.write_text("\n".join(str(x) for x in g["f0_lines"]) + "\n")
+        f0_file = types.SimpleNamespace(name=str(path))
     out = vc.pipeline(model=hub, net_g=net_g, sid=0, audio=g["audio"].copy(), pitch=float(g["pitch"]),
                       f0_method="rmvpe", file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3,
-                      volume_envelope=1, version=version, protect=float(g["protect"]), hop_length=64,
-                      f0_autotune=False, f0_autotune_strength=1, suffix=".pth", embed_suffix=".pt", pbar=pb)
+                      volume_envelope=float(g.get("volume_envelope", 1)), version=version,
+                      protect=float(g["protect"]), hop_length=64, f0_autotune="f0_autotune_strength" in g,
+                      f0_autotune_strength=float(g.get("f0_autotune_strength", 1)), suffix=".pth",
+                      embed_suffix=".pt", f0_file=f0_file, pbar=pb)
     vc.rmvpe.check_error()
     assert out.dtype == np.float32 and out.shape == g["out"].shape
     err = float(np.sqrt(np.mean((out.astype(np.float64) - g["out"]) ** 2)))
@@ -83,3 +92,72 @@ def test_long_input_segments_vs_oracle():
     assert out.shape == ref.shape
     err = float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2)))
     assert err < 1e-4, err
+
+
+def test_change_rms_matches_reference(golden):
+    """change_rms (convert.py:150-152) on the device vs the reference's output (f0_opts golden)."""
+    from rvc_amd import ops
+    g = golden("f0_opts")
+    src64 = torch.from_numpy(g["rms_src"]).to(DEV)
+    out = torch.from_numpy(g["rms_tgt"]).to(DEV)
+    ops.change_rms(None, src64, out, 8000, 0.35)
+    np.testing.assert_allclose(out.cpu().numpy(), g["rms_out"], rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_f0_post_autotune_override(golden, dtype):
+    """The decode kernels' autotune + shift + f0-file steps (rvc_f0_post) vs the reference: the f64 RMVPE
+    path through rmvpe_decode on a one-hot salience, the f32 CREPE path through crepe_smooth_coarse."""
+    import ctypes
+    from rvc_amd import _lib, ops
+    from rvc_amd.pipeline import f0_override
+    from oracle import pipeline as opl
+    g = golden("f0_opts")
+    c = opl.Consts(48000)
+    rep, off = f0_override(g["inp_f0"], 1)
+    if dtype == "f64":
+        # a salience with one bin (i) above threshold decodes to f0 = 10 * 2^((20 i + 1997.379...) / 1200)
+        T = 600
+        rng = np.random.default_rng(5)
+        bins = rng.integers(0, 360, T)
+        sal = np.zeros((360, T), np.float32)
+        sal[bins, np.arange(T)] = 0.9
+        sal[:, ::13] = 0.0  # unvoiced frames (autotune moves them to 49 * strength)
+        post = ops.F0Post(0.6, rep, off, DEV)
+        coarse = torch.empty(T, dtype=torch.int64, device=DEV)
+        pitchf = torch.empty(T, device=DEV)
+        f0 = torch.empty(T, dtype=torch.float64, device=DEV)
+        ops.rmvpe_decode(torch.from_numpy(sal).to(DEV), T, T, 0.03, 2 ** (3 / 12), f0, coarse, pitchf, post)
+        raw = np.where(sal.max(0) > 0.03, 10 * 2 ** ((20 * bins + 1997.3794084376191) / 1200), 0.0)
+        raw[raw == 10] = 0
+        ref_c, ref_f0 = opl.coarse_f0(raw, 3, c, 0.6, g["inp_f0"])
+        np.testing.assert_allclose(f0.cpu().numpy(), ref_f0, rtol=1e-12)
+    else:
+        track = g["f32"][:600].copy()
+        T = track.size
+        post = ops.F0Post(0.75, rep, off, DEV)
+        # pd = 1 everywhere; mean-3 smoothing is undone by feeding a constant-run track (each value x3)
+        f0r = np.repeat(track, 3)
+        pd = np.ones_like(f0r)
+        T3 = f0r.size
+        coarse = torch.empty(T3, dtype=torch.int64, device=DEV)
+        pitchf = torch.empty(T3, device=DEV)
+        lib = _lib.load()
+        st = post.struct(T3)
+        _lib.check(lib.rvc_crepe_smooth_coarse(ops._p(torch.from_numpy(f0r).to(DEV)),
+                                               ops._p(torch.from_numpy(pd).to(DEV)), T3, ctypes.c_float(2 ** (3 / 12)),
+                                               c.f0_mel_min, c.f0_mel_max, ctypes.byref(st), ops._p(coarse),
+                                               ops._p(pitchf), ops._stream()), "crepe_smooth_coarse")
+        sm = np.convolve(f0r, np.ones(3, np.float32), "same").astype(np.float32)
+        cnt = np.full(T3, 3.0, np.float32)
+        cnt[0] = cnt[-1] = 2
+        sm = (sm / cnt).astype(np.float32)
+        at = opl.autotune_f0(sm, 0.75)
+        ref_f0 = at * np.float32(2 ** (3 / 12))
+        ref_f0[off: off + rep.size] = rep[:max(0, min(rep.size, T3 - off))]
+        # interior frames of each run are exact copies; compare those (edges go through the mean)
+        inner = np.arange(T3) % 3 == 1
+        np.testing.assert_allclose(pitchf.cpu().numpy()[inner], ref_f0[inner], rtol=1e-6)
+        return
+    np.testing.assert_array_equal(coarse.cpu().numpy(), ref_c)
+    np.testing.assert_array_equal(pitchf.cpu().numpy(), ref_f0.astype(np.float32))

@@ -79,7 +79,19 @@ def test_filtfilt_matches_reference(golden):
     np.testing.assert_allclose(signal.filtfilt(opl.BH, opl.AH, g["x"]), g["y"], rtol=0, atol=1e-12)
 
 
-@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1"])
+def golden_opts(g):
+    """The VC.pipeline options a golden case was generated with (make_golden.gen_pipeline)."""
+    opts = {}
+    if "f0_autotune_strength" in g:
+        opts["autotune_strength"] = float(g["f0_autotune_strength"])
+    if "f0_lines" in g:
+        opts["inp_f0"] = np.array([[float(v) for v in ln.split(",")] for ln in g["f0_lines"]], dtype=np.float32)
+    if "volume_envelope" in g:
+        opts["volume_envelope"] = float(g["volume_envelope"])
+    return opts
+
+
+@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1", "pipeline_48k_v2_opts"])
 def test_pipeline_matches_reference(golden, name):
     g = golden(name)
     sr, version, seed = int(g["sr"]), str(g["version"]), int(g["seed"])
@@ -95,9 +107,26 @@ def test_pipeline_matches_reference(golden, name):
         return a
 
     out = opl.pipeline(Wc, Ws, Wr, mb, ck["config"], 0, g["audio"].astype(np.float32), float(g["pitch"]), version,
-                       float(g["protect"]), noise)
+                       float(g["protect"]), noise, **golden_opts(g))
     assert out.shape == g["out"].shape
     assert rms(out, g["out"]) < 1e-5
+
+
+def test_f0_options_match_reference(golden):
+    """Autotune.autotune_f0 on f64 and f32 tracks (convert.py:168-179), get_f0 with autotune + pitch shift +
+    f0-file override (convert.py:304-323), change_rms (convert.py:150-152) -- vs the reference's outputs."""
+    g = golden("f0_opts")
+    np.testing.assert_array_equal(opl.autotune_f0(g["f64"].copy(), 0.75), g["at64"])
+    at32 = opl.autotune_f0(g["f32"].copy(), 0.75)
+    assert at32.dtype == np.float32
+    np.testing.assert_array_equal(at32, g["at32"])
+    c = opl.Consts(48000)
+    coarse, f0 = opl.coarse_f0(g["track"].copy(), 3, c, 0.6, g["inp_f0"])
+    np.testing.assert_array_equal(f0, g["f0"])
+    np.testing.assert_array_equal(coarse, g["coarse"])
+    out = opl.change_rms(g["rms_src"], 16000, g["rms_tgt"].copy(), 16000, 0.35)
+    assert out.dtype == g["rms_out"].dtype
+    np.testing.assert_array_equal(out, g["rms_out"])
 
 
 def test_coarse_quantiser_sweep():
