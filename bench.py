@@ -28,6 +28,9 @@ import torch  # noqa: E402
 METRIC = "audio-seconds/sec/GPU (xRT) end-to-end VC, 48k v2; 1/2/4/8 GPU scaling"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 PEAK_X6_TFLOPS = 2500.0 / 6  # bf16 dense MFMA peak (~2.5 PF) over the six split-bf16 passes per f32 product
+DTYPES = {"fp32": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
+          "bf16x3": "bf16x3 (3-pass split-bf16 MFMA convs, f32 accumulate; f32 elsewhere)",
+          "bf16": "bf16 (bf16-operand MFMA convs, f32 accumulate; f32 elsewhere)"}
 
 
 def build_models(dev, sr=48000, version="v2", seed=1234):
@@ -129,6 +132,8 @@ def main():
     # variants beyond the headline config (BASELINE configs 3/5 ingredients); defaults = configs[1]
     ap.add_argument("--sr", type=int, default=48000, choices=[32000, 40000, 48000])
     ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"],
+                    help="split-bf16 conv engine arithmetic: 6 / 3 / 1 bf16 MFMA passes per product")
     ap.add_argument("--index-rate", type=float, default=0.0,
                     help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
@@ -144,8 +149,11 @@ def main():
     dev = f"cuda:{local}"
     torch.cuda.set_device(local)
 
-    from rvc_amd import synthetic
+    from rvc_amd import ops, synthetic
     from rvc_amd.shard import gather_waveforms
+    ops.set_precision(args.precision)
+    npass = ops.PASSES[args.precision]
+    peak = 2500.0 / npass  # bf16 dense MFMA peak over the passes per product
     vc, hub, net_g = build_models(dev, sr=args.sr)
     index = None
     if args.index_rate > 0:
@@ -193,10 +201,10 @@ def main():
         n, ms, flops = probe.summary(engine=1)  # dominant family: the split-bf16 conv engine
         n32, ms32, fl32 = probe.summary(engine=0)
         achieved = flops / (ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_X6_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_X6_TFLOPS, 4), "traffic": None,
-                "kernel": "conv_x6_kernel<*> (implicit-GEMM conv, f32 via 6 split-bf16 MFMA passes); achieved = "
-                          "algorithmic f32 FLOPs / kernel time; peak = bf16 dense MFMA peak / 6",
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": f"conv_x6_kernel<*> (implicit-GEMM conv, {npass} split-bf16 MFMA pass(es) per product); "
+                          f"achieved = algorithmic FLOPs / kernel time; peak = bf16 dense MFMA peak / {npass}",
                 "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "algorithmic_gflop_per_step": round(flops / 1e9, 1), "kernel_ms_per_step": round(ms, 3),
                 "f32_engine": {"launches": n32, "kernel_ms": round(ms32, 3), "gflop": round(fl32 / 1e9, 1),
@@ -207,7 +215,7 @@ def main():
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "audio-s/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPES[args.precision],
                 "data": "synthetic 16 kHz audio (SURVEY §8d generator), random-init weights of the true shapes",
                 "config": {"workload": f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, one "
                                        f"{args.seconds:g} s clip per GPU per step, "

@@ -83,9 +83,11 @@ typedef struct rvc_conv1d_args {
     int toff[16];
     /* Split-bf16 engine: wx = the same weights pre-split into bf16 h/m/l planes by
        rvc_conv1d_pack_x6 (NULL = f32 MFMA engine).  Used for stride-1, ungrouped, 1-D convs;
-       other shapes ignore it.  wx_nmf = its padded 16-row fragment count. */
+       other shapes ignore it.  wx_nmf = its padded 16-row fragment count.
+       wx_passes: bf16 MFMA passes per product -- 0 or 6 = f32-accurate (hH+hM+mH+hL+mM+lH),
+       3 = hH+hM+mH (16-bit operand mantissas), 1 = hH (bf16 operands); f32 accumulation always. */
     const void* wx;
-    int wx_nmf, _pad1;
+    int wx_nmf, wx_passes;
 } rvc_conv1d_args;
 
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned

@@ -14,6 +14,7 @@
 // conditioning), activation, residual add, accumulate, polyphase/strided stores (ConvTranspose)
 // and border masking (2-D mode).
 #include "rvc_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -40,7 +41,8 @@ struct ConvParams {
     int ntoff, wrap;
     int toff[16];
     const uint4* wx;  // split-bf16 packed weights (x6 engine) or null
-    int wx_nmf, wx_nch;
+    int wx_nmf, wx_nch, wx_passes;
+    int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
 };
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
@@ -385,16 +387,29 @@ RVC_DEV void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
 
 constexpr int X6_NI_MAX = 6;  // staged (position, 8-channel group) items per loader thread: 4 * span <= 256 NI
 
+// NP = MFMA passes per product: 6 (f32-accurate, above), 3 (hH + hM + mH: 16-bit-mantissa products,
+// ~2^-16 relative) or 1 (hH: plain bf16 operands, f32 accumulation).  Only the NPL = 3 / 2 / 1 planes a
+// pass set reads are staged and loaded.  LDS rows are [pos][NPL planes][4 x 16 B]; the 16-B group is
+// XOR-swizzled so that 16 consecutive positions of one (plane, group) hit 16 distinct bank quads:
+// NPL 3 and 1 by (pos>>2)&3 within the plane, NPL 2 by (pos>>1)&7 across the two planes.
+template <int NPL>
+RVC_DEV int x_slot(int pos, int q, int g) {
+    if constexpr (NPL == 2) return pos * 8 + ((4 * q + g) ^ ((pos >> 1) & 7));
+    else return pos * (4 * NPL) + 4 * q + (g ^ ((pos >> 2) & 3));
+}
+
 // Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
 // input prefetch never wait on each other.  One workgroup barrier per 32-channel chunk hands the
 // next staged X buffer (double-buffered in LDS) to the compute waves.
-template <int FM, int FN, int WM, int WN, int X6_NI>
+template <int FM, int FN, int WM, int WN, int X6_NI, int NP>
 __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4, "4 compute waves");
+    static_assert(NP == 6 || NP == 3 || NP == 1, "6, 3 or 1 passes");
+    constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
-    extern __shared__ uint4 xs[];  // [2 buffers][span][3 planes][4 x 16 B]
+    extern __shared__ uint4 xs[];  // [2 buffers][span][NPL planes][4 x 16 B]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int zb = blockIdx.z;
     const int split = zb % p.ksplit;
@@ -410,7 +425,7 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
     const int ch_beg = split * p.chunks_per_split;
     const int ch_end = min(nch, ch_beg + p.chunks_per_split);
     const int nck = ch_end - ch_beg;
-    const int bufsz = 3 * span * 4;  // uint4 per buffer
+    const int bufsz = NPL * span * 4;  // uint4 per buffer
 
     if (wave >= 4) {
         // ---------------- loader waves: chunk c+1 split into LDS while chunk c computes
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
                 for (int e = 0; e < 8; ++e) {
                     int c = ch * 32 + ig8[it] * 8 + e;
                     c = c < Cig ? c : Cig - 1;
-                    r[it][e] = xb[(int64_t)c * lin + qc];
+                    r[it][e] = (p.dbg & 4) ? 0.f : xb[(int64_t)c * lin + qc];
                 }
             }
         };
@@ -465,10 +480,9 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
                         lw[e2] = l2[0] | (l2[1] << 16);
                     }
                     const int pos = ipos[it];
-                    const int slot = pos * 12 + (ig8[it] ^ ((pos >> 2) & 3));
-                    dst[slot] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-                    dst[slot + 4] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
-                    dst[slot + 8] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                    dst[x_slot<NPL>(pos, 0, ig8[it])] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                    if constexpr (NPL >= 2) dst[x_slot<NPL>(pos, 1, ig8[it])] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+                    if constexpr (NPL >= 3) dst[x_slot<NPL>(pos, 2, ig8[it])] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
                 }
             }
         };
@@ -494,7 +508,7 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
     const int wm = wave / WN, wn = wave % WN;
     const uint4* wxp = p.wx + (int64_t)phase * K * nch * nmf * 3 * 64;
     const int mf0 = m0g / 16 + wm * FM;
-    auto aload = [&](int s, uint4 (&a)[3][FM]) __attribute__((always_inline)) {
+    auto aload = [&](int s, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
         // wave-uniform fragment base (scalar registers) + one per-lane offset: saddr loads, no
         // per-fragment 64-bit address registers
         const int ch = s / K, t = s - ch * K;
@@ -503,7 +517,7 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) a[q][i] = src[(i * 3 + q) * 64 + lane];
+            for (int q = 0; q < NPL; ++q) a[q][i] = src[(i * 3 + q) * 64 + lane];
     };
     floatx4 acc[FM][FN];
 #pragma unroll
@@ -512,38 +526,64 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
         for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int ln = lane & 15, lg = lane >> 4;
     const int pb = wn * 16 * FN + ln;
-    auto compute = [&](int t, const uint4* xbuf, const uint4 (&a)[3][FM]) __attribute__((always_inline)) {
-        uint4 bq[3][FN];
+    // B operands are read from LDS one column fragment j at a time (NPL ds_read_b128 each), the next
+    // fragment's reads issued before the current one's MFMAs: only 2 x NPL B registers stay live, which
+    // leaves room for the PD-deep weight prefetch ring at 2 waves per SIMD.
+    auto compute = [&](int t, const uint4* xbuf, const uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
+        const int tof = tap_off(p, t);
+        auto bload = [&](int j, uint4 (&bq)[NPL]) __attribute__((always_inline)) {
+            const int pos = pb + 16 * j + tof;
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) bq[q] = xbuf[x_slot<NPL>(pos, q, lg)];
+        };
+        uint4 bb[2][NPL];
+        bload(0, bb[0]);
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-            const int pos = pb + 16 * j + tap_off(p, t);
-            const int slot = pos * 12 + (lg ^ ((pos >> 2) & 3));
+            if (j + 1 < FN) bload(j + 1, bb[(j + 1) & 1]);
+            const uint4 (&bq)[NPL] = bb[j & 1];
+            if (p.dbg & 2) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) bq[q][j] = xbuf[slot + 4 * q];
+                for (int i = 0; i < FM; ++i) acc[i][j][0] += __builtin_bit_cast(float, (a[0][i].x ^ bq[NPL - 1].y) & 0x3fffffu);
+                continue;
+            }
+            // NP passes over the FM accumulators of this column fragment
+            constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
+            constexpr int PB[6] = {0, 1, 0, 2, 1, 0};
+#pragma unroll
+            for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+                for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
         }
-        // six passes, each over all FM x FN accumulators (no back-to-back dependent MFMAs)
-        constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
-        constexpr int PB[6] = {0, 1, 0, 2, 1, 0};
-#pragma unroll
-        for (int ps = 0; ps < 6; ++ps)
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]][j], acc[i][j]);
     };
     const int s_beg = ch_beg * K, s_end = ch_end * K;
-    uint4 a0[3][FM], a1[3][FM];
-    if (s_beg < s_end) aload(s_beg, a0);
+    // Weight fragments are prefetched PD k-steps ahead through a ring of NB = PD + 1 register buffers
+    // (the L2 latency must hide behind PD steps of MFMAs: 1 step of 6 passes, 2 of 3, 4 of 1).  The
+    // sched_barrier pins each prefetch ahead of the MFMAs it must overlap (hipcc otherwise sinks the
+    // independent loads below them and every k-step pays the full L2 round trip).
+    constexpr int PD = NP == 6 ? 1 : (NP == 3 ? 2 : 4);
+    constexpr int NB = PD + 1;
+    uint4 abuf[NB][NPL][FM];
+#pragma unroll
+    for (int i = 0; i < PD; ++i)
+        if (s_beg + i < s_end) aload(s_beg + i, abuf[i]);
     __syncthreads();  // chunk 0 staged
-    auto step = [&](int s, const uint4 (&cur)[3][FM], uint4 (&nxt)[3][FM]) __attribute__((always_inline)) {
-        const int ch = s / K, t = s - ch * K;
-        if (s + 1 < s_end) aload(s + 1, nxt);
-        compute(t, xs + ((ch - ch_beg) & 1) * bufsz, cur);
-        if (t == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
-    };
-    for (int s = s_beg; s < s_end; s += 2) {
-        step(s, a0, a1);
-        if (s + 1 < s_end) step(s + 1, a1, a0);
+    for (int s0 = s_beg; s0 < s_end; s0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int s = s0 + u;
+            if (s < s_end) {
+                const int ch = s / K, t = s - ch * K;
+                if (s + PD < s_end) aload(s + PD, abuf[(u + PD) % NB]);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(t, xs + ((ch - ch_beg) & 1) * bufsz, abuf[u]);
+                if (t == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
+            }
+        }
+    }
+    if (p.dbg & 1) {
+        if (acc[0][0][0] == 1234.5f) p.y[lane] = acc[FM - 1][FN - 1][3];  // keep the loop live
+        return;
     }
     conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
 }
@@ -571,11 +611,18 @@ hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int FM, int FN, int WM, int WN, int NP>
+void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
+    // loader items per thread sized to the staged span (unused items would still issue loads)
+    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP>), grid, dim3(512), lds, s, p);
+    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP>), grid, dim3(512), lds, s, p);
+}
+
 template <int FM, int FN, int WM, int WN>
 hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    // loader items per thread sized to the staged span (unused items would still issue loads)
-    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3>), grid, dim3(512), lds, s, p);
-    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6>), grid, dim3(512), lds, s, p);
+    if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
+    else if (p.wx_passes == 3) launch_x6_np<FM, FN, WM, WN, 3>(p, grid, lds, s);
+    else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);
     return hipGetLastError();
 }
 
@@ -595,6 +642,9 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff ? a->toff[i] : 0;
     p.wx = nullptr;
     p.wx_nmf = p.wx_nch = 0;
+    p.wx_passes = a->wx_passes == 0 ? 6 : a->wx_passes;
+    static const int dbg = getenv("RVC_CONV_DEBUG") ? atoi(getenv("RVC_CONV_DEBUG")) : 0;
+    p.dbg = dbg;
 }
 
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
@@ -622,7 +672,8 @@ int max_tap_off(const rvc_conv1d_args* a) {
 bool x6_eligible(const rvc_conv1d_args* a) {
     return a->wx && a->stride == 1 && a->groups == 1 && a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) &&
            a->K <= 16 && X6_BN + max_tap_off(a) <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
-           (int64_t)a->wx_nmf * 16 >= a->Co;
+           (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 || a->wx_passes == 3 ||
+                                                a->wx_passes == 1);
 }
 
 int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& lds) {
@@ -661,7 +712,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
         const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
         split_k(p, tiles, p.wx_nch);
-        lds = (size_t)2 * 3 * p.span * 64;
+        lds = (size_t)2 * (p.wx_passes == 6 ? 3 : (p.wx_passes == 3 ? 2 : 1)) * p.span * 64;
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         return RVC_OK;

@@ -54,6 +54,42 @@ def pack_convT(w: torch.Tensor, u: int) -> tuple[torch.Tensor, int]:
 # Split-bf16 engine switch (the f32-MFMA engine runs when off); RVC_AMD_X6=0 disables it.
 X6 = os.environ.get("RVC_AMD_X6", "1") != "0"
 
+# Arithmetic of the split-bf16 engine (bf16 MFMA passes per product, f32 accumulation):
+#   "fp32"   6 passes, f32-accurate products (the default; BASELINE configs 1-2, 4)
+#   "bf16x3" 3 passes, 16-bit operand mantissas (~2^-16 relative per product)
+#   "bf16"   1 pass, bf16 operands (BASELINE configs 3 and 5)
+PASSES = {"fp32": 6, "bf16x3": 3, "bf16": 1}
+_PRECISION = os.environ.get("RVC_AMD_PRECISION", "fp32")
+if _PRECISION not in PASSES:
+    raise ValueError(f"RVC_AMD_PRECISION must be one of {sorted(PASSES)}")
+
+
+def get_precision() -> str:
+    return _PRECISION
+
+
+def set_precision(name: str) -> str:
+    """Set the conv engine's arithmetic for subsequent launches; returns the previous setting."""
+    global _PRECISION
+    if name not in PASSES:
+        raise ValueError(f"precision must be one of {sorted(PASSES)}, got {name!r}")
+    prev, _PRECISION = _PRECISION, name
+    return prev
+
+
+class precision:
+    """Context manager: ``with ops.precision("bf16"): ...``."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = set_precision(self.name)
+        return self
+
+    def __exit__(self, *a):
+        set_precision(self.prev)
+
 
 def pack_x6(w_km: torch.Tensor, nphase: int, Ci: int, K: int, Co: int):
     """Device KM weights [nphase][Ci*K][Co] -> split-bf16 fragment image for the x6 engine
@@ -185,7 +221,7 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
             a.toff[i] = int(v)
     a.wrap = wrap
     if wx is not None:
-        a.wx, a.wx_nmf = ctypes.c_void_p(wx.data_ptr()), wx_nmf
+        a.wx, a.wx_nmf, a.wx_passes = ctypes.c_void_p(wx.data_ptr()), wx_nmf, PASSES[_PRECISION]
     if flops is None:
         valid = (Lout // wrap - 2) * (wrap - 2) if wrap else (ncols or Lout) * nphase
         flops = 2.0 * B * Co * Cig * K * min(valid, Lout)

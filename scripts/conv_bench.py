@@ -24,8 +24,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", type=str, default="", help="comma list of shape indices")
+    ap.add_argument("--precision", default="fp32")
     args = ap.parse_args()
     from rvc_amd import ops
+    ops.set_precision(args.precision)
     print("lib:", ops._lib.LIB_PATH)
     g = torch.Generator().manual_seed(0)
     tot_ms = tot_fl = 0.0

@@ -75,6 +75,24 @@ def test_conv1d(ops, engine, case):
     close(y, ref)
 
 
+@pytest.mark.parametrize("prec,lo,hi", [("bf16x3", 0.0, 1e-4), ("bf16", 1e-4, 1e-2)])
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] == 1 and c[6] == 1 and c[2] <= 16])
+def test_conv1d_reduced_precision(ops, case, prec, lo, hi):
+    """The split-bf16 engine at 3 passes (hH+hM+mH) and 1 pass (bf16 operands): relative RMS error vs the
+    fp32 reference inside the band each arithmetic implies (the lower bound proves the mode is live)."""
+    Ci, Co, K, s, d, p, g, L = case
+    x = torch.randn(Ci, L, generator=gen(1))
+    w = torch.randn(Co, Ci, K, generator=gen(2)) / math.sqrt(Ci * K)
+    b = torch.randn(Co, generator=gen(3)) * 0.1
+    ref = F.conv1d(x.unsqueeze(0).double(), w.double(), b.double(), s, p, d)[0]
+    c = ops.Conv(w, b)
+    with ops.precision(prec):
+        y = c(x.to(DEV), stride=s, pad=p, dil=d)
+    assert ops.LAST_CONV_ENGINE == 1
+    rel = float(((y.cpu().double() - ref).pow(2).mean() / ref.pow(2).mean()).sqrt())
+    assert lo <= rel < hi, rel
+
+
 def test_conv1d_fused_epilogue(ops, engine):
     Ci, Co, K, L = 64, 64, 5, 3000
     x = torch.randn(Ci, L, generator=gen(4))

@@ -144,8 +144,8 @@ def test_f0_post_autotune_override(golden, dtype):
         pitchf = torch.empty(T3, device=DEV)
         lib = _lib.load()
         st = post.struct(T3)
-        _lib.check(lib.rvc_crepe_smooth_coarse(ops._p(torch.from_numpy(f0r).to(DEV)),
-                                               ops._p(torch.from_numpy(pd).to(DEV)), T3, ctypes.c_float(2 ** (3 / 12)),
+        f0r_d, pd_d = torch.from_numpy(f0r).to(DEV), torch.from_numpy(pd).to(DEV)  # held across the launch
+        _lib.check(lib.rvc_crepe_smooth_coarse(ops._p(f0r_d), ops._p(pd_d), T3, ctypes.c_float(2 ** (3 / 12)),
                                                c.f0_mel_min, c.f0_mel_max, ctypes.byref(st), ops._p(coarse),
                                                ops._p(pitchf), ops._stream()), "crepe_smooth_coarse")
         sm = np.convolve(f0r, np.ones(3, np.float32), "same").astype(np.float32)
