@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"],
                     help="split-bf16 conv engine arithmetic: 6 / 3 / 1 bf16 MFMA passes per product")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one hipGraph per clip (rvc_amd.graph.ClipGraph, BASELINE configs[4])")
     ap.add_argument("--index-rate", type=float, default=0.0,
                     help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
@@ -166,8 +168,16 @@ def main():
     audio_dev = torch.from_numpy(audio).to(dev)  # input resident in HBM before the timed region
     vc.seed = 17 + rank
 
+    clip_graph = None
+    if args.graph:
+        from rvc_amd.graph import ClipGraph
+        clip_graph = ClipGraph(vc, hub, net_g, 0, audio_dev.numel(), 0, "v2", 0.33, index, args.index_rate, args.f0)
+
     def step():
-        out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
+        if clip_graph is not None:
+            out = clip_graph(audio_dev)
+        else:
+            out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
             gather_waveforms([out], dist, dst=0)
@@ -196,8 +206,8 @@ def main():
 
     roof = None
     if rank == 0:
-        with ConvProbe() as probe:
-            step()
+        with ConvProbe() as probe:  # one eager pass (a graph replay launches no host-side conv calls)
+            vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
         n, ms, flops = probe.summary(engine=1)  # dominant family: the split-bf16 conv engine
         n32, ms32, fl32 = probe.summary(engine=0)
         achieved = flops / (ms * 1e-3) / 1e12
@@ -220,7 +230,7 @@ def main():
                 "config": {"workload": f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, one "
                                        f"{args.seconds:g} s clip per GPU per step, "
                                        + (f"IVF-Flat index_rate {args.index_rate:g}" if index is not None else "no index")
-                                       + ", protect 0.33",
+                                       + ", protect 0.33" + (", hipGraph replay per clip" if args.graph else ""),
                            "model": f"RVC v2 {args.sr // 1000}k (NSF-HiFiGAN) + ContentVec + {args.f0}",
                            "global_batch": world,
                            "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",

@@ -156,6 +156,13 @@ int rvc_flip_channels(const float* x, float* out, int64_t B, int64_t C, int64_t 
 int rvc_transpose(const float* in, float* out, int64_t B, int64_t R, int64_t C, rvc_stream_t stream);
 /* standard normal noise, Philox4x32-10 counter stream (seed, offset) */
 int rvc_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, rvc_stream_t stream);
+/* the same with seed += *seed_add read on the device (seed_add may be NULL): graph replays draw fresh noise */
+int rvc_randn_ex(float* out, int64_t n, uint64_t seed, uint64_t offset, const uint64_t* seed_add,
+                 rvc_stream_t stream);
+/* symmetric triangular draws on [lo, hi] (CREPE's dither, scipy.stats.triang(c=0.5), CREPE.py:118),
+ * same counter stream; used when the CREPE pass is graph-captured (host numpy draws cannot be) */
+int rvc_rand_triang(float* out, int64_t n, float lo, float hi, uint64_t seed, uint64_t offset,
+                    const uint64_t* seed_add, rvc_stream_t stream);
 /* NSF harmonic source: SineGen + Linear(1,1) + tanh    synthesizers.py:69-112
  * f0 [B][T] -> har [B][T*upp]; noise [B][T*upp]; work: [B][T] floats scratch */
 int rvc_sine_source(const float* f0, const float* noise, float* har, float* work, int64_t B, int64_t T, int upp,

@@ -42,6 +42,7 @@ struct ConvParams {
     int toff[16];
     const uint4* wx;  // split-bf16 packed weights (x6 engine) or null
     int wx_nmf, wx_nch, wx_passes;
+    int rot;  // x6: rotate each block's (chunk, tap) order so that the CUs of an XCD spread over the weight image
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
 };
 
@@ -426,6 +427,11 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
     const int ch_end = min(nch, ch_beg + p.chunks_per_split);
     const int nck = ch_end - ch_beg;
     const int bufsz = NPL * span * 4;  // uint4 per buffer
+    // Blocks co-resident on one XCD (ids = x mod 8) walk the k-steps from different starting
+    // (chunk, tap): in lockstep they would all read the same few weight lines, i.e. the same L2 channels.
+    const int rseed = p.rot ? (int)(blockIdx.x >> 3) : 0;
+    const int rt = rseed % K, rc = (rseed / K) % max(nck, 1);
+    auto pchunk = [&](int i) __attribute__((always_inline)) { return ch_beg + (min(i, nck - 1) + rc) % nck; };
 
     if (wave >= 4) {
         // ---------------- loader waves: chunk c+1 split into LDS while chunk c computes
@@ -487,14 +493,14 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
             }
         };
         // prologue: chunk 0 -> LDS buffer 0, chunk 1 in flight
-        xload(ch_beg, xr[0]);
-        xload(min(ch_beg + 1, nch - 1), xr[1]);
-        xstore(ch_beg, xr[0], xs);
+        xload(pchunk(0), xr[0]);
+        xload(pchunk(1), xr[1]);
+        xstore(pchunk(0), xr[0], xs);
         __syncthreads();
         // iteration i (chunk ch_beg + i computing): regs slot (i+1)&1 holds chunk i+1; slot i&1 is free
         auto iter = [&](int i, float (&nxt)[X6_NI][8], float (&fre)[X6_NI][8]) __attribute__((always_inline)) {
-            xload(min(ch_beg + i + 2, nch - 1), fre);
-            if (i + 1 < nck) xstore(ch_beg + i + 1, nxt, xs + ((i + 1) & 1) * bufsz);
+            xload(pchunk(i + 2), fre);
+            if (i + 1 < nck) xstore(pchunk(i + 1), nxt, xs + ((i + 1) & 1) * bufsz);
             __syncthreads();
         };
         for (int i = 0; i < nck; i += 2) {
@@ -506,12 +512,20 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
 
     // ---------------- compute waves
     const int wm = wave / WN, wn = wave % WN;
+    const int s_beg = ch_beg * K, s_end = ch_end * K;
     const uint4* wxp = p.wx + (int64_t)phase * K * nch * nmf * 3 * 64;
     const int mf0 = m0g / 16 + wm * FM;
+    // logical k-step s (chunk-major from s_beg) -> physical (chunk, tap)
+    auto kstep = [&](int s, int& ch, int& t) __attribute__((always_inline)) {
+        const int i = (s - s_beg) / K, tl = s - s_beg - i * K;
+        ch = pchunk(i);
+        t = tl + rt < K ? tl + rt : tl + rt - K;
+    };
     auto aload = [&](int s, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
         // wave-uniform fragment base (scalar registers) + one per-lane offset: saddr loads, no
         // per-fragment 64-bit address registers
-        const int ch = s / K, t = s - ch * K;
+        int ch, t;
+        kstep(s, ch, t);
         const int frag0 = __builtin_amdgcn_readfirstlane((t * nch + ch) * nmf + mf0);
         const uint4* src = wxp + (int64_t)frag0 * 3 * 64;
 #pragma unroll
@@ -556,12 +570,13 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
                 for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
         }
     };
-    const int s_beg = ch_beg * K, s_end = ch_end * K;
     // Weight fragments are prefetched PD k-steps ahead through a ring of NB = PD + 1 register buffers
     // (the L2 latency must hide behind PD steps of MFMAs: 1 step of 6 passes, 2 of 3, 4 of 1).  The
     // sched_barrier pins each prefetch ahead of the MFMAs it must overlap (hipcc otherwise sinks the
     // independent loads below them and every k-step pays the full L2 round trip).
-    constexpr int PD = NP == 6 ? 1 : (NP == 3 ? 2 : 4);
+    // depth: as many k-steps as fit a 24-uint4 (96-VGPR) ring, at most 4
+    constexpr int PD_FIT = 24 / (NPL * FM) - 1;
+    constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > 4 ? 4 : PD_FIT);
     constexpr int NB = PD + 1;
     uint4 abuf[NB][NPL][FM];
 #pragma unroll
@@ -573,11 +588,12 @@ __global__ __launch_bounds__(512) void conv_x6_kernel(ConvParams p) {
         for (int u = 0; u < NB; ++u) {
             const int s = s0 + u;
             if (s < s_end) {
-                const int ch = s / K, t = s - ch * K;
+                const int i = (s - s_beg) / K, tl = s - s_beg - i * K;
+                const int t = tl + rt < K ? tl + rt : tl + rt - K;
                 if (s + PD < s_end) aload(s + PD, abuf[(u + PD) % NB]);
                 __builtin_amdgcn_sched_barrier(0);
-                compute(t, xs + ((ch - ch_beg) & 1) * bufsz, abuf[u]);
-                if (t == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
+                compute(t, xs + (i & 1) * bufsz, abuf[u]);
+                if (tl == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
             }
         }
     }
@@ -645,6 +661,8 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.wx_passes = a->wx_passes == 0 ? 6 : a->wx_passes;
     static const int dbg = getenv("RVC_CONV_DEBUG") ? atoi(getenv("RVC_CONV_DEBUG")) : 0;
     p.dbg = dbg;
+    static const int rot = getenv("RVC_X6_ROT") ? atoi(getenv("RVC_X6_ROT")) : 1;
+    p.rot = rot;
 }
 
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip

@@ -14,36 +14,67 @@ RVC_DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
     }
 }
 
-__global__ void randn_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread -> 4 normals
+// kind 0: standard normals (Box-Muller); kind 1: symmetric triangular on [lo, hi] (inverse CDF).
+// seed_add (device, may be null) is added to the seed at run time, so that a captured graph draws
+// fresh noise on every replay (graph.py).
+__global__ void rand_kernel(float* out, int64_t n, uint64_t seed, uint64_t offset, const uint64_t* seed_add, int kind,
+                            float lo, float hi) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread -> 4 draws
     int64_t base = i * 4;
     if (base >= n) return;
+    if (seed_add) seed += *seed_add;
     uint64_t ctr = (uint64_t)i + offset;
     uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x7A3Bu, 0x52u};
     philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     float r[4];
+    if (kind == 0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        float u1 = ((c[2 * j] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
-        float u2 = (c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
-        float rad = sqrtf(-2.0f * logf(u1));
-        float s, co;
-        sincosf(6.2831853071795864f * u2, &s, &co);
-        r[2 * j] = rad * co;
-        r[2 * j + 1] = rad * s;
+        for (int j = 0; j < 2; ++j) {
+            float u1 = ((c[2 * j] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+            float u2 = (c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
+            float rad = sqrtf(-2.0f * logf(u1));
+            float s, co;
+            sincosf(6.2831853071795864f * u2, &s, &co);
+            r[2 * j] = rad * co;
+            r[2 * j + 1] = rad * s;
+        }
+    } else {
+        const float w = hi - lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float u = ((c[j] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+            r[j] = u < 0.5f ? lo + w * sqrtf(0.5f * u) : hi - w * sqrtf(0.5f * (1.0f - u));
+        }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         if (base + j < n) out[base + j] = r[j];
 }
 
-extern "C" int rvc_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, rvc_stream_t stream) {
-    RVC_CHECK_ARG(out && n >= 0, "randn: bad args");
+static int launch_rand(float* out, int64_t n, uint64_t seed, uint64_t offset, const uint64_t* seed_add, int kind,
+                       float lo, float hi, rvc_stream_t stream) {
+    RVC_CHECK_ARG(out && n >= 0, "rand: bad args");
     if (n == 0) return RVC_OK;
     int64_t thr = (n + 3) / 4;
-    hipLaunchKernelGGL(randn_kernel, dim3(cdiv(thr, 256)), dim3(256), 0, (hipStream_t)stream, out, n, seed, offset);
+    hipLaunchKernelGGL(rand_kernel, dim3(cdiv(thr, 256)), dim3(256), 0, (hipStream_t)stream, out, n, seed, offset,
+                       seed_add, kind, lo, hi);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
+}
+
+extern "C" int rvc_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, rvc_stream_t stream) {
+    return launch_rand(out, n, seed, offset, nullptr, 0, 0.f, 0.f, stream);
+}
+
+extern "C" int rvc_randn_ex(float* out, int64_t n, uint64_t seed, uint64_t offset, const uint64_t* seed_add,
+                            rvc_stream_t stream) {
+    return launch_rand(out, n, seed, offset, seed_add, 0, 0.f, 0.f, stream);
+}
+
+extern "C" int rvc_rand_triang(float* out, int64_t n, float lo, float hi, uint64_t seed, uint64_t offset,
+                               const uint64_t* seed_add, rvc_stream_t stream) {
+    RVC_CHECK_ARG(hi > lo, "rand_triang: hi <= lo");
+    return launch_rand(out, n, seed, offset, seed_add, 1, lo, hi, stream);
 }
 
 // ---------------------------------------------------------------- TextEncoder input

@@ -66,6 +66,8 @@ SIGNATURES = {
     "rvc_flip_channels": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_transpose": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_randn": [c_void_p, c_int64, c_uint64, c_uint64, c_void_p],
+    "rvc_randn_ex": [c_void_p, c_int64, c_uint64, c_uint64, c_void_p, c_void_p],
+    "rvc_rand_triang": [c_void_p, c_int64, c_float, c_float, c_uint64, c_uint64, c_void_p, c_void_p],
     "rvc_sine_source": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_float, c_float, c_float,
                         c_void_p],
     "rvc_stft_frames": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p],

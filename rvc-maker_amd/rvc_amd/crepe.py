@@ -114,13 +114,19 @@ class CrepeAMD:
             trace["probs"] = probs.t().cpu().numpy().copy()
         if self.dither_fn is not None:
             dither = np.asarray(self.dither_fn(T), dtype=np.float64)
+            dither_d = torch.from_numpy(dither.astype(np.float32)).to(dev)
+        elif ops.graph_mode():  # captured pass: the same triangular law drawn on the device (graph.py)
+            dither_d = ops.rand_triang(torch.empty(T, device=dev), -20.0, 20.0, 0x43524550, 0)
         else:  # scipy.stats.triang.rvs(c=0.5, loc=-20, scale=40): numpy's triangular on [-20, 20]
             dither = np.random.triangular(-20.0, 0.0, 20.0, size=T)
-        dither_d = torch.from_numpy(dither.astype(np.float32)).to(dev)
+            dither_d = torch.from_numpy(dither.astype(np.float32)).to(dev)
         lib = _lib.load()
         need = lib.rvc_crepe_decode_ws_bytes(T)
         ws = ops._workspace(dev, need, "crepe")
-        seq_off = torch.tensor(seq, dtype=torch.int64, device=dev)
+        key = (str(dev), T)  # batch offsets, resident per length (no host copy inside a captured pass)
+        seq_off = self.__dict__.setdefault("_seq_off", {}).get(key)
+        if seq_off is None:
+            seq_off = self._seq_off[key] = torch.tensor(seq, dtype=torch.int64, device=dev)
         f0r = torch.empty(T, device=dev)
         pdr = torch.empty(T, device=dev)
         check(lib.rvc_crepe_decode(ops._p(probs), T, self.lo, self.hi, ops._p(seq_off), len(seq) - 1,

@@ -295,8 +295,41 @@ def transpose(x, out, B, R, C):
     return out
 
 
+# Device-resident seed added to every Philox draw while set (graph.ClipGraph: replays draw fresh noise).
+_DEV_SEED = None
+
+
+class device_seed:
+    """``with ops.device_seed(t):`` -- t: device int64 [1]; draws use seed + t[0], read at run time."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __enter__(self):
+        global _DEV_SEED
+        self.prev, _DEV_SEED = _DEV_SEED, self.t
+        return self
+
+    def __exit__(self, *a):
+        global _DEV_SEED
+        _DEV_SEED = self.prev
+
+
+def graph_mode() -> bool:
+    """True while a device seed is set, i.e. while ClipGraph warms up or captures."""
+    return _DEV_SEED is not None
+
+
 def randn(out, seed, offset=0):
-    check(_lib.load().rvc_randn(_p(out), out.numel(), seed, offset, _stream()), "randn")
+    add = _p(_DEV_SEED) if _DEV_SEED is not None else None
+    check(_lib.load().rvc_randn_ex(_p(out), out.numel(), seed, offset, add, _stream()), "randn")
+    return out
+
+
+def rand_triang(out, lo, hi, seed, offset=0):
+    """Symmetric triangular draws on [lo, hi] (Philox counter stream; device seed added when set)."""
+    add = _p(_DEV_SEED) if _DEV_SEED is not None else None
+    check(_lib.load().rvc_rand_triang(_p(out), out.numel(), lo, hi, seed, offset, add, _stream()), "rand_triang")
     return out
 
 

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", type=str, default="", help="comma list of shape indices")
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--check", action="store_true", help="compare each shape with the f32-MFMA engine")
     args = ap.parse_args()
     from rvc_amd import ops
     ops.set_precision(args.precision)
@@ -52,7 +53,18 @@ def main():
         fl = 2.0 * C * C * K * L
         tot_ms += ms
         tot_fl += fl
-        print(f"C={C:4d} K={K:2d} d={d} L={L:8d}: {ms * 1e3:9.1f} us {fl / ms / 1e9:7.1f} TFLOP/s")
+        chk = ""
+        if args.check:
+            wx, conv.wx = conv.wx, None  # f32-MFMA engine
+            yr = torch.empty_like(y)
+            conv(x, pad=p, dil=d, out=yr, res=res, in_act=ops.ACT_LRELU, in_slope=0.1)
+            conv.wx = wx
+            fn()
+            torch.cuda.synchronize()
+            rel = float((y - yr).pow(2).mean().sqrt() / (yr - res).pow(2).mean().sqrt())
+            chk = f"  rel err vs f32 engine {rel:.2e}"
+            assert rel < {"fp32": 1e-5, "bf16x3": 1e-4, "bf16": 2e-2}[args.precision], chk
+        print(f"C={C:4d} K={K:2d} d={d} L={L:8d}: {ms * 1e3:9.1f} us {fl / ms / 1e9:7.1f} TFLOP/s{chk}")
     print(f"total {tot_ms:.3f} ms, {tot_fl / tot_ms / 1e9:.1f} TFLOP/s")
 
 
