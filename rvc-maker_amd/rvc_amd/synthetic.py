@@ -315,3 +315,26 @@ def synthetic_audio(seconds: float, seed: int = 1000, sr: int = 16000) -> np.nda
     if peak > 0.9:
         x *= 0.9 / peak
     return x.astype(np.float32)
+
+
+def silence_layout_audio(layout, seed: int = 5000, sr: int = 16000, floor: float = 1e-5) -> np.ndarray:
+    """Test signal for the silence slicer (edges.py): ``layout`` = [(seconds, voiced?), ...]; voiced
+    spans are the §8(d) glide, silent spans seeded noise at ``floor`` (≈ -100 dBFS, no exact ties)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parts = []
+    for k, (sec, voiced) in enumerate(layout):
+        n = int(round(sec * sr))
+        if voiced:
+            parts.append(synthetic_audio(sec, seed=seed + 1 + k, sr=sr)[:n].astype(np.float64))
+        else:
+            parts.append(floor * rng.standard_normal(n))
+    return np.concatenate(parts).astype(np.float32)
+
+
+# slicer cases: leading / short (< max_sil_kept) / medium (1-2x) / long (> 2x) middle silences, trailing
+SLICER_LAYOUTS = {
+    "mixed": [(1.0, 0), (6.0, 1), (0.7, 0), (6.0, 1), (7.0, 0), (6.0, 1), (11.0, 0), (5.0, 1), (2.0, 0)],
+    "no_silence": [(8.0, 1)],
+    "short_input": [(0.5, 0), (3.0, 1)],
+    "lead_long": [(12.0, 0), (6.0, 1), (0.3, 0), (2.0, 1)],
+}

@@ -330,12 +330,57 @@ def gen_f0_opts(seed):
     print("f0_opts", float(np.abs(at64 - f64).max()), coarse[:5], float(np.abs(cr).mean()))
 
 
+def gen_edges(seed):
+    """The reference's own silence slicer / RMS / restore (utils.py:172-250, preprocess.py:45-127) on
+    the layouts of ``synthetic.SLICER_LAYOUTS`` (inputs rebuilt from their seeds on the test side)."""
+    from main.library.utils import cut, restore
+    from main.inference.preprocess import Slicer, get_rms
+    out = {"seed": seed}
+    for name, layout in synthetic.SLICER_LAYOUTS.items():
+        audio = synthetic.silence_layout_audio(layout, seed=seed)
+        chunks = cut(audio, 16000, db_thresh=-60, min_interval=500)
+        out[f"{name}_bounds"] = np.array([[s, e] for _, s, e in chunks], dtype=np.int64)
+        out[f"{name}_lens"] = np.array([len(c) for c, _, _ in chunks], dtype=np.int64)
+        out[f"{name}_sums"] = np.array([float(np.sum(c, dtype=np.float64)) for c, _, _ in chunks])
+        conv = [(s, e, np.repeat(c, 3) * 0.5) for c, s, e in chunks]  # stand-in "converted" chunks at 3x
+        rest = restore(conv, total_len=len(audio), dtype=conv[0][2].dtype) if len(chunks) > 1 else conv[0][2]
+        out[f"{name}_restore_len"] = np.int64(len(rest))
+        out[f"{name}_restore_sum"] = float(np.sum(rest, dtype=np.float64))
+        out[f"{name}_restore_nz"] = np.flatnonzero(rest == 0)[:: 997][:200]
+        # dataset preprocessing slicer at a training rate (preprocess.py:131)
+        a40 = synthetic.silence_layout_audio(layout, seed=seed, sr=40000)
+        sl = Slicer(sr=40000, threshold=-42, min_length=1500, min_interval=400, hop_size=15, max_sil_kept=500)
+        ch40 = sl.slice(a40)
+        out[f"{name}_pre_lens"] = np.array([len(c) for c in ch40], dtype=np.int64)
+        out[f"{name}_pre_sums"] = np.array([float(np.sum(c, dtype=np.float64)) for c in ch40])
+        out[f"{name}_rms"] = get_rms(audio, 1280, 320).squeeze(0)
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    y = (rng.standard_normal(50000) * 0.1).astype(np.float32)
+    out["rms_in"] = y
+    out["rms_2048_512"] = get_rms(y, 2048, 512)
+    # extract.py's coarse quantiser on f64 (RMVPE) and f32 (CREPE) tracks (extract.py:225-226)
+    from main.inference.extract import FeatureInput
+    fi = FeatureInput(device="cpu")
+    f64 = rng.uniform(0, 1300, 4001)
+    f64[::7] = 0.0
+    out["coarse_in64"] = f64
+    out["coarse_out64"] = fi.coarse_f0(f64)
+    f32 = f64.astype(np.float32)
+    out["coarse_in32"] = f32
+    out["coarse_out32"] = fi.coarse_f0(f32)
+    np.savez_compressed(os.path.join(OUT, "edges.npz"), **out)
+    print("edges", {k: v.shape for k, v in out.items() if hasattr(v, "shape") and v.ndim})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     setup_harness()
     torch.set_num_threads(8)
     if len(sys.argv) > 1 and sys.argv[1] == "crepe":
         gen_crepe(6.0, seed=81)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "edges":
+        gen_edges(seed=101)
         return
     if len(sys.argv) > 1 and sys.argv[1] == "opts":
         gen_f0_opts(seed=91)
@@ -356,6 +401,7 @@ def main():
     gen_pipeline("pipeline_48k_v2_opts", 48000, "v2", 2.5, seed=53, pitch=2, protect=0.33, f0_autotune=True,
                  f0_autotune_strength=0.8, f0_lines=["0.0,200", "0.4,260.5", "0.9,150", "1.6,0", "2.0,310"],
                  volume_envelope=0.6)
+    gen_edges(seed=101)
 
 
 if __name__ == "__main__":
