@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"],
                     help="split-bf16 conv engine arithmetic: 6 / 3 / 1 bf16 MFMA passes per product")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="clips per GPU per step (BASELINE configs[2]: 64 x 10 s chunks; each a distinct clip)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one hipGraph per clip (rvc_amd.graph.ClipGraph, BASELINE configs[4])")
     ap.add_argument("--index-rate", type=float, default=0.0,
@@ -164,8 +166,10 @@ def main():
         from rvc_amd.crepe import CrepeAMD
         cap = args.f0.split("-", 1)[1]
         vc.crepe[cap] = CrepeAMD(synthetic.crepe_state_dict(1240, cap), cap, dev)
-    audio = synthetic.synthetic_audio(args.seconds, seed=1000 + rank)
-    audio_dev = torch.from_numpy(audio).to(dev)  # input resident in HBM before the timed region
+    # inputs resident in HBM before the timed region: one distinct clip per chunk
+    clips = [torch.from_numpy(synthetic.synthetic_audio(args.seconds, seed=1000 + 97 * rank + c)).to(dev)
+             for c in range(max(1, args.chunks))]
+    audio_dev = clips[0]
     vc.seed = 17 + rank
 
     clip_graph = None
@@ -174,14 +178,16 @@ def main():
         clip_graph = ClipGraph(vc, hub, net_g, 0, audio_dev.numel(), 0, "v2", 0.33, index, args.index_rate, args.f0)
 
     def step():
-        if clip_graph is not None:
-            out = clip_graph(audio_dev)
-        else:
-            out = vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
+        outs = []
+        for clip in clips:
+            if clip_graph is not None:
+                outs.append(clip_graph(clip).clone() if len(clips) > 1 else clip_graph(clip))
+            else:
+                outs.append(vc.pipeline_device(hub, net_g, 0, clip, 0, "v2", 0.33, index, args.index_rate, args.f0))
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
-            gather_waveforms([out], dist, dst=0)
-        return out
+            gather_waveforms(outs, dist, dst=0)
+        return outs[-1]
 
     for _ in range(args.warmup):
         out = step()
@@ -202,7 +208,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     audio_s = out_len / float(args.sr)
-    value = world * args.steps * audio_s / dt
+    value = world * args.steps * len(clips) * audio_s / dt
 
     roof = None
     if rank == 0:
@@ -227,12 +233,13 @@ def main():
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPES[args.precision],
                 "data": "synthetic 16 kHz audio (SURVEY §8d generator), random-init weights of the true shapes",
-                "config": {"workload": f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, one "
+                "config": {"workload": f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, "
+                                       f"{'one' if len(clips) == 1 else f'{len(clips)} x'} "
                                        f"{args.seconds:g} s clip per GPU per step, "
                                        + (f"IVF-Flat index_rate {args.index_rate:g}" if index is not None else "no index")
                                        + ", protect 0.33" + (", hipGraph replay per clip" if args.graph else ""),
                            "model": f"RVC v2 {args.sr // 1000}k (NSF-HiFiGAN) + ContentVec + {args.f0}",
-                           "global_batch": world,
+                           "global_batch": world * len(clips),
                            "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",
                            "output_seconds_per_clip": round(audio_s, 4)},
                 "roofline": roof, "cpu_baseline": cpu}

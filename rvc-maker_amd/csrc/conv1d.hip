@@ -404,8 +404,16 @@ RVC_DEV int x_slot(int pos, int q, int g) {
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
 // input prefetch never wait on each other.  One workgroup barrier per 32-channel chunk hands the
 // next staged X buffer (double-buffered in LDS) to the compute waves.
+// Small tiles (FM x FN <= 4 fragments per wave: <= 32-channel convs) are short blocks whose prologue
+// and epilogue latencies dominate: they are built for 2 co-resident blocks per CU (<= 128 VGPRs,
+// a 1-deep weight ring) so that one block's waits overlap the other's MFMAs.
+// (measured on the 32-channel generator convs: -17..20 % at 6 and 3 passes, +8 % at 1 pass, which
+// stays at one block).
+template <int FM, int FN, int NCW, int NP>
+constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2 : 1; }
+
 template <int FM, int FN, int WM, int WN, int X6_NI, int NP>
-__global__ __launch_bounds__(64 * (WM * WN + 4)) void conv_x6_kernel(ConvParams p) {
+__global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
     constexpr int NCW = WM * WN;  // compute waves; 4 loader waves follow them
     static_assert(NP == 6 || NP == 3 || NP == 1, "6, 3 or 1 passes");
@@ -579,7 +587,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4)) void conv_x6_kernel(ConvParams 
     // depth: as many k-steps as fit a 24-uint4 (96-VGPR) ring, at most 4
     // (8 compute waves = 3 waves per SIMD: an 18-uint4 ring, at most 2 deep)
     constexpr int PD_FIT = (NCW == 8 ? 18 : 24) / (NPL * FM) - 1;
-    constexpr int PD_MAX = NCW == 8 ? 2 : 4;
+    constexpr int PD_MAX = x6_min_blocks<FM, FN, NCW, NP>() == 2 ? 1 : (NCW == 8 ? 2 : 4);
     constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > PD_MAX ? PD_MAX : PD_FIT);
     constexpr int NB = PD + 1;
     uint4 abuf[NB][NPL][FM];
