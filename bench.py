@@ -62,7 +62,7 @@ class ConvProbe:
             e0.record(s)
             out = self.orig(*a, **k)
             e1.record(s)
-            self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE))
+            self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE, self._bytes(a, k, out)))
             return out
         self.ops.conv1d = wrapped
         return self
@@ -70,13 +70,42 @@ class ConvProbe:
     def __exit__(self, *exc):
         self.ops.conv1d = self.orig
 
+    @staticmethod
+    def _bytes(a, k, out):
+        """Algorithmic HBM bytes of one conv launch: input once, f32 weights once, output written,
+        residual / accumulate operands read once."""
+        x, Ci, Co, K = a[0], a[2], a[3], a[4]
+        B = k.get("B") or (1 if x.dim() == 2 else x.shape[0])
+        Lin = k.get("Lin") or x.shape[-1]
+        groups, nphase = k.get("groups", 1), k.get("nphase", 1)
+        n_out = out.numel() if k.get("out") is None else B * Co * (k.get("Lout") or out.shape[-1])
+        reads = B * Ci * Lin + nphase * (Ci // groups) * K * Co
+        reads += n_out * ((k.get("res") is not None) + bool(k.get("accumulate")))
+        return 4.0 * (reads + n_out)
+
     def summary(self, engine=None):
         """(launches, kernel ms, algorithmic FLOPs) over the launches of one engine (None = all)."""
         torch.cuda.synchronize()
         rec = [r for r in self.rec if engine is None or r[3] == engine]
-        ms = [e0.elapsed_time(e1) for e0, e1, _, _ in rec]
-        fl = [f for _, _, f, _ in rec]
+        ms = [e0.elapsed_time(e1) for e0, e1, _, _, _ in rec]
+        fl = [f for _, _, f, _, _ in rec]
         return len(ms), float(sum(ms)), float(sum(fl))
+
+    def algorithmic_bytes(self, engine=None):
+        rec = [r for r in self.rec if engine is None or r[3] == engine]
+        return float(sum(r[4] for r in rec)) / max(len(rec), 1)
+
+
+def pmc_traffic(kernel_family="x6"):
+    """Per-launch HBM bytes of a conv family from the committed PMC summary of this same bench step
+    (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled
+    per MI355X_MICROARCH.md), or None when absent."""
+    path = os.path.join(REPO, "profiles", "r1_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)[kernel_family]["traffic_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
@@ -190,9 +219,8 @@ def main():
         return outs[-1]
 
     for _ in range(args.warmup):
-        out = step()
+        step()
     torch.cuda.synchronize()
-    out_len = out.numel()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -207,7 +235,7 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
-    audio_s = out_len / float(args.sr)
+    audio_s = out.numel() / float(args.sr)  # every clip has the same length
     value = world * args.steps * len(clips) * audio_s / dt
 
     roof = None
@@ -218,7 +246,13 @@ def main():
         n32, ms32, fl32 = probe.summary(engine=0)
         achieved = flops / (ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4),
+                # HBM bytes per x6 launch from PMC (default 48k / rmvpe / fp32 step only), beside the
+                # algorithmic bytes per launch measured here
+                "traffic": (pmc_traffic("x6") if (args.sr, args.f0, args.precision, args.index_rate, args.seconds)
+                            == (48000, "rmvpe", "fp32", 0.0, 30.0) else None),
+                "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r1_pmc_traffic.json)",
+                "algorithmic_bytes_per_launch": round(probe.algorithmic_bytes(engine=1)),
                 "kernel": f"conv_x6_kernel<*> (implicit-GEMM conv, {npass} split-bf16 MFMA pass(es) per product); "
                           f"achieved = algorithmic FLOPs / kernel time; peak = bf16 dense MFMA peak / {npass}",
                 "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4),

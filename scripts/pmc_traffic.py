@@ -1,0 +1,39 @@
+"""Per-launch HBM bytes of the conv kernel families from two rocprofv3 --pmc passes.
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
+FETCH_SIZE counts half the bytes of wide coalesced reads (128-B requests tallied at 64 B), so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  The step runs every kernel once per pass,
+the model build (weight packing) included, so only the conv families are summarised."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+fam = {"conv_x6_kernel": "x6", "conv1d_mfma_kernel": "f32"}
+out = {}
+for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    per = defaultdict(list)
+    for f in glob.glob(f"{root}/{counter}/**/*counter_collection.csv", recursive=True):
+        vals = defaultdict(float)
+        names = {}
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"]
+        for d, v in vals.items():
+            for pat, key in fam.items():
+                if pat in names[d]:
+                    per[key].append(v)
+    for key, v in per.items():
+        out.setdefault(key, {})[counter] = (sum(v) / len(v), len(v))
+res = {}
+for key, d in out.items():
+    fetch_kib, n = d.get("FETCH_SIZE", (0.0, 0))
+    write_kib, _ = d.get("WRITE_SIZE", (0.0, 0))
+    res[key] = {"launches": n, "hbm_read_bytes_per_launch": 2 * fetch_kib * 1024,
+                "hbm_write_bytes_per_launch": write_kib * 1024,
+                "traffic_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024}
+print(json.dumps(res, indent=1))
