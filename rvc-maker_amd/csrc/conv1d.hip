@@ -49,15 +49,16 @@ struct ConvParams {
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
 
-// Output column n -> store position t (or -1 when the column is not stored: beyond ncols / Lout,
-// or a border cell in 2-D mode).  32-bit math: every per-batch extent here is < 2^31.
+// Output column n -> store position t; -1 when the column is not stored (beyond ncols / Lout);
+// -(t + 2) for a border cell of a 2-D image, which is stored as 0 (the bordered [C][H+2][W+2]
+// images then need no zero-fill).  32-bit math: every per-batch extent here is < 2^31.
 __device__ __forceinline__ int out_pos(const ConvParams& p, int64_t n, int phase) {
     if (n >= p.ncols) return -1;
     const int t = (int)n * p.ostride + p.ooffset + phase;
     if (t < 0 || t >= (int)p.Lout) return -1;
     if (p.wrap) {
         const int row = t / p.wrap, col = t - row * p.wrap;
-        if (col == 0 || col == p.wrap - 1 || row == 0 || row == (int)p.Lout / p.wrap - 1) return -1;
+        if (col == 0 || col == p.wrap - 1 || row == 0 || row == (int)p.Lout / p.wrap - 1) return -(t + 2);
     }
     return t;
 }
@@ -75,6 +76,7 @@ __device__ __forceinline__ void epilogue_store(const ConvParams& p, float acc, i
     float* yb = p.y + b * p.y_bstride;
     if (p.accumulate) v += yb[o];
     if (ok) yb[o] = v;
+    else if (t <= -2) yb[m * p.Lout + (-t - 2)] = 0.f;  // 2-D border cell
 }
 
 template <int ACT, int FM, int FN>
@@ -163,8 +165,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int j = 0; j < FN; ++j)
+            for (int j = 0; j < FN; ++j) {
                 if (mok[r] && tcol[j] >= 0) yb[mrow[r] * Lo + tcol[j]] = av[0][j][r];
+                else if (mok[r] && tcol[j] <= -2) yb[mrow[r] * Lo + (-tcol[j] - 2)] = 0.f;  // 2-D border cell
+            }
     }
 }
 
@@ -769,6 +773,7 @@ __global__ __launch_bounds__(512) void conv_x6p_kernel(ConvParams p, int ntiles,
                 if (p.bias2) c += p.bias2[mr];
                 c = act_apply(c, ACT, p.out_slope) * p.out_scale + v[ii];
                 if (m0g + m < Cog && tcol >= 0) yb[mr * Lo + tcol] = c;
+                else if (m0g + m < Cog && tcol <= -2) yb[mr * Lo + (-tcol - 2)] = 0.f;  // 2-D border cell
             }
             }
         };

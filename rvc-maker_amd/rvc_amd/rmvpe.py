@@ -80,7 +80,7 @@ class _ConvT2d:
         """x bordered [Ci][H+2][W+2] -> first Co channels of bordered out_cat [*][2H+2][2W+2]."""
         wrap = W + 2
         L = (H + 2) * wrap
-        ph = torch.zeros(4, self.Co, H + 2, W + 2, device=x.device)
+        ph = torch.empty(4, self.Co, H + 2, W + 2, device=x.device)  # the phase convs write the zero border
         for i, (wp, taps, wx, wx_nmf) in enumerate(self.phases):
             toff = [dy * wrap + dx for dy, dx in taps]
             ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, B=1, out=ph[i],
@@ -154,10 +154,11 @@ class RMVPEAMD:
     def _cbr(self, blk, x, H, W, out):
         dev = x.device
         Co = blk["conv.0"].Co
-        h = torch.zeros(Co, H + 2, W + 2, device=dev)
+        # 2-D convs cover the whole bordered image and write its border as 0: no zero-fill needed
+        h = torch.empty(Co, H + 2, W + 2, device=dev)
         blk["conv.0"](x, H, W, h, out_act=ACT_RELU)
         if "sc" in blk:
-            sc = torch.zeros(Co, H + 2, W + 2, device=dev)
+            sc = torch.empty(Co, H + 2, W + 2, device=dev)
             blk["sc"](x, H, W, sc)
             res = sc
         else:
@@ -178,7 +179,7 @@ class RMVPEAMD:
         for l in range(5):
             cat = torch.zeros(2 * C, H + 2, W + 2, device=dev)
             for b, blk in enumerate(self.enc[l]):
-                out = cat[C:] if b == self.nb - 1 else torch.zeros(C, H + 2, W + 2, device=dev)
+                out = cat[C:] if b == self.nb - 1 else torch.empty(C, H + 2, W + 2, device=dev)
                 x = self._cbr(blk, x, H, W, out)
             cats.append((cat, C, H, W))
             pooled = torch.zeros(C, H // 2 + 2, W // 2 + 2, device=dev)
@@ -187,14 +188,14 @@ class RMVPEAMD:
             C *= 2
         for layer in self.inter:
             for blk in layer:
-                x = self._cbr(blk, x, H, W, torch.zeros(blk["conv.0"].Co, H + 2, W + 2, device=dev))
+                x = self._cbr(blk, x, H, W, torch.empty(blk["conv.0"].Co, H + 2, W + 2, device=dev))
         for i, (convt, blocks) in enumerate(self.dec):
             cat, C, Ho, Wo = cats[-1 - i]
             convt(x, H, W, cat)
             x, H, W = cat, Ho, Wo
             for blk in blocks:
-                x = self._cbr(blk, x, H, W, torch.zeros(blk["conv.0"].Co, H + 2, W + 2, device=dev))
-        img = torch.zeros(3, H + 2, W + 2, device=dev)
+                x = self._cbr(blk, x, H, W, torch.empty(blk["conv.0"].Co, H + 2, W + 2, device=dev))
+        img = torch.empty(3, H + 2, W + 2, device=dev)
         self.cnn(x, H, W, img)
         seq = torch.empty(3 * W, H, device=dev)
         ops.img_to_seq(img, seq, 3, H, W)

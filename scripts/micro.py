@@ -64,7 +64,7 @@ def branches():
     import bench
     from rvc_amd import synthetic
     vc, hub, net_g = bench.build_models("cuda:0")
-    audio = torch.from_numpy(synthetic.synthetic_audio(30.0, seed=1000)).cuda()
+    audio = torch.from_numpy(synthetic.synthetic_audio(float(os.environ.get("SECONDS", 30)), seed=1000)).cuda()
     xp, _ = vc.filt(audio, vc.t_pad)
     print(f"filtfilt+pad:      {timeit(lambda: vc.filt(audio, vc.t_pad), 5):9.1f} us")
     print(f"ContentVec feats:  {timeit(lambda: vc.features_device(hub, xp, 'v2'), 5):9.1f} us")
