@@ -78,7 +78,7 @@ def branches():
     print(f"full pipeline_device: {timeit(lambda: vc.pipeline_device(hub, net_g, 0, audio, 0, 'v2', 0.33), 3):9.1f} us")
 
 
-if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] == "retrieval"):
+if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] in ("retrieval", "synth")):
     if len(sys.argv) > 1 and sys.argv[1] == "branches":
         branches()
         sys.exit(0)
@@ -97,3 +97,26 @@ def retrieval():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "retrieval":
     retrieval()
+
+
+def synth_stages():
+    """The synthesizer's stages at the 30 s shape (T = 3198), each timed alone."""
+    import bench
+    vc, hub, net_g = bench.build_models("cuda:0")
+    T = 3198
+    g = torch.Generator().manual_seed(0)
+    phone = torch.randn(768, T, generator=g).cuda()
+    pitch = torch.randint(1, 255, (T,), generator=g).cuda()
+    f0 = (torch.rand(T, generator=g) * 300 + 80).cuda()
+    gc = net_g.speaker_cond(0)
+    stats = net_g.text_encoder(phone, pitch, T)
+    z_p = stats[:net_g.inter].contiguous()
+    z = net_g.flow_reverse(z_p, gc, T)
+    sn = torch.randn(T * net_g.upp, generator=g).cuda()
+    print(f"text encoder: {timeit(lambda: net_g.text_encoder(phone, pitch, T), 5):9.1f} us")
+    print(f"flow reverse: {timeit(lambda: net_g.flow_reverse(z_p, gc, T), 5):9.1f} us")
+    print(f"generator:    {timeit(lambda: net_g.generator(z, f0, gc[4 * 6 * net_g.hidden:], T, sn), 3):9.1f} us")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "synth":
+    synth_stages()
