@@ -452,7 +452,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         const int ltid = tid - 64 * NCW;
         const int lin = (int)p.Lin;
         const float* xb = p.x + b * p.x_bstride;
-        const int base = (int)(n0 - p.pad);
+        const int base = (int)(n0 * p.stride - p.pad);
         int ipos[X6_NI], ig8[X6_NI];
         unsigned iok = 0;
 #pragma unroll
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     auto compute = [&](int t, const uint4* xbuf, const uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
         const int tof = tap_off(p, t);
         auto bload = [&](int j, uint4 (&bq)[NPL]) __attribute__((always_inline)) {
-            const int pos = pb + 16 * j + tof;
+            const int pos = (pb + 16 * j) * p.stride + tof;
 #pragma unroll
             for (int q = 0; q < NPL; ++q) bq[q] = xbuf[x_slot<NPL>(pos, q, lg)];
         };
@@ -958,7 +958,7 @@ size_t x6p_lds(const ConvParams& p, int BM, int BN, size_t lds) { return lds + (
 
 bool x6p_ok(const ConvParams& p, int BM, int BN, size_t lds) {
     static const int on = getenv("RVC_X6_PERSIST") ? atoi(getenv("RVC_X6_PERSIST")) : 0;
-    return on && p.ksplit == 1 && p.wx_nch >= 2 && x6p_lds(p, BM, BN, lds) <= 160 * 1024;
+    return on && p.ksplit == 1 && p.stride == 1 && p.wx_nch >= 2 && x6p_lds(p, BM, BN, lds) <= 160 * 1024;
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -1025,9 +1025,13 @@ int max_tap_off(const rvc_conv1d_args* a) {
     return m;
 }
 
+// stride 2 only with >= 32 input channels (ContentVec's feature extractor): the staged span doubles,
+// and the operand reads of even positions are 2-way bank conflicted
 bool x6_eligible(const rvc_conv1d_args* a) {
-    return a->wx && a->stride == 1 && a->groups == 1 && a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) &&
-           a->K <= 16 && X6_BN + max_tap_off(a) <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
+    static const int s2 = getenv("RVC_X6_STRIDE2") ? atoi(getenv("RVC_X6_STRIDE2")) : 1;
+    return a->wx && (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
+           a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= 16 &&
+           (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
            (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 || a->wx_passes == 3 ||
                                                 a->wx_passes == 1);
 }
@@ -1063,7 +1067,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         else if (Cog > 16) cfg = {2, 2, 1, 4, true};   // 32 x 128
         else cfg = {1, 2, 1, 4, true};                 // 16 x 128
         const int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
-        p.span = BN + max_tap_off(a);
+        p.span = (BN - 1) * a->stride + max_tap_off(a) + 1;
         p.span_s = p.span;
         p.rows_max = 0;
         p.inv_span = 1.0f / (float)p.span;

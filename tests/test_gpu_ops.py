@@ -58,6 +58,7 @@ CONV_CASES = [
     (256, 4608, 1, 1, 1, 0, 1, 1),
     (64, 64, 11, 1, 5, 25, 1, 4000),     # generator ResBlock shape (dilated)
     (40, 72, 3, 1, 1, 1, 1, 777),        # ragged channel chunks / fragments
+    (40, 72, 3, 2, 1, 1, 1, 777),        # the same, stride 2 (split-bf16 strided staging)
     (768, 3072, 1, 1, 1, 0, 1, 1599),    # ContentVec fc1
     (256, 256, 7, 1, 1, 3, 1, 300),      # ragged N tile
 ]
