@@ -36,10 +36,12 @@ class ClipGraph:
         args = (model, net_g, sid, self.inp, pitch, version, protect, index, index_rate, f0_method)
         kw = dict(volume_envelope=volume_envelope)
         seed0, vc.seed = vc.seed, 0  # the captured seed is 0 + the device seed
+        prio0, vc.side_priority = getattr(vc, "side_priority", None), 0  # normal-priority fork in graphs
         try:
             self._capture(vc, dev, args, kw, warmup)
         finally:
             vc.seed = seed0
+            vc.side_priority = prio0
 
     def _capture(self, vc, dev, args, kw, warmup):
         # warm up on a side stream (allocator pools, per-stream workspaces, lazily created streams)

@@ -165,13 +165,15 @@ class VC:
                                         index_rate, f0_method, f0_opts, volume_envelope, src64)
 
     def _side_stream(self, device):
-        key = str(device)
+        # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a high-priority
+        # stream so that its launches are dispatched ahead of the ContentVec ones: +1.5 % eager (603 ->
+        # 612 xRT).  A captured graph runs 17 % slower with it, so ClipGraph sets side_priority = 0.
+        prio = self.side_priority if getattr(self, "side_priority", None) is not None \
+            else int(os.environ.get("RVC_AMD_SIDE_PRIORITY", "-1"))
+        key = f"{device}/{prio}"
         if getattr(self, "_streams", None) is None:
             self._streams = {}
         if key not in self._streams:
-            # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a
-            # high-priority stream so that its launches are dispatched ahead of the ContentVec ones
-            prio = int(os.environ.get("RVC_AMD_SIDE_PRIORITY", "-1"))  # +1.5 % measured (603 -> 612 xRT)
             self._streams[key] = torch.cuda.Stream(device=device, priority=prio)
         return self._streams[key]
 
