@@ -4,6 +4,9 @@ output waveforms gathered to rank 0 over RCCL).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--no-cpu-baseline]
 
+--gpus N without WORLD_SIZE in the environment starts N ranks itself (torch.distributed.run as a
+child process, one rank per GPU); under an external launcher WORLD_SIZE must equal N.
+
 Prints ONE JSON line on rank 0 (contract in the task statement): metric/value = output
 audio-seconds per wall-second for the whole job, plus "roofline" for the dominant kernel
 family (the f32-MFMA implicit-GEMM conv engine, measured live with HIP events on its stream)
@@ -128,8 +131,19 @@ def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
     return IVFFlatDevice(IVFFlatIndex(768, cent, codes, ids, nprobe=1, ntotal=n), dev)
 
 
-def cpu_baseline(seconds=8.0):
-    """The torch-CPU oracle (a restatement of the reference's CPU path) on a bounded clip."""
+def cpu_calibration():
+    """Oracle-vs-reference CPU timing ratio measured in the build container (scripts/cpu_calibrate.py:
+    the reference's own VC.pipeline and oracle.pipeline on the same clip, same threads), or None."""
+    try:
+        with open(os.path.join(REPO, "profiles", "cpu_calibration.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(seconds=30.0):
+    """The torch-CPU oracle (a restatement of the reference's CPU path) on the config's own clip length
+    (30 s, ~15-20 s of CPU work on the GPU box's host threads)."""
     from oracle import contentvec as ocv
     from oracle import pipeline as opl
     from oracle import rmvpe as orm
@@ -146,9 +160,15 @@ def cpu_baseline(seconds=8.0):
     t0 = time.perf_counter()
     out = opl.pipeline(Wc, Ws, Wr, mb, ck["config"], 0, audio, 0.0, "v2", 0.33, noise)
     dt = time.perf_counter() - t0
+    cal = cpu_calibration()
     return {"value": round(len(out) / 48000 / dt, 4), "unit": "audio-s/s", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"{seconds:g} s clip, 48k v2, RMVPE, fp32, torch-CPU oracle (oracle/), "
-            f"wall {dt:.2f} s"}
+            "host_cpus": os.cpu_count(), "kind": "port",
+            "sample": f"{seconds:g} s clip, 48k v2, RMVPE, fp32, torch-CPU oracle (oracle/), wall {dt:.2f} s, "
+                      f"{torch.get_num_threads()} torch threads",
+            "oracle_over_reference_time": cal.get("oracle_over_reference_time") if cal else None,
+            "calibration": (f"oracle / reference wall time on one {cal['seconds']:g} s clip in the build container "
+                            f"({cal['threads']} threads): {cal['oracle_s']:.2f} s / {cal['reference_s']:.2f} s "
+                            "(profiles/cpu_calibration.json)") if cal else None}
 
 
 def main():
@@ -171,16 +191,30 @@ def main():
                     help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launcher: start one rank per GPU under torch.distributed.run as a CHILD process and exit with
+        # its code.  This process never touches the GPU (no exec after GPU init).
+        return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
+    ndev = torch.cuda.device_count()
+    dev_idx = local % max(ndev, 1)
+    # ranks sharing a device (a rehearsal on a box with fewer GPUs than ranks) cannot use RCCL between
+    # them: the gather then runs over gloo through host memory, and the line says so
+    shared = world > ndev
+    backend = "gloo" if shared else "nccl"
     dist = None
+    torch.cuda.set_device(dev_idx)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = f"cuda:{local}"
-    torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_idx}"))
+        else:
+            dist.init_process_group("gloo")
+    dev = f"cuda:{dev_idx}"
 
     from rvc_amd import ops, synthetic
     from rvc_amd.shard import gather_waveforms
@@ -215,8 +249,12 @@ def main():
                 outs.append(vc.pipeline_device(hub, net_g, 0, clip, 0, "v2", 0.33, index, args.index_rate, args.f0))
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
-            gather_waveforms(outs, dist, dst=0)
+            got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0)
+            if got is not None:
+                gathered[0] += sum(len(g) for g in got)
         return outs[-1]
+
+    gathered = [0]
 
     for _ in range(args.warmup):
         step()
@@ -231,12 +269,14 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    vc.check_errors()  # device-side failure flags (BiGRU hand-off timeout) -- raises instead of a number
     if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     audio_s = out.numel() / float(args.sr)  # every clip has the same length
-    value = world * args.steps * len(clips) * audio_s / dt
+    value = world * args.steps * len(clips) * audio_s / dt  # whole job: every rank's clips over the max time
+    gathered_per_step = gathered[0] / max(args.warmup + args.steps, 1) if dist is not None else len(clips)
 
     roof = None
     if rank == 0:
@@ -264,6 +304,10 @@ def main():
         cpu = cpu_baseline()
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "audio-s/s", "n_gpus": world,
+                "value_per_gpu": round(value / world, 3), "world_size": world, "devices_used": min(world, ndev),
+                "collective": ("none" if world == 1 else
+                               "RCCL gather over xGMI" if backend == "nccl" else "gloo (ranks share a GPU)"),
+                "waveforms_gathered_per_step": gathered_per_step,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPES[args.precision],
                 "data": "synthetic 16 kHz audio (SURVEY §8d generator), random-init weights of the true shapes",
@@ -282,5 +326,21 @@ def main():
         dist.destroy_process_group()
 
 
+def launch_ranks(n):
+    """``bench.py --gpus N`` without a launcher: run ``torch.distributed.run --nproc-per-node N`` over this
+    same script as a child process (rendezvous on 127.0.0.1) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -176,7 +176,10 @@ int rvc_sine_source(const float* f0, const float* noise, float* har, float* work
  * img_to_seq: [C][H][W] image -> [C*W][H] sequence                       RMVPE.py:144
  * bigru: recurrence of nn.GRU(384, 256, bidirectional); gi = W_ih x + b_ih
  *        [2][768][T], whh [2][768][256], bhh [2][768], y [512][T];
- *        gran_ws: 8 KiB scratch (zeroed by the call), err: device int set on timeout
+ *        gran_ws: 8 KiB scratch (zeroed by the call), err: device int set to 1 when a step's hand-off wait
+ *        exceeds the spin limit (the kernel then drains and y is incomplete); sticky until the caller clears it
+ * bigru_set_spin_limit: polls per hand-off wait before the timeout fires (default 2^22); 0 only queries.
+ *        Returns the previous limit.  For tests that force the timeout path.
  * rmvpe_decode: salience [360][ld] -> f0 (f64, optional), coarse (int64), pitchf (f32)
  *        RMVPE.py:217-252 + convert.py:311-323, f64, numpy's reduction order
  */
@@ -190,6 +193,7 @@ int rvc_interleave4(const float* phases, float* out, int64_t C, int64_t H, int64
 int rvc_img_to_seq(const float* img, float* x, int64_t C, int64_t H, int64_t W, rvc_stream_t stream);
 int rvc_bigru(const float* gi, const float* whh, const float* bhh, float* y, void* gran_ws, int* err, int64_t T,
               rvc_stream_t stream);
+unsigned rvc_bigru_set_spin_limit(unsigned limit);
 /* Optional steps of VC.get_f0 between the raw f0 and the mel quantiser (convert.py:311-318), in
  * the reference's order: autotune (Autotune.autotune_f0, convert.py:168-179: f += (nearest of the 54
  * reference notes - f) * strength, first note on ties, unvoiced frames included) on the raw f0, then

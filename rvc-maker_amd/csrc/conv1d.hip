@@ -1025,12 +1025,16 @@ int max_tap_off(const rvc_conv1d_args* a) {
     return m;
 }
 
+// Taps per conv on the split-bf16 engine: CREPE's k=64 layers (CREPE.py:11-69) are the widest; the staged
+// span (BN - 1) * stride + (K - 1) * dil + 1 is checked against the loader's item budget below.
+constexpr int X6_K_MAX = 64;
+
 // stride 2 only with >= 32 input channels (ContentVec's feature extractor): the staged span doubles,
 // and the operand reads of even positions are 2-way bank conflicted
 bool x6_eligible(const rvc_conv1d_args* a) {
     static const int s2 = getenv("RVC_X6_STRIDE2") ? atoi(getenv("RVC_X6_STRIDE2")) : 1;
     return a->wx && (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
-           a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= 16 &&
+           a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= X6_K_MAX &&
            (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
            (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 || a->wx_passes == 3 ||
                                                 a->wx_passes == 1);

@@ -155,7 +155,8 @@ constexpr int GRU_H = 256;
 constexpr int GRU_WG_PER_DIR = 16;
 
 __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float* whh, const float* bhh, float* y,
-                                                    unsigned long long* gran, int* err, int64_t T) {
+                                                    unsigned long long* gran, int* err, int64_t T,
+                                                    unsigned spin_limit) {
     const int d = blockIdx.x / GRU_WG_PER_DIR;
     const int j = blockIdx.x % GRU_WG_PER_DIR;
     const int tid = threadIdx.x;
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float
             for (;;) {
                 v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((uint32_t)(v >> 32) == (uint32_t)t) break;
-                if (++spins > (1u << 22)) {
+                if (++spins > spin_limit) {
                     atomicExch(err, 1);
                     abort_flag = 1;
                     break;
@@ -234,13 +235,21 @@ __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float
     }
 }
 
+static unsigned g_bigru_spin_limit = 1u << 22;
+
+extern "C" unsigned rvc_bigru_set_spin_limit(unsigned limit) {
+    const unsigned prev = g_bigru_spin_limit;
+    if (limit) g_bigru_spin_limit = limit;
+    return prev;
+}
+
 extern "C" int rvc_bigru(const float* gi, const float* whh, const float* bhh, float* y, void* gran_ws, int* err,
                          int64_t T, rvc_stream_t stream) {
     RVC_CHECK_ARG(gi && whh && bhh && y && gran_ws && err && T > 0 && T < (1ll << 31), "bigru: bad args");
     hipStream_t s = (hipStream_t)stream;
     RVC_HIP(hipMemsetAsync(gran_ws, 0, 2 * 2 * GRU_H * sizeof(unsigned long long), s));
     hipLaunchKernelGGL(bigru_kernel, dim3(2 * GRU_WG_PER_DIR), dim3(256), 0, s, gi, whh, bhh, y,
-                       (unsigned long long*)gran_ws, err, T);
+                       (unsigned long long*)gran_ws, err, T, g_bigru_spin_limit);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }

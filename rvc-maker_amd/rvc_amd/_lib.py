@@ -77,6 +77,7 @@ SIGNATURES = {
     "rvc_interleave4": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_img_to_seq": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_bigru": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    "rvc_bigru_set_spin_limit": [ctypes.c_uint],
     "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, POINTER(F0Post), c_void_p, c_void_p,
                          c_void_p, c_void_p],
     "rvc_filtfilt_work_bytes": [c_int64],
@@ -104,7 +105,7 @@ SIGNATURES = {
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
-             "rvc_rms_frames_len": c_int64}
+             "rvc_rms_frames_len": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}
 
 _lib = None
 

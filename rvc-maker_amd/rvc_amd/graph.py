@@ -45,15 +45,18 @@ class ClipGraph:
 
     def _capture(self, vc, dev, args, kw, warmup):
         # warm up on a side stream (allocator pools, per-stream workspaces, lazily created streams)
+        # The graph owns its scratch: every split-K / split-KV / decode workspace its kernels point at
+        # lives in self.workspaces for the graph's lifetime, shared with no eager pass or other graph.
+        self.workspaces = {}
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s), ops.device_seed(self.seed):
+        with torch.cuda.stream(s), ops.device_seed(self.seed), ops.private_workspaces(self.workspaces):
             for _ in range(max(1, warmup)):
                 vc.pipeline_device(*args, **kw)
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph), ops.device_seed(self.seed):
+        with torch.cuda.graph(self.graph), ops.device_seed(self.seed), ops.private_workspaces(self.workspaces):
             self.out = vc.pipeline_device(*args, **kw)
 
     def __call__(self, audio: torch.Tensor, seed: int | None = None) -> torch.Tensor:

@@ -117,8 +117,9 @@ class Conv:
         self.Ci = self.Cig * groups
         self.w = pack_km(w.float(), groups).to(device)
         self.b = b.float().to(device) if b is not None else None
-        # the split-bf16 engine takes ungrouped convs with <= 16 taps (see x6_eligible in conv1d.hip)
-        self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co) if groups == 1 and self.K <= 16 \
+        # the split-bf16 engine takes ungrouped convs with <= 64 taps (X6_K_MAX / x6_eligible in conv1d.hip;
+        # CREPE's k=64 layers are the widest)
+        self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co) if groups == 1 and self.K <= 64 \
             else (None, 0)
 
     def __call__(self, x, Lout=None, stride=1, pad=0, dil=1, **kw):
@@ -152,16 +153,40 @@ class ConvT:
 LAST_CONV_FLOPS = 0.0
 LAST_CONV_ENGINE = 0  # 0 = f32 MFMA engine, 1 = split-bf16 (x6) engine
 _WS = {}
+_WS_PRIVATE = None  # a workspace store owned by a captured graph (private_workspaces)
+
+
+class private_workspaces:
+    """``with ops.private_workspaces(store):`` -- split-K / split-KV / decode scratch comes from ``store``
+    (a dict the caller keeps) instead of the shared per-stream pool.  A captured graph bakes the raw
+    workspace pointers into its kernel nodes, so it must own them: buffers in a private store are never
+    freed while the store lives (a grown buffer's predecessor is retired into the store, not released),
+    and no eager launch or other graph draws from it (graph.ClipGraph)."""
+
+    def __init__(self, store: dict):
+        self.store = store
+
+    def __enter__(self):
+        global _WS_PRIVATE
+        self.prev, _WS_PRIVATE = _WS_PRIVATE, self.store
+        return self.store
+
+    def __exit__(self, *a):
+        global _WS_PRIVATE
+        _WS_PRIVATE = self.prev
 
 
 def _workspace(device, nbytes, kind="conv"):
     """Split-K / split-KV scratch per (device, stream), grown on demand: reuse is stream-ordered, and
     work running concurrently on another stream (VC's side stream) gets its own buffer."""
     key = f"{device}/{kind}/{torch.cuda.current_stream(device).stream_id}"
-    buf = _WS.get(key)
+    pool = _WS if _WS_PRIVATE is None else _WS_PRIVATE
+    buf = pool.get(key)
     if buf is None or buf.numel() * 4 < nbytes:
+        if buf is not None and _WS_PRIVATE is not None:
+            pool.setdefault("_retired", []).append(buf)  # a captured node may still point at it
         buf = torch.empty((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
-        _WS[key] = buf
+        pool[key] = buf
     return buf
 
 

@@ -217,9 +217,17 @@ class VC:
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=xp.device)
         ops.peak_normalize(out, self._ws)
-        if os.environ.get("RVC_AMD_CHECK") and f0_method == "rmvpe":
-            self._rmvpe().check_error()
+        if os.environ.get("RVC_AMD_CHECK"):  # debugging: synchronous check inside the device pass
+            self.check_errors()
         return out
+
+    def check_errors(self):
+        """Raise if a device-side failure was flagged since the last check: the RMVPE BiGRU's hand-off
+        timeout (f0 would be garbage).  ``pipeline()`` calls it after its output copy (one 4-byte read
+        behind a sync that happens anyway); HBM-resident callers (``pipeline_device``, ClipGraph replays,
+        the bench) call it once after their own synchronisation."""
+        if self.rmvpe is not None:
+            self.rmvpe.check_error()
 
     def _index(self, path):
         """Device-resident IVF-Flat index per path (the reference re-reads it every call)."""
@@ -252,7 +260,9 @@ class VC:
                                    inp_f0, volume_envelope)
         if pbar is not None:
             pbar.update(2)
-        return out.cpu().numpy()
+        out = out.cpu().numpy()
+        self.check_errors()
+        return out
 
 
 def read_f0_file(f0_file):

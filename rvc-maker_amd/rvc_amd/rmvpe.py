@@ -219,8 +219,10 @@ class RMVPEAMD:
         return coarse, pitchf, f0
 
     def check_error(self):
+        """Raise if a BiGRU launch since the last check timed out (its f0 is then garbage); clears the flag."""
         if int(self.err.item()) != 0:
-            raise RuntimeError("rvc_amd: bigru recurrence timed out (granule hand-off stalled)")
+            self.err.zero_()
+            raise RuntimeError("rvc_amd: bigru recurrence timed out (granule hand-off stalled); f0 invalid")
 
     # ------------------------------------------------------------------ reference API
     def infer_from_audio(self, audio: np.ndarray, thred: float = 0.03) -> np.ndarray:

@@ -80,3 +80,26 @@ def test_coarse_matches_oracle_quantiser(model):
         want_c, want_f = opl.coarse_f0(base.copy(), shift, opl.Consts(48000))
         np.testing.assert_allclose(f0.cpu().numpy(), want_f, rtol=1e-12)
         assert np.array_equal(coarse.cpu().numpy(), want_c)
+
+
+def test_bigru_timeout_is_reported_and_cleared(model):
+    """A BiGRU hand-off that exceeds its spin limit flags err; check_error raises once, then the flag
+    is clear and a normal run passes (the kernel drains instead of hanging)."""
+    from rvc_amd import _lib
+    m, g = model
+    lib = _lib.load()
+    audio = torch.from_numpy(g["audio"]).float().to(DEV)
+    prev = lib.rvc_bigru_set_spin_limit(1)
+    try:
+        m.f0_device(audio)
+        torch.cuda.synchronize()
+    finally:
+        lib.rvc_bigru_set_spin_limit(prev)
+    assert lib.rvc_bigru_set_spin_limit(0) == prev
+    with pytest.raises(RuntimeError, match="bigru"):
+        m.check_error()
+    m.check_error()  # cleared
+    coarse, pitchf, f0 = m.f0_device(audio, want_f0=True)
+    torch.cuda.synchronize()
+    m.check_error()
+    assert np.max(np.abs(f0.cpu().numpy() - g["f0"])) < 1e-2
