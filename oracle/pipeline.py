@@ -154,11 +154,13 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
 
 
 def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None, index=None,
-             index_rate=0.0, crepe=None, autotune_strength=None, inp_f0=None, volume_envelope=1.0):
+             index_rate=0.0, crepe=None, autotune_strength=None, inp_f0=None, volume_envelope=1.0, f0_track=None):
     """VC.pipeline (convert.py:388-458): f0 = rmvpe (or crepe), optional index, autotune, f0 file
     (``inp_f0`` [n][2] f32) and volume envelope.
 
-    noise(seg_index, name, shape) -> torch tensor for "z" [1, 192, T] and "sine" [1, T*upp, 1]."""
+    noise(seg_index, name, shape) -> torch tensor for "z" [1, 192, T] and "sine" [1, T*upp, 1].
+    ``f0_track`` (f64 [1 + len(padded) // 160]) replaces the f0 estimator's raw output: the parity tests
+    use it to check everything after the f0 decision against the device's own decisions."""
     tgt_sr = cfg[-1]
     upp = int(np.prod(cfg[12]))
     c = Consts(tgt_sr)
@@ -171,7 +173,11 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
     sid_t = torch.tensor(sid).unsqueeze(0).long()
     big_npy = index.reconstruct_n(0, index.ntotal) if index is not None and index_rate != 0 else None
     p_len = audio_pad.shape[0] // c.window
-    if crepe is not None:  # f0_method "crepe-<capacity>": (state dict, capacity, dither cents [T])
+    if f0_track is not None:
+        f0 = np.array(f0_track, dtype=np.float64, copy=True)
+        if f0.shape != (1 + audio_pad.shape[0] // c.window,):
+            raise ValueError(f"f0_track has {f0.shape}, expected {(1 + audio_pad.shape[0] // c.window,)}")
+    elif crepe is not None:  # f0_method "crepe-<capacity>": (state dict, capacity, dither cents [T])
         from . import crepe as oc
         csd, capacity, dither = crepe
         f0 = oc.get_f0_crepe(csd, audio_pad, dither, capacity)

@@ -132,6 +132,11 @@ class RMVPEAMD:
         self.fc = ops.Conv(sd["fc.1.weight"].float().unsqueeze(-1), sd["fc.1.bias"].float(), device=dev)
         self.gran = torch.zeros(1024, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # The f0 is a per-frame decision (argmax over 360 bins, voicing threshold): RMVPE's convs run at the
+        # f32-accurate 6-pass arithmetic whatever ops.precision says (None = follow it).  At 3 passes the
+        # salience moves by 1.5e-2 and at 1 pass by 0.24 on the synthetic weights, which flips decisions;
+        # RMVPE is 5 % of a 48k clip's FLOPs and runs beside ContentVec (tests/test_gpu_configs.py).
+        self.precision = "fp32"
 
     @classmethod
     def from_file(cls, path, device="cuda"):
@@ -208,9 +213,10 @@ class RMVPEAMD:
                   post=None):
         """audio [N] f32 device -> (coarse int64 [F], pitchf f32 [F], f0 f64 [F] | None) on the device;
         ``post`` (ops.F0Post) adds get_f0's autotune / f0-file steps."""
-        mel = self.mel_spectrogram(audio)
-        F = mel.shape[-1]
-        sal, Tp = self.salience(mel)
+        with ops.precision(self.precision or ops.get_precision()):
+            mel = self.mel_spectrogram(audio)
+            F = mel.shape[-1]
+            sal, Tp = self.salience(mel)
         dev = audio.device
         coarse = torch.empty(F, dtype=torch.int64, device=dev)
         pitchf = torch.empty(F, device=dev)

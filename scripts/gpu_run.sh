@@ -18,7 +18,7 @@ step() {
 }
 for s in "$@"; do
   case $s in
-    pytest) step pytest 1100 python -u -m pytest tests -x -q -m gpu -rf --timeout 900 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    pytest) step pytest 1100 python -u -m pytest tests -q -m gpu --maxfail=${MAXFAIL:-1} -rf --timeout 900 --timeout-method thread ${PYTEST_ARGS:-} ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 2 ;;
     bench2) step bench2 600 python bench.py --gpus 2 --steps 5 --warmup 2 ;;
     graph) step graph 600 python bench.py --steps 10 --warmup 2 --graph --no-cpu-baseline ;;

@@ -8,9 +8,18 @@
 Waveform tolerances ("Precision budget"):
   * fp32 and bf16x3 (3-pass split-bf16 convs): RMS error <= 1e-4 against the fp32 oracle -- the
     north-star bar of BASELINE.json.  bf16x3 is the arithmetic the bf16 configs are benchmarked at.
-  * bf16 (1-pass, bf16 operands, f32 accumulation): measured here and bounded by BF16_REL_RMS relative
-    to the output's RMS, with the f0 track checked separately (it decides voicing): these weights are
-    random-init, and the generator's response to a 2^-8 operand perturbation is what the bound states.
+  * bf16 (1-pass, bf16 operands, f32 accumulation): bounded by BF16_REL_RMS relative to the output's RMS.
+  * RMVPE runs f32-accurate under every precision setting (RMVPEAMD.precision): at 3 passes its salience
+    moved by 1.5e-2 and at 1 pass by 0.24 on these weights, flipping f0 decisions.
+  * RMVPE's f0 is a discrete decision per frame (argmax over 360 bins, voicing threshold 0.03).  On these
+    random-init weights some frames are near-ties far below the f32 noise floor of the network itself (the
+    reference's own f32 and f64 salience differ by 4.3e-4, its f32 at 8 vs 3 threads by 2.0e-4:
+    scripts/f0_diag.py), and one flipped frame shifts the SineGen phase of the rest of the
+    clip.  So the f0 stage is checked as a decision: salience within SAL_TOL of the oracle's, every frame's
+    argmax / voicing equal to the oracle's except where the oracle's own margin (top-1 minus top-2, or
+    |max - 0.03|) is below SAL_TOL; and the waveform is checked against the oracle run on the device's f0
+    track (everything after the decision is continuous) at the bars above.  With no ill-conditioned flip
+    the fully independent oracle run must meet the same bar.
 """
 import json
 import os
@@ -23,7 +32,8 @@ from rvc_amd import ops, synthetic
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-BF16_REL_RMS = 0.35  # 1-pass bf16: measured 1.0e-1 .. 2.0e-1 relative on these weights
+BF16_REL_RMS = 0.03  # 1-pass bf16 on the device f0 decisions: measured 7.5e-3 (cfg3), 1.5e-2 (cfg5)
+SAL_TOL = 2e-3  # RMVPE salience bound (fp32, bf16x3): 5x the reference's own f32-vs-f64 spread
 RESULTS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
                        "config_parity.json")
 
@@ -92,6 +102,36 @@ class SeededNoise:
         return self.cache[(seg, kind)]
 
 
+def _f0_decisions(vc, m, audio, sal_tol, max_flip_frac=1e-3):
+    """RMVPE on the device vs the oracle for one clip: (device raw f0 track, report).  Asserts the salience
+    bound and that every argmax / voicing disagreement sits on a frame the oracle itself cannot resolve."""
+    from oracle import pipeline as opl
+    from oracle import rmvpe as orm
+    xp, _ = vc.filt(torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)).to(DEV), vc.t_pad)
+    with ops.precision(vc.rmvpe.precision or ops.get_precision()):  # as f0_device runs it
+        mel = vc.rmvpe.mel_spectrogram(xp)
+        F = mel.shape[-1]
+        sal, _ = vc.rmvpe.salience(mel)
+    sd = sal[:, :F].t().cpu().numpy().astype(np.float64)
+    _, _, f0 = vc.rmvpe.f0_device(xp, 0.03, 0.0, want_f0=True)
+    f0 = f0.cpu().numpy()
+    vc.check_errors()
+    ap = np.pad(opl.signal.filtfilt(opl.BH, opl.AH, audio), (vc.t_pad, vc.t_pad), mode="reflect")
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        so = orm.mel2hidden(m["Wr"], orm.mel_spectrogram(torch.from_numpy(ap).float().unsqueeze(0),
+                                                         m["mel_basis"])).squeeze(0).numpy().astype(np.float64)
+    srt = np.sort(so, axis=1)
+    margin = np.minimum(srt[:, -1] - srt[:, -2], np.abs(srt[:, -1] - 0.03))
+    flips = np.flatnonzero((sd.argmax(1) != so.argmax(1)) | ((sd.max(1) > 0.03) != (so.max(1) > 0.03)))
+    rep = dict(frames=int(F), salience_max_abs=float(np.abs(sd - so).max()), flips=flips.tolist(),
+               flip_margins=margin[flips].tolist())
+    assert rep["salience_max_abs"] < sal_tol, rep
+    assert all(margin[flips] < sal_tol), rep
+    assert len(flips) <= max(2, int(F * max_flip_frac)), rep
+    return f0, rep
+
+
 @pytest.mark.timeout(600)
 def test_cfg2_headline_30s_48k_fp32_vs_oracle():
     """configs[1] at the benchmarked shape: one 30 s clip (T_f 1599, T 3198, 1 439 040 output samples)."""
@@ -102,11 +142,17 @@ def test_cfg2_headline_30s_48k_fp32_vs_oracle():
     vc.noise_fn = lambda s, k, sh: noise(s, k, sh).to(DEV)
     out = vc.pipeline(hub, net_g, 0, audio.copy(), 0, "rmvpe", "", 0.0, 1, 3, 1, "v2", 0.33, 64, False, 1, ".pth",
                       ".pt")
-    ref = _oracle(_oracle_models(sr, "v2", seed), audio, noise)
+    m = _oracle_models(sr, "v2", seed)
+    f0, rep = _f0_decisions(vc, m, audio, SAL_TOL)
+    ref = _oracle(m, audio, noise, f0_track=f0)
     assert out.shape == ref.shape == (1439040,)
     err = _rms(out, ref)
-    _record("cfg2_30s_fp32", rms=err, ref_rms=_rms(ref, 0 * ref))
+    ind = _oracle(m, audio, noise)
+    err_ind = _rms(out, ind)
+    _record("cfg2_30s_fp32", rms_on_device_f0=err, rms_independent=err_ind, ref_rms=_rms(ref, 0 * ref), **rep)
     assert err < 1e-4, err
+    if not rep["flips"]:
+        assert err_ind < 1e-4, err_ind
 
 
 @pytest.fixture(scope="module")
@@ -124,37 +170,44 @@ def cfg3():
     chunks = [synthetic.synthetic_audio(10.0, seed=1100 + c) for c in range(3)]
     noises = [SeededNoise(50 + c) for c in range(3)]
     m = _oracle_models(sr, "v2", seed)
-    refs = [_oracle(m, a, n, index=idx, index_rate=0.75) for a, n in zip(chunks, noises)]
-    return vc, hub, net_g, dindex, chunks, noises, refs
+    return vc, hub, net_g, dindex, idx, chunks, noises, m
 
 
-def _run_cfg3(cfg3, precision):
-    vc, hub, net_g, dindex, chunks, noises, refs = cfg3
-    errs, scales = [], []
+def _run_cfg3(cfg3, precision, sal_tol, max_flip_frac=1e-3):
+    vc, hub, net_g, dindex, idx, chunks, noises, m = cfg3
+    errs, scales, reps, ind = [], [], [], []
     with ops.precision(precision):
-        for a, n, ref in zip(chunks, noises, refs):
+        for a, n in zip(chunks, noises):
             vc.noise_fn = lambda s, k, sh, n=n: n(s, k, sh).to(DEV)
             out = vc.pipeline_device(hub, net_g, 0, a, 0, "v2", 0.33, dindex, 0.75).cpu().numpy()
+            f0, rep = _f0_decisions(vc, m, a, sal_tol, max_flip_frac)
+            ref = _oracle(m, a, n, index=idx, index_rate=0.75, f0_track=f0)
             assert out.shape == ref.shape
             errs.append(_rms(out, ref))
             scales.append(_rms(ref, 0 * ref))
+            reps.append(rep)
+            if not rep["flips"]:  # the independent oracle run, where no decision is ill-conditioned
+                ind.append(_rms(out, _oracle(m, a, n, index=idx, index_rate=0.75)))
     vc.check_errors()
-    return errs, scales
+    return errs, scales, reps, ind
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 def test_cfg3_index_chunks_vs_oracle(cfg3, precision):
-    errs, scales = _run_cfg3(cfg3, precision)
-    _record(f"cfg3_index075_10s_{precision}", rms=errs, ref_rms=scales)
+    errs, scales, reps, ind = _run_cfg3(cfg3, precision, SAL_TOL)
+    _record(f"cfg3_index075_10s_{precision}", rms_on_device_f0=errs, rms_independent=ind, ref_rms=scales,
+            f0=[dict(r, flips=len(r["flips"])) for r in reps])
     assert max(errs) < 1e-4, errs
+    assert all(e < 1e-4 for e in ind), ind
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_cfg3_index_chunks_bf16_bounded(cfg3):
-    errs, scales = _run_cfg3(cfg3, "bf16")
+    errs, scales, reps, ind = _run_cfg3(cfg3, "bf16", SAL_TOL)
     rel = [e / s for e, s in zip(errs, scales)]
-    _record("cfg3_index075_10s_bf16", rms=errs, ref_rms=scales, rel=rel)
+    _record("cfg3_index075_10s_bf16", rms_on_device_f0=errs, ref_rms=scales, rel=rel,
+            f0=[dict(r, flips=len(r["flips"])) for r in reps])
     assert max(rel) < BF16_REL_RMS, rel
 
 
