@@ -235,6 +235,29 @@ int rvc_rms_frames(const double* y64, const float* y32, int64_t n, int64_t hop, 
 int rvc_rms_mix(float* y, int64_t n, const float* r1, int64_t n1, const float* r2, int64_t n2, double rate,
                 rvc_stream_t stream);
 
+/* ------------------------------------------------------------------ spectral-gate denoise
+ * Replaces main/tools/noisereduce.py:reduce_noise(y, sr, prop_decrease=clean_strength) as
+ * VoiceConverter.convert_audio calls it for clean_audio (convert.py:514-516): the non-stationary TG
+ * (noisereduce.py:124-180) over SpectralGate.get_traces' chunks (:96-122: chunk_size samples, each
+ * zero-padded by `padding` both sides and gated independently), in f64 like the reference.
+ *   window: device f64 [n_fft] = torch.hann_window(n_fft) (float32, promoted);
+ *   filt:   device f64 [filt_h][filt_w] (TG._generate_mask_smoothing_filter, :144-154) or NULL
+ *           with filt_h = filt_w = 0;
+ *   n_movemean = int(time_constant_s / hop * sr) (:193); n_thresh = thresh_n_mult_nonstationary;
+ *   temp_coeff = 1 / sigmoid_slope_nonstationary.
+ * y f32 [n] -> out f32 [n]; work: rvc_denoise_work_bytes(n, a) bytes of device scratch. */
+typedef struct rvc_denoise_args {
+    int64_t chunk_size, padding;
+    int n_fft, hop, n_movemean, filt_h, filt_w, _pad0;
+    double prop_decrease, n_thresh, temp_coeff;
+    const double* window;
+    const double* filt;
+} rvc_denoise_args;
+
+int64_t rvc_denoise_work_bytes(int64_t n, const rvc_denoise_args* a);
+int rvc_denoise(const float* y, int64_t n, const rvc_denoise_args* a, void* work, int64_t work_bytes, float* out,
+                rvc_stream_t stream);
+
 /* ------------------------------------------------------------------ FAISS IVF-Flat retrieval
  * Replaces faiss IndexIVFFlat(L2).search(feats, k=8) + the blend of convert.py:349-359.
  * Queries (query i, dim c) live at q[c*cs + i*qs] (channels-first [d][nq]: cs = nq, qs = 1).

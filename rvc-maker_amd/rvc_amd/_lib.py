@@ -45,6 +45,14 @@ class F0Post(ctypes.Structure):
                 ("rep_off", c_int64), ("rep_len", c_int64)]
 
 
+class DenoiseArgs(ctypes.Structure):
+    """rvc_denoise_args: the non-stationary spectral gate (main/tools/noisereduce.py:124-199)."""
+    _fields_ = [("chunk_size", c_int64), ("padding", c_int64), ("n_fft", c_int), ("hop", c_int),
+                ("n_movemean", c_int), ("filt_h", c_int), ("filt_w", c_int), ("_pad0", c_int),
+                ("prop_decrease", c_double), ("n_thresh", c_double), ("temp_coeff", c_double),
+                ("window", c_void_p), ("filt", c_void_p)]
+
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "rvc_last_error": [],
@@ -101,11 +109,13 @@ SIGNATURES = {
     "rvc_rms_frames_len": [c_int64, c_int64],
     "rvc_rms_frames": [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
     "rvc_rms_mix": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p],
+    "rvc_denoise_work_bytes": [c_int64, POINTER(DenoiseArgs)],
+    "rvc_denoise": [c_void_p, c_int64, POINTER(DenoiseArgs), c_void_p, c_int64, c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
-             "rvc_rms_frames_len": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}
+             "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}
 
 _lib = None
 

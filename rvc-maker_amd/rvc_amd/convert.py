@@ -6,7 +6,8 @@ nearest standard rate, write.
 Batch mode shards the files over ranks (one process per GPU, longest file first to the least-loaded
 rank -- shard.shard_utterances); each rank writes its own outputs, so no waveform crosses ranks.
 
-Not on the device path (raise): formant shifting, ``clean_audio`` (noisereduce), non-WAV export.
+``clean_audio`` runs the spectral gate of main/tools/noisereduce.py on the device (rvc_amd.denoise).
+Not on the device path (raise): formant shifting, non-WAV export.
 Resampling (input != 16 kHz, or a model rate that is not a standard rate) is parity-unpinned
 (audio_io module note).
 """
@@ -48,8 +49,8 @@ class VoiceConverterAMD:
         """convert.py:479-523.  Like the reference, errors are logged and the call returns None;
         on success the written waveform is returned."""
         try:
-            if formant_shifting or clean_audio:
-                raise NotImplementedError("formant shifting / clean_audio are not on the MI355X path")
+            if formant_shifting:
+                raise NotImplementedError("formant shifting is not on the MI355X path")
             if export_format != "wav":
                 raise NotImplementedError("only WAV export (no soundfile / ffmpeg in this build)")
             audio = audio_io.load_audio(audio_input_path, self.sample_rate)
@@ -75,6 +76,9 @@ class VoiceConverterAMD:
                 else converted[0][2]
             if target_sr >= self.sample_rate and self.tgt_sr != target_sr:
                 out = audio_io.resample(out, self.tgt_sr, target_sr)
+            if clean_audio:  # convert.py:514-516
+                from .denoise import reduce_noise
+                out = reduce_noise(y=out, sr=target_sr, prop_decrease=clean_strength, device=self.vc.device)
             audio_io.write_wav(audio_output_path, out, target_sr)
             return out
         except Exception as e:  # noqa: BLE001 -- the reference logs and returns (convert.py:520-523)

@@ -372,12 +372,38 @@ def gen_edges(seed):
     print("edges", {k: v.shape for k, v in out.items() if hasattr(v, "shape") and v.ndim})
 
 
+def gen_denoise(seed):
+    """noisereduce.reduce_noise (main/tools/noisereduce.py:199) as convert_audio calls it (convert.py:514-516):
+    a single-chunk 48 kHz case at clean_strength 0.7, and a multi-chunk 44.1 kHz case (odd/even moving-mean
+    window, chunk seams) with a small chunk_size / padding."""
+    from main.tools.noisereduce import reduce_noise
+    rng = np.random.default_rng(seed)
+    out = {}
+    cases = [("a", 48000, 2.0, 0.7, {}), ("b", 44100, 1.6, 1.0, dict(chunk_size=30000, padding=5000)),
+             ("c", 40000, 1.2, 0.45, dict(chunk_size=20000, padding=3000))]
+    for name, sr, secs, prop, kw in cases:
+        n = int(sr * secs)
+        t = np.arange(n) / sr
+        y = (0.3 * np.sin(2 * np.pi * 220 * t) * (0.5 + 0.5 * np.sin(2 * np.pi * 0.7 * t)) +
+             0.02 * rng.standard_normal(n)).astype(np.float32)
+        y[n // 3: n // 3 + sr // 10] *= 0.01  # a near-silent gap
+        o = reduce_noise(y=y, sr=sr, prop_decrease=prop, device="cpu", **kw)
+        out[f"{name}_y"], out[f"{name}_out"] = y, np.asarray(o, dtype=np.float32)
+        out[f"{name}_meta"] = np.array([sr, prop, kw.get("chunk_size", 600000), kw.get("padding", 30000)],
+                                       dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "denoise.npz"), **out)
+    print("denoise", {k: v.shape for k, v in out.items()})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     setup_harness()
     torch.set_num_threads(8)
     if len(sys.argv) > 1 and sys.argv[1] == "crepe":
         gen_crepe(6.0, seed=81)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "denoise":
+        gen_denoise(seed=111)
         return
     if len(sys.argv) > 1 and sys.argv[1] == "edges":
         gen_edges(seed=101)
@@ -402,6 +428,7 @@ def main():
                  f0_autotune_strength=0.8, f0_lines=["0.0,200", "0.4,260.5", "0.9,150", "1.6,0", "2.0,310"],
                  volume_envelope=0.6)
     gen_edges(seed=101)
+    gen_denoise(seed=111)
 
 
 if __name__ == "__main__":

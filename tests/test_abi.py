@@ -44,7 +44,9 @@ def test_errors_are_reported_without_gpu():
 def test_struct_layouts_match_c_compiler(tmp_path):
     import subprocess
     fields = {"rvc_conv1d_args": [f[0] for f in _lib.Conv1dArgs._fields_],
-              "rvc_attn_args": [f[0] for f in _lib.AttnArgs._fields_]}
+              "rvc_attn_args": [f[0] for f in _lib.AttnArgs._fields_],
+              "rvc_f0_post": [f[0] for f in _lib.F0Post._fields_],
+              "rvc_denoise_args": [f[0] for f in _lib.DenoiseArgs._fields_]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rvc_amd.h"', "int main(void){"]
     for st, fs in fields.items():
         lines.append(f'printf("%zu\\n", sizeof({st}));')
@@ -57,7 +59,7 @@ def test_struct_layouts_match_c_compiler(tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = []
-    for cls in (_lib.Conv1dArgs, _lib.AttnArgs):
+    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs):
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f[0]).offset for f in cls._fields_]
     assert got == want
