@@ -49,13 +49,15 @@ def build_models(dev, sr=48000, version="v2", seed=1234):
 
 
 class ConvProbe:
-    """Wraps ops.conv1d during one instrumented step: HIP events around every launch on the launch
-    stream + the launch's algorithmic FLOPs (reference conv FLOPs) + its engine."""
+    """Wraps ops.conv1d and ops.resblock_pair during one instrumented step: HIP events around every
+    launch on the launch stream + the launch's algorithmic FLOPs (reference conv FLOPs) +
+    its engine (a fused ResBlock pair counts as split-bf16 work: its two convs' FLOPs)."""
 
     def __init__(self):
         from rvc_amd import ops
         self.ops = ops
         self.orig = ops.conv1d
+        self.orig_rb = ops.resblock_pair
         self.rec = []
 
     def __enter__(self):
@@ -67,11 +69,24 @@ class ConvProbe:
             e1.record(s)
             self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE, self._bytes(a, k, out)))
             return out
+        def wrapped_rb(x, y, c1, c2, dil, slope, accumulate=False):
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            out = self.orig_rb(x, y, c1, c2, dil, slope, accumulate=accumulate)
+            e1.record(s)
+            C, L = x.shape
+            flops = 2 * 2.0 * C * C * c1.K * L
+            nbytes = 4.0 * (C * L * (2 + bool(accumulate)) + 2 * C * C * c1.K)  # x, y (+ y read), both weights
+            self.rec.append((e0, e1, flops, 1, nbytes))
+            return out
         self.ops.conv1d = wrapped
+        self.ops.resblock_pair = wrapped_rb
         return self
 
     def __exit__(self, *exc):
         self.ops.conv1d = self.orig
+        self.ops.resblock_pair = self.orig_rb
 
     @staticmethod
     def _bytes(a, k, out):
@@ -293,7 +308,8 @@ def main():
                             == (48000, "rmvpe", "fp32", 0.0, 30.0) else None),
                 "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r1_pmc_traffic.json)",
                 "algorithmic_bytes_per_launch": round(probe.algorithmic_bytes(engine=1)),
-                "kernel": f"conv_x6_kernel<*> (implicit-GEMM conv, {npass} split-bf16 MFMA pass(es) per product); "
+                "kernel": f"conv_x6_kernel<*> + resblock_x6_kernel<*> (implicit-GEMM convs / fused ResBlock conv "
+                          f"pairs, {npass} split-bf16 MFMA pass(es) per product); "
                           f"achieved = algorithmic FLOPs / kernel time; peak = bf16 dense MFMA peak / {npass}",
                 "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "algorithmic_gflop_per_step": round(flops / 1e9, 1), "kernel_ms_per_step": round(ms, 3),

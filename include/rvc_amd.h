@@ -102,6 +102,30 @@ int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co);
 int rvc_conv1d_pack_x6(const float* w_km, int64_t nphase, int64_t Ci, int K, int64_t Co, void* out, int* nmf_out,
                        rvc_stream_t stream);
 
+/* ------------------------------------------------------------------ fused ResBlock pair
+ * One (convs1[i], convs2[i]) pair of the NSF-HiFiGAN ResBlock (residuals.py:22-44) in one launch:
+ *   y = x + c2(lrelu(c1(lrelu(x), dilation dil, pad dil*(K-1)/2)), pad (K-1)/2)   [+ y when accumulate]
+ * on the split-bf16 engine, with c1's output kept in LDS (never written to HBM).  C = 32 or 64 channels
+ * (the generator's last two stages, synthesizers.py:157-159), odd K <= 15, (K-1)*dil <= 64.
+ * w1x / w2x: the convs' rvc_conv1d_pack_x6 images (nphase 1, Ci = Co = C; nmf1 / nmf2 their wx_nmf);
+ * b1 / b2: f32 biases [C]; passes 6 / 3 / 1 as rvc_conv1d_args.wx_passes; slope: the lrelu slope (0.1).
+ * x and y must not alias.  Bit-identical to the two rvc_conv1d launches it replaces. */
+typedef struct rvc_resblock_args {
+    const float* x;
+    float* y;
+    const void* w1x;
+    const float* b1;
+    const void* w2x;
+    const float* b2;
+    int64_t C, L;
+    int K, dil, nmf1, nmf2, passes, accumulate;
+    float slope;
+    int _pad0;
+} rvc_resblock_args;
+
+int64_t rvc_resblock_lds_bytes(int64_t C, int K, int dil, int passes);
+int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream);
+
 /* ------------------------------------------------------------------ attention
  * Flash-style multi-head attention on f32 MFMA over channels-first Q/K/V
  * ([B][H][D][T], channel stride ldc, t contiguous); O written in the same layout.

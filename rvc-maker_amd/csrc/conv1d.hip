@@ -14,6 +14,7 @@
 // conditioning), activation, residual add, accumulate, polyphase/strided stores (ConvTranspose)
 // and border masking (2-D mode).
 #include "rvc_common.h"
+#include "x6_common.h"
 #include <stdlib.h>
 #include <type_traits>
 
@@ -368,41 +369,11 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
 // flow, TextEncoder and the ContentVec linears).
 //
 // k-steps are (32-channel chunk, tap): a chunk's input rows are staged ONCE into LDS (split into
-// h/m/l planes, channel-contiguous [pos][32 ch] rows, 16-B groups XOR-swizzled by (pos>>2)&3 so
+// h/m/l planes, channel-contiguous [pos][32 ch] rows, 16-B groups XOR-swizzled (x6_common.h x_slot) so
 // both the staging writes and the operand reads are conflict-free) and reused by all K taps.
 // B operands are one ds_read_b128 per plane per fragment; A operands (weights) come pre-split
 // and pre-arranged per lane from global memory (L2-resident), prefetched one k-step ahead.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-RVC_DEV floatx4 mfma_bf16(const uint4& a, const uint4& b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                   0, 0, 0);
-}
-
-// v -> (h, m, l) bf16 bit patterns, v == h + m + (exactly representable rest), l = bf16(rest)
-RVC_DEV void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
-    const __bf16 bh = (__bf16)v;
-    const float r1 = v - (float)bh;  // exact (Sterbenz)
-    const __bf16 bm = (__bf16)r1;
-    const float r2 = r1 - (float)bm;  // exact
-    const __bf16 bl = (__bf16)r2;
-    h = __builtin_bit_cast(uint16_t, bh);
-    m = __builtin_bit_cast(uint16_t, bm);
-    l = __builtin_bit_cast(uint16_t, bl);
-}
-
 constexpr int X6_NI_MAX = 6;  // staged (position, 8-channel group) items per loader thread: 4 * span <= 256 NI
-
-// NP = MFMA passes per product: 6 (f32-accurate, above), 3 (hH + hM + mH: 16-bit-mantissa products,
-// ~2^-16 relative) or 1 (hH: plain bf16 operands, f32 accumulation).  Only the NPL = 3 / 2 / 1 planes a
-// pass set reads are staged and loaded.  LDS rows are [pos][NPL planes][4 x 16 B]; the 16-B group is
-// XOR-swizzled so that 16 consecutive positions of one (plane, group) hit 16 distinct bank quads:
-// NPL 3 and 1 by (pos>>2)&3 within the plane, NPL 2 by (pos>>1)&7 across the two planes.
-template <int NPL>
-RVC_DEV int x_slot(int pos, int q, int g) {
-    if constexpr (NPL == 2) return pos * 8 + ((4 * q + g) ^ ((pos >> 1) & 7));
-    else return pos * (4 * NPL) + 4 * q + (g ^ ((pos >> 2) & 3));
-}
 
 // Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep

@@ -1,0 +1,399 @@
+// Fused HiFiGAN ResBlock pair on the split-bf16 matrix cores:
+//     y (+)= x + c2(lrelu(c1(lrelu(x), dilation d)))        (residuals.py:22-44, one (convs1[i], convs2[i]) pair)
+// for the generator's small-channel stages (C = 32, 64: 13 of its 28.6 ms in the unfused engine, where a
+// 32-channel conv is a GEMM only 96-352 deep and every launch pays its staging, epilogue and HBM latency).
+//
+// One persistent workgroup per CU walks time tiles of N outputs.  The tile's input span (N + halo) is
+// staged ONCE into LDS as lrelu'd split-bf16 planes, c1's output T (N + K - 1 columns, lrelu'd, zero
+// outside [0, L) = c2's zero padding) stays in LDS as split planes, and c2 reads it from there: the
+// intermediate never touches HBM and each pair reads x once and writes y once.
+//
+// Roles (12 waves): 8 compute waves (row groups x column groups, 2 x 2 fragments each, so every B
+// fragment read from LDS feeds 2 x NP MFMAs; weights streamed per lane from the x6 fragment image through
+// an L2 prefetch ring that runs on across phases and tiles), 4 loader waves that fetch the NEXT tile's raw
+// x into registers while the current tile's c1 runs, write it (lrelu'd, split) into X while c2 runs, and
+// its raw residual rows into R at the next tile start.
+// Two barriers per tile:  S0 (X of tile k staged) -> c1 -> T written -> S1 -> c2 -> S0 of tile k+1.
+//
+// Summation order, pass order and epilogue order are those of conv_x6_kernel (chunk-major (chunk, tap)
+// k-steps; hH hM mH hL mM lH; acc + bias, + residual, + accumulate), so the result is bit-identical to the
+// two-launch form.
+#include "rvc_common.h"
+#include "x6_common.h"
+
+namespace {
+
+struct RbParams {
+    const float* x;    // [C][L] chain state in (also the residual)
+    float* y;          // [C][L] out (accumulated into when accumulate)
+    const uint4* w1x;  // c1 split-bf16 image [K][C/32][nmf][3][64]
+    const uint4* w2x;  // c2 image
+    const float* b1;
+    const float* b2;
+    int L, K, dil, nmf1, nmf2, accumulate;
+    float slope;
+};
+
+#ifndef RB_YREG
+#define RB_YREG 1  // accumulate operands loaded at S1 into registers (else in the epilogue)
+#endif
+#ifndef RB_FM_
+#define RB_FM_ 1
+#define RB_FN_ 4
+#endif
+constexpr int RB_FM = RB_FM_;  // row fragments per compute wave
+constexpr int RB_FN = RB_FN_;  // column fragments per compute wave
+constexpr int RB_MAXSPAN = 64; // (K - 1) * dil bound (generator: 10 * 5 = 50)
+
+template <int C>
+struct RbGeom {
+    static constexpr int RF = C / 16;            // row fragments
+    static constexpr int NCH = C / 32;           // 32-channel chunks
+    static constexpr int RG = RF / RB_FM;        // row groups
+    static constexpr int CG = 8 / RG;            // column groups (RG x CG = 8 compute waves)
+    static constexpr int NF1 = CG * RB_FN;       // c1 column fragments: T holds 16 NF1 positions
+    static constexpr int NF2 = NF1 - 1;          // c2 column fragments
+    static constexpr int N = 16 * NF2;           // outputs per tile (240 at C = 32, 112 at C = 64)
+    static constexpr int TW = 16 * NF1;
+    static constexpr int RSTR = N + 4;           // residual row stride (floats): 4 rows apart = distinct banks
+    static constexpr int NI = (NCH * (TW + RB_MAXSPAN) * 4 + 255) / 256;  // loader items per thread
+};
+
+template <int C, int NP>
+size_t rb_lds_bytes(int K, int dil) {
+    using G = RbGeom<C>;
+    constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
+    const int Wx = G::TW + (K - 1) * dil;
+    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (size_t)C * G::RSTR * 4;
+}
+
+template <int C, int NP>
+__global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
+    using G = RbGeom<C>;
+    constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
+    constexpr int N = G::N, TW = G::TW, NCH = G::NCH, NF1 = G::NF1, NF2 = G::NF2, RSTR = G::RSTR;
+    constexpr int FM = RB_FM, FN = RB_FN;
+    extern __shared__ uint4 lds[];
+    const int K = p.K, d = p.dil, L = p.L;
+    const int hk = (K - 1) / 2;
+    const int H = d * hk + hk;  // input halo per side
+    const int Wx = TW + (K - 1) * d;
+    uint4* Xs = lds;                          // [NCH][Wx][NPL][4]
+    uint4* Ts = Xs + NCH * Wx * NPL * 4;      // [NCH][TW][NPL][4]
+    float* Rs = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [C][RSTR]
+    const int ntiles = (L + N - 1) / N;
+    const int my_n = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+
+    if (wave >= 8) {
+        // ---------------- loader waves.  Tile k+1's raw x is loaded into registers after S0(k) (while c1
+        // runs), written to X as lrelu'd split planes after S1(k) (X free: c1 done), and its residual rows
+        // to R after S0(k+1) (R free: tile k's c2 epilogue done), just before the registers are reloaded.
+        const int ltid = threadIdx.x - 512;
+        const int nitems = NCH * Wx * 4;
+        float xr[G::NI][8];
+        auto item = [&](int it, int& ch, int& g8, int& pos) __attribute__((always_inline)) {
+            int idx = ltid + 256 * it;
+            idx = idx < nitems ? idx : nitems - 1;
+            ch = idx / (Wx * 4);
+            const int rem = idx - ch * Wx * 4;
+            g8 = rem / Wx;
+            pos = rem - g8 * Wx;
+        };
+        auto xload = [&](int tile) __attribute__((always_inline)) {
+            const int base = tile * N - H;
+#pragma unroll
+            for (int it = 0; it < G::NI; ++it) {
+                int ch, g8, pos;
+                item(it, ch, g8, pos);
+                int q = base + pos;
+                q = q < 0 ? 0 : (q >= L ? L - 1 : q);
+                const float* src = p.x + (int64_t)(ch * 32 + g8 * 8) * L + q;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xr[it][e] = src[(int64_t)e * L];
+            }
+        };
+        auto xstore = [&](int tile) __attribute__((always_inline)) {
+            const int base = tile * N - H;
+#pragma unroll
+            for (int it = 0; it < G::NI; ++it) {
+                if (ltid + 256 * it < nitems) {
+                    int ch, g8, pos;
+                    item(it, ch, g8, pos);
+                    const int q = base + pos;
+                    const bool ok = q >= 0 && q < L;
+                    uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) {
+                        uint32_t h2[2], m2[2], l2[2];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const float v = ok ? xr[it][2 * e2 + u] : 0.f;
+                            split3(v >= 0.f ? v : v * p.slope, h2[u], m2[u], l2[u]);
+                        }
+                        hw[e2] = h2[0] | (h2[1] << 16);
+                        mw[e2] = m2[0] | (m2[1] << 16);
+                        lw[e2] = l2[0] | (l2[1] << 16);
+                    }
+                    uint4* dst = Xs + ch * Wx * NPL * 4;
+                    dst[x_slot<NPL>(pos, 0, g8)] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                    if constexpr (NPL >= 2) dst[x_slot<NPL>(pos, 1, g8)] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+                    if constexpr (NPL >= 3) dst[x_slot<NPL>(pos, 2, g8)] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                }
+            }
+        };
+        auto rstore = [&]() __attribute__((always_inline)) {  // raw residual rows of the staged tile
+#pragma unroll
+            for (int it = 0; it < G::NI; ++it) {
+                if (ltid + 256 * it < nitems) {
+                    int ch, g8, pos;
+                    item(it, ch, g8, pos);
+                    const int rc = pos - H;
+                    if (rc >= 0 && rc < N) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) Rs[(ch * 32 + g8 * 8 + e) * RSTR + rc] = xr[it][e];
+                    }
+                }
+            }
+        };
+        if (my_n > 0) {
+            xload(blockIdx.x);
+            xstore(blockIdx.x);
+        }
+        for (int k = 0; k < my_n; ++k) {
+            __syncthreads();  // S0(k): X(k) staged; R free
+            rstore();         // R(k) from the registers still holding tile k
+            const bool more = k + 1 < my_n;
+            if (more) xload(blockIdx.x + (k + 1) * gridDim.x);
+            __syncthreads();  // S1(k): c1 of tile k done -> X free
+            if (more) xstore(blockIdx.x + (k + 1) * gridDim.x);
+        }
+        return;
+    }
+
+    // ---------------- compute waves: row group rg (FM row fragments), column group cg (FN fragments)
+    const int rg = wave % G::RG, cg = wave / G::RG;
+    const int ln = lane & 15, lg = lane >> 4;
+    const int SPH = NCH * K;      // k-steps per phase
+    const int SPT = 2 * SPH;      // per tile
+    const int S_end = my_n * SPT;
+    auto aload = [&](int S, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
+        const int sl = S % SPT;
+        const bool two = sl >= SPH;
+        const int s2 = two ? sl - SPH : sl;
+        const int ch = s2 / K, t = s2 - ch * K;
+        const uint4* img = two ? p.w2x : p.w1x;
+        const int nmf = two ? p.nmf2 : p.nmf1;
+        const int frag = __builtin_amdgcn_readfirstlane((t * NCH + ch) * nmf + rg * FM);
+        const uint4* src = img + (int64_t)frag * 3 * 64;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) a[q][i] = src[(i * 3 + q) * 64 + lane];
+    };
+    floatx4 acc[FM][FN];
+    // one k-step: B fragments from the LDS image (X for c1 with tap stride d, T for c2), NP passes
+    auto compute = [&](const uint4* buf, int tof, int nfrag, const uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
+        auto bload = [&](int j, uint4 (&bq)[NPL]) __attribute__((always_inline)) {
+            const int pos = (cg * FN + j) * 16 + ln + tof;
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) bq[q] = buf[x_slot<NPL>(pos, q, lg)];
+        };
+        uint4 bb[2][NPL];
+        bload(0, bb[0]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            if (j + 1 < FN && cg * FN + j + 1 < nfrag) bload(j + 1, bb[(j + 1) & 1]);
+            if (cg * FN + j < nfrag) {
+                const uint4 (&bq)[NPL] = bb[j & 1];
+                constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
+                constexpr int PB[6] = {0, 1, 0, 2, 1, 0};
+#pragma unroll
+                for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+            }
+        }
+    };
+    // weight prefetch depth (k-steps): as many as fit the register budget of 3 waves per SIMD
+#ifndef RB_PD3
+#define RB_PD3 3
+#endif
+    constexpr int PD = NPL == 3 ? RB_PD3 : (NPL == 2 ? 2 : 4);
+    constexpr int NB = PD + 1;            // ring slots: k-step S uses slot S % NB (compile-time below)
+    uint4 abuf[NB][NPL][FM];
+#pragma unroll
+    for (int i = 0; i < PD; ++i)
+        if (i < S_end) aload(i, abuf[i]);
+    float yold[FM][FN][4];
+    int n0 = 0;
+    // One loop over the block's k-steps (tile k: c1 steps [k SPT, k SPT + SPH), c2 steps after), unrolled by
+    // the ring size so every ring slot index is a compile-time constant; the tile / phase seams (barriers,
+    // epilogues) are uniform branches inside it and the weight prefetch runs on across them.
+    for (int S0 = 0; S0 < S_end; S0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int S = S0 + u;
+            if (S < S_end) {
+                const int k = S / SPT, ss = S - k * SPT;
+                if (ss == 0) {  // ---- tile start: X of tile k staged
+                    n0 = ((int)blockIdx.x + k * (int)gridDim.x) * N;
+                    __syncthreads();  // S0(k)
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                }
+                const bool two = ss >= SPH;
+                const int s2 = two ? ss - SPH : ss;
+                const int ch = s2 / K, t = s2 - ch * K;
+                if (S + PD < S_end) aload(S + PD, abuf[(u + PD) % NB]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (!two) compute(Xs + ch * (Wx * NPL * 4), t * d, NF1, abuf[u]);  // c1 over X, tap stride d
+                else compute(Ts + ch * (TW * NPL * 4), t, NF2, abuf[u]);        // c2 over T
+                if (ss == SPH - 1) {
+                    // ---- c1 epilogue: + bias, lrelu, zero outside [0, L) (c2's padding) -> T (split planes)
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) {
+                        const int mf = rg * FM + i;
+                        const int m0 = mf * 16 + 4 * lg;  // this lane's 4 rows
+                        const int tch = (mf * 16) / 32, tg8 = (mf & 1) * 2 + (lg >> 1), thalf = lg & 1;
+                        uint4* tb = Ts + tch * TW * NPL * 4;
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) {
+                            const int it = (cg * FN + j) * 16 + ln;  // T position
+                            const int q = n0 - hk + it;
+                            const bool ok = q >= 0 && q < L;
+                            uint32_t hw[2], mw[2], lw[2];
+#pragma unroll
+                            for (int r2 = 0; r2 < 2; ++r2) {
+                                uint32_t h2[2], m2[2], l2[2];
+#pragma unroll
+                                for (int e = 0; e < 2; ++e) {
+                                    float v = acc[i][j][2 * r2 + e] + p.b1[m0 + 2 * r2 + e];
+                                    v = v >= 0.f ? v : v * p.slope;
+                                    split3(ok ? v : 0.f, h2[e], m2[e], l2[e]);
+                                }
+                                hw[r2] = h2[0] | (h2[1] << 16);
+                                mw[r2] = m2[0] | (m2[1] << 16);
+                                lw[r2] = l2[0] | (l2[1] << 16);
+                            }
+                            reinterpret_cast<uint2*>(tb + x_slot<NPL>(it, 0, tg8))[thalf] = make_uint2(hw[0], hw[1]);
+                            if constexpr (NPL >= 2)
+                                reinterpret_cast<uint2*>(tb + x_slot<NPL>(it, 1, tg8))[thalf] = make_uint2(mw[0], mw[1]);
+                            if constexpr (NPL >= 3)
+                                reinterpret_cast<uint2*>(tb + x_slot<NPL>(it, 2, tg8))[thalf] = make_uint2(lw[0], lw[1]);
+                            acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                        }
+                    }
+                    __syncthreads();  // S1(k): T written; X free for the loaders
+                    if (RB_YREG && p.accumulate) {
+#pragma unroll
+                        for (int i = 0; i < FM; ++i)
+#pragma unroll
+                            for (int j = 0; j < FN; ++j) {
+                                int q = n0 + (cg * FN + j) * 16 + ln;
+                                q = q < L ? q : L - 1;
+#pragma unroll
+                                for (int r = 0; r < 4; ++r)
+                                    yold[i][j][r] = p.y[(int64_t)((rg * FM + i) * 16 + 4 * lg + r) * L + q];
+                            }
+                    }
+                }
+                if (ss == SPT - 1) {
+                    // ---- c2 epilogue: + bias, + residual (from R) (+ accumulate) -> y
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) {
+                        const int m0 = (rg * FM + i) * 16 + 4 * lg;
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) {
+                            const int col = (cg * FN + j) * 16 + ln;
+                            const int q = n0 + col;
+                            if (cg * FN + j < NF2 && col < N && q < L) {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    float v = acc[i][j][r] + p.b2[m0 + r];
+                                    v = v + Rs[(m0 + r) * RSTR + col];
+                                    if (p.accumulate) v += RB_YREG ? yold[i][j][r] : p.y[(int64_t)(m0 + r) * L + q];
+                                    p.y[(int64_t)(m0 + r) * L + q] = v;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int C, int NP>
+int launch_rb(const RbParams& p, hipStream_t s) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (ncu <= 0) ncu = 256;
+    }
+    const size_t lds = rb_lds_bytes<C, NP>(p.K, p.dil);
+    static bool attr = false;
+    if (!attr) {
+        RVC_HIP(hipFuncSetAttribute((const void*)resblock_x6_kernel<C, NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024));
+        attr = true;
+    }
+    const int ntiles = (p.L + RbGeom<C>::N - 1) / RbGeom<C>::N;
+    hipLaunchKernelGGL((resblock_x6_kernel<C, NP>), dim3(ntiles < ncu ? ntiles : ncu), dim3(768), lds, s, p);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+int rb_check(const rvc_resblock_args* a) {
+    RVC_CHECK_ARG(a && a->x && a->y && a->w1x && a->w2x && a->b1 && a->b2, "resblock: null pointer");
+    RVC_CHECK_ARG(a->C == 32 || a->C == 64, "resblock: C must be 32 or 64 (got %lld)", (long long)a->C);
+    RVC_CHECK_ARG(a->L > 0 && a->C * a->L < (1ll << 31), "resblock: bad length");
+    RVC_CHECK_ARG(a->K >= 1 && a->K % 2 == 1 && a->K <= 15 && a->dil >= 1 && (a->K - 1) * a->dil <= RB_MAXSPAN,
+                  "resblock: odd K <= 15 with (K-1)*dil <= %d expected", RB_MAXSPAN);
+    RVC_CHECK_ARG(a->passes == 6 || a->passes == 3 || a->passes == 1, "resblock: passes must be 6, 3 or 1");
+    RVC_CHECK_ARG(a->nmf1 * 16 >= a->C && a->nmf2 * 16 >= a->C, "resblock: weight image too small");
+    RVC_CHECK_ARG(a->x != a->y, "resblock: x and y must not alias (tiles read x halos other tiles overwrite)");
+    return RVC_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t rvc_resblock_lds_bytes(int64_t C, int K, int dil, int passes) {
+    if (C == 32) return passes == 6 ? rb_lds_bytes<32, 6>(K, dil) : passes == 3 ? rb_lds_bytes<32, 3>(K, dil)
+                                                                                : rb_lds_bytes<32, 1>(K, dil);
+    if (C == 64) return passes == 6 ? rb_lds_bytes<64, 6>(K, dil) : passes == 3 ? rb_lds_bytes<64, 3>(K, dil)
+                                                                                : rb_lds_bytes<64, 1>(K, dil);
+    return -1;
+}
+
+extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream) {
+    const int rc = rb_check(a);
+    if (rc != RVC_OK) return rc;
+    RbParams p;
+    p.x = a->x;
+    p.y = a->y;
+    p.w1x = (const uint4*)a->w1x;
+    p.w2x = (const uint4*)a->w2x;
+    p.b1 = a->b1;
+    p.b2 = a->b2;
+    p.L = (int)a->L;
+    p.K = a->K;
+    p.dil = a->dil;
+    p.nmf1 = a->nmf1;
+    p.nmf2 = a->nmf2;
+    p.accumulate = a->accumulate;
+    p.slope = a->slope;
+    hipStream_t s = (hipStream_t)stream;
+    if (a->C == 32) {
+        if (a->passes == 6) return launch_rb<32, 6>(p, s);
+        if (a->passes == 3) return launch_rb<32, 3>(p, s);
+        return launch_rb<32, 1>(p, s);
+    }
+    if (a->passes == 6) return launch_rb<64, 6>(p, s);
+    if (a->passes == 3) return launch_rb<64, 3>(p, s);
+    return launch_rb<64, 1>(p, s);
+}

@@ -45,6 +45,13 @@ class F0Post(ctypes.Structure):
                 ("rep_off", c_int64), ("rep_len", c_int64)]
 
 
+class ResblockArgs(ctypes.Structure):
+    """rvc_resblock_args: one fused (convs1[i], convs2[i]) ResBlock pair (residuals.py:22-44)."""
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("w1x", c_void_p), ("b1", c_void_p), ("w2x", c_void_p),
+                ("b2", c_void_p), ("C", c_int64), ("L", c_int64), ("K", c_int), ("dil", c_int), ("nmf1", c_int),
+                ("nmf2", c_int), ("passes", c_int), ("accumulate", c_int), ("slope", c_float), ("_pad0", c_int)]
+
+
 class DenoiseArgs(ctypes.Structure):
     """rvc_denoise_args: the non-stationary spectral gate (main/tools/noisereduce.py:124-199)."""
     _fields_ = [("chunk_size", c_int64), ("padding", c_int64), ("n_fft", c_int), ("hop", c_int),
@@ -110,12 +117,14 @@ SIGNATURES = {
     "rvc_rms_frames": [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
     "rvc_rms_mix": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_double, c_void_p],
     "rvc_denoise_work_bytes": [c_int64, POINTER(DenoiseArgs)],
+    "rvc_resblock_lds_bytes": [c_int64, c_int, c_int, c_int],
+    "rvc_resblock_pair": [POINTER(ResblockArgs), c_void_p],
     "rvc_denoise": [c_void_p, c_int64, POINTER(DenoiseArgs), c_void_p, c_int64, c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
-             "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}
+             "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}
 
 _lib = None
 

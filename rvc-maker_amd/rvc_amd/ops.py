@@ -261,6 +261,31 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
     return out
 
 
+# Fused ResBlock pairs for the 32/64-channel generator stages (RVC_AMD_FUSED_RB=0: two conv launches each)
+FUSED_RB = os.environ.get("RVC_AMD_FUSED_RB", "1") != "0"
+
+
+def resblock_fusable(c1: "Conv", c2: "Conv", dil: int) -> bool:
+    return (FUSED_RB and c1.wx is not None and c2.wx is not None and c1.Ci == c1.Co == c2.Ci == c2.Co
+            and c1.Co in (32, 64) and c1.K == c2.K and c1.K % 2 == 1 and c1.K <= 15 and (c1.K - 1) * dil <= 64)
+
+
+def resblock_pair(x, y, c1: "Conv", c2: "Conv", dil: int, slope: float, accumulate: bool = False):
+    """y (+)= x + c2(lrelu(c1(lrelu(x), dil)))  (residuals.py:22-44, one pair) in one launch; x [C][L]."""
+    C, L = x.shape
+    if y.shape != x.shape or not x.is_contiguous() or not y.is_contiguous() or x.data_ptr() == y.data_ptr():
+        raise ValueError("resblock_pair: x, y must be distinct contiguous [C][L] buffers")
+    a = _lib.ResblockArgs()
+    a.x, a.y = _p(x), _p(y)
+    a.w1x, a.w2x = ctypes.c_void_p(c1.wx.data_ptr()), ctypes.c_void_p(c2.wx.data_ptr())
+    a.b1, a.b2 = _p(c1.b), _p(c2.b)
+    a.C, a.L, a.K, a.dil = C, L, c1.K, dil
+    a.nmf1, a.nmf2 = c1.wx_nmf, c2.wx_nmf
+    a.passes, a.accumulate, a.slope = PASSES[_PRECISION], int(bool(accumulate)), slope
+    check(_lib.load().rvc_resblock_pair(ctypes.byref(a), _stream()), "resblock_pair")
+    return y
+
+
 def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_bs=0, k_bs=0, v_bs=0, o_bs=0,
               rk=None, ev=None, ml=None, W=0):
     a = _lib.AttnArgs()

@@ -10,7 +10,8 @@ All compute runs in librvc_amd.so kernels on the current torch stream:
   flow^-1      4 x [flip, pre, WaveNet(3 x conv k5 + gate + res/skip convs), post (fused x1 - m)]
   NSF-HiFiGAN  sine_source, conv_pre(+cond), 4 x [ConvT (polyphase, lrelu fused on staging)
                + noise_conv (accumulate) + 3 ResBlocks (lrelu fused, residual / running sum
-               fused in the epilogue)], conv_post (lrelu 0.01 + tanh fused)
+               fused in the epilogue; at 32 / 64 channels each conv pair is one fused launch,
+               csrc/resblock.hip)], conv_post (lrelu 0.01 + tanh fused)
 
 Only full-length phones are supported (x_mask all ones): in ``VC.voice_conversion``
 ``p_len == phone length`` always holds (2*T_f <= N//160; see DESIGN.md).
@@ -190,13 +191,21 @@ class SynthesizerAMD:
             nc, s, pad = self.noise[i]
             nc(har.view(1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True)
             C = self.chans[i]
-            t1 = torch.empty(C, Li, device=dev)
+            t1 = None  # c1 output of the unfused pairs
             xa = torch.empty(C, Li, device=dev)
             xb = torch.empty(C, Li, device=dev)
             xs = torch.empty(C, Li, device=dev)
             for j, (kk, pairs) in enumerate(self.res[i]):
                 cur = y
                 for m, (d, c1, c2) in enumerate(pairs):
+                    last = m == len(pairs) - 1
+                    if ops.resblock_fusable(c1, c2, d):  # one launch, c1's output stays in LDS
+                        nxt = xs if last else (xa if cur is not xa else xb)
+                        ops.resblock_pair(cur, nxt, c1, c2, d, LRELU_SLOPE, accumulate=last and j > 0)
+                        cur = nxt
+                        continue
+                    if t1 is None:
+                        t1 = torch.empty(C, Li, device=dev)
                     c1(cur, pad=(kk * d - d) // 2, dil=d, out=t1, in_act=ACT_LRELU, in_slope=LRELU_SLOPE)
                     if m == len(pairs) - 1:
                         c2(t1, pad=(kk - 1) // 2, out=xs, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,

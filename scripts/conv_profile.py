@@ -48,10 +48,25 @@ def main():
         rec.append((key, e0, e1, ops.LAST_CONV_FLOPS))
         return out
 
+    orig_rb = ops.resblock_pair
+
+    def wrapped_rb(x, y, c1, c2, dil, slope, accumulate=False):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        out = orig_rb(x, y, c1, c2, dil, slope, accumulate=accumulate)
+        e1.record(s)
+        C, L = x.shape
+        key = (1, C, C, c1.K, 1, dil, 1, L, 1, "", "pair", "acc" if accumulate else "", "rb")
+        rec.append((key, e0, e1, 2 * 2.0 * C * C * c1.K * L))
+        return out
+
     ops.conv1d = wrapped
+    ops.resblock_pair = wrapped_rb
     vc.pipeline_device(hub, net_g, 0, audio, 0, "v2", 0.33)
     torch.cuda.synchronize()
     ops.conv1d = orig
+    ops.resblock_pair = orig_rb
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
     for key, e0, e1, fl in rec:
         a = agg[key]

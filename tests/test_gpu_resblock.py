@@ -1,0 +1,86 @@
+"""Fused ResBlock pair (csrc/resblock.hip): one launch of y (+)= x + c2(lrelu(c1(lrelu(x), d))) against
+the two-launch split-bf16 conv path it replaces (bit-identical: same k-order, passes and epilogue order)
+and against a plain torch fp32 reference of residuals.py:22-44 (one pair)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from rvc_amd import ops
+from rvc_amd.ops import ACT_LRELU, Conv
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def make_pair(C, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    s = 1.0 / np.sqrt(C * K)
+    w1 = torch.randn(C, C, K, generator=g) * s
+    w2 = torch.randn(C, C, K, generator=g) * s
+    b1 = torch.randn(C, generator=g) * 0.1
+    b2 = torch.randn(C, generator=g) * 0.1
+    return (w1, b1, w2, b2), Conv(w1, b1, device=DEV), Conv(w2, b2, device=DEV)
+
+
+def two_launch(x, c1, c2, K, d, y=None, accumulate=False):
+    t1 = c1(x, pad=(K * d - d) // 2, dil=d, in_act=ACT_LRELU, in_slope=0.1)
+    out = y if y is not None else torch.empty_like(x)
+    c2(t1, pad=(K - 1) // 2, out=out, res=x, in_act=ACT_LRELU, in_slope=0.1, accumulate=accumulate)
+    return out
+
+
+def torch_ref(x, w, K, d):
+    w1, b1, w2, b2 = w
+    xt = F.conv1d(F.leaky_relu(x[None], 0.1), w1, b1, padding=(K * d - d) // 2, dilation=d)
+    xt = F.conv1d(F.leaky_relu(xt, 0.1), w2, b2, padding=(K - 1) // 2)
+    return (xt + x[None])[0]
+
+
+@pytest.mark.parametrize("C", [32, 64])
+@pytest.mark.parametrize("K,d", [(3, 1), (3, 5), (7, 3), (11, 1), (11, 5)])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+def test_fused_pair_bit_identical_to_two_launches(C, K, d, precision):
+    w, c1, c2 = make_pair(C, K, seed=C * 100 + K * 10 + d)
+    L = 5003  # several tiles and a partial one
+    x = torch.randn(C, L, generator=torch.Generator().manual_seed(K + d)).to(DEV)
+    with ops.precision(precision):
+        ref = two_launch(x, c1, c2, K, d)
+        y = torch.full_like(x, float("nan"))
+        ops.resblock_pair(x, y, c1, c2, d, 0.1)
+        acc0 = torch.randn(C, L, generator=torch.Generator().manual_seed(7)).to(DEV)
+        ya, yb = acc0.clone(), acc0.clone()
+        two_launch(x, c1, c2, K, d, y=ya, accumulate=True)
+        ops.resblock_pair(x, yb, c1, c2, d, 0.1, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert torch.equal(ya, yb)
+    if precision == "fp32":
+        r = torch_ref(x.cpu(), w, K, d)
+        err = (y.cpu() - r).abs().max().item()
+        assert err <= 2e-5 * max(1.0, r.abs().max().item()), err
+
+
+@pytest.mark.parametrize("L", [1, 7, 100, 239, 240, 241])
+def test_fused_pair_short_and_edge_lengths(L):
+    C, K, d = 32, 11, 5
+    w, c1, c2 = make_pair(C, K, seed=5)
+    x = torch.randn(C, L, generator=torch.Generator().manual_seed(L)).to(DEV)
+    y = torch.empty_like(x)
+    ops.resblock_pair(x, y, c1, c2, d, 0.1)
+    torch.cuda.synchronize()
+    r = torch_ref(x.cpu(), w, K, d)
+    assert (y.cpu() - r).abs().max().item() <= 2e-5 * max(1.0, r.abs().max().item())
+    assert torch.equal(y, two_launch(x, c1, c2, K, d))
+
+
+def test_fused_pair_rejects_bad_args():
+    w, c1, c2 = make_pair(32, 3, seed=1)
+    x = torch.randn(32, 100, device=DEV)
+    with pytest.raises(ValueError):
+        ops.resblock_pair(x, x, c1, c2, 1, 0.1)  # aliasing
+    w16, c16a, c16b = make_pair(16, 3, seed=2)
+    assert not ops.resblock_fusable(c16a, c16b, 1)
+    x16 = torch.randn(16, 100, device=DEV)
+    with pytest.raises(RuntimeError):
+        ops.resblock_pair(x16, torch.empty_like(x16), c16a, c16b, 1, 0.1)
