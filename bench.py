@@ -200,6 +200,9 @@ def main():
                     help="split-bf16 conv engine arithmetic: 6 / 3 / 1 bf16 MFMA passes per product")
     ap.add_argument("--chunks", type=int, default=1,
                     help="clips per GPU per step (BASELINE configs[2]: 64 x 10 s chunks; each a distinct clip)")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="clips per batched pass (VC.pipeline_device_batch: RMVPE + ContentVec batched over equal-"
+                         "length clips); --chunks must be a multiple")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one hipGraph per clip (rvc_amd.graph.ClipGraph, BASELINE configs[4])")
     ap.add_argument("--index-rate", type=float, default=0.0,
@@ -255,9 +258,19 @@ def main():
         from rvc_amd.graph import ClipGraph
         clip_graph = ClipGraph(vc, hub, net_g, 0, audio_dev.numel(), 0, "v2", 0.33, index, args.index_rate, args.f0)
 
+    if args.batch > 1 and (args.graph or len(clips) % args.batch):
+        raise SystemExit("bench.py: --batch needs eager mode and --chunks a multiple of it")
+
     def step():
         outs = []
-        for clip in clips:
+        if args.batch > 1:
+            for g0 in range(0, len(clips), args.batch):
+                outs += vc.pipeline_device_batch(hub, net_g, 0, clips[g0:g0 + args.batch], 0, "v2", 0.33, index,
+                                                 args.index_rate, args.f0)
+            clips_iter = []
+        else:
+            clips_iter = clips
+        for clip in clips_iter:
             if clip_graph is not None:
                 outs.append(clip_graph(clip).clone() if len(clips) > 1 else clip_graph(clip))
             else:
@@ -331,7 +344,9 @@ def main():
                                        f"{'one' if len(clips) == 1 else f'{len(clips)} x'} "
                                        f"{args.seconds:g} s clip per GPU per step, "
                                        + (f"IVF-Flat index_rate {args.index_rate:g}" if index is not None else "no index")
-                                       + ", protect 0.33" + (", hipGraph replay per clip" if args.graph else ""),
+                                       + ", protect 0.33" + (", hipGraph replay per clip" if args.graph else "")
+                                       + (f", RMVPE + ContentVec batched {args.batch} clips per pass"
+                                          if args.batch > 1 else ""),
                            "model": f"RVC v2 {args.sr // 1000}k (NSF-HiFiGAN) + ContentVec + {args.f0}",
                            "global_batch": world * len(clips),
                            "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",

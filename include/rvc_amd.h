@@ -218,6 +218,9 @@ int rvc_img_to_seq(const float* img, float* x, int64_t C, int64_t H, int64_t W, 
 int rvc_bigru(const float* gi, const float* whh, const float* bhh, float* y, void* gran_ws, int* err, int64_t T,
               rvc_stream_t stream);
 unsigned rvc_bigru_set_spin_limit(unsigned limit);
+/* bigru_batched: B independent sequences (gi + b*gi_bs, y + b*y_bs); gran_ws: 8192 B * min(B, 16) scratch. */
+int rvc_bigru_batched(const float* gi, int64_t gi_bs, const float* whh, const float* bhh, float* y, int64_t y_bs,
+                      void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream);
 /* Optional steps of VC.get_f0 between the raw f0 and the mel quantiser (convert.py:311-318), in
  * the reference's order: autotune (Autotune.autotune_f0, convert.py:168-179: f += (nearest of the 54
  * reference notes - f) * strength, first note on ties, unvoiced frames included) on the raw f0, then

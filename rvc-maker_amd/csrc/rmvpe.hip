@@ -154,9 +154,14 @@ extern "C" int rvc_img_to_seq(const float* img, float* x, int64_t C, int64_t H, 
 constexpr int GRU_H = 256;
 constexpr int GRU_WG_PER_DIR = 16;
 
+// Batched form: blockIdx.y = sequence b (gi + b gi_bs, y + b y_bs, its own granule pair): B sequences
+// advance in lockstep-free parallel at the latency of one (VC.pipeline_device_batch's equal-length chunks).
 __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float* whh, const float* bhh, float* y,
                                                     unsigned long long* gran, int* err, int64_t T,
-                                                    unsigned spin_limit) {
+                                                    unsigned spin_limit, int64_t gi_bs, int64_t y_bs) {
+    gi += (int64_t)blockIdx.y * gi_bs;
+    y += (int64_t)blockIdx.y * y_bs;
+    gran += (int64_t)blockIdx.y * 2 * 2 * GRU_H;
     const int d = blockIdx.x / GRU_WG_PER_DIR;
     const int j = blockIdx.x % GRU_WG_PER_DIR;
     const int tid = threadIdx.x;
@@ -245,12 +250,25 @@ extern "C" unsigned rvc_bigru_set_spin_limit(unsigned limit) {
 
 extern "C" int rvc_bigru(const float* gi, const float* whh, const float* bhh, float* y, void* gran_ws, int* err,
                          int64_t T, rvc_stream_t stream) {
-    RVC_CHECK_ARG(gi && whh && bhh && y && gran_ws && err && T > 0 && T < (1ll << 31), "bigru: bad args");
+    return rvc_bigru_batched(gi, 0, whh, bhh, y, 0, gran_ws, err, 1, T, stream);
+}
+
+// Sequences per launch: 32 workgroups each, all of which must be co-resident for the granule hand-off
+// (2 per CU at 16 sequences); larger batches run as consecutive launches.
+constexpr int GRU_B_MAX = 16;
+
+extern "C" int rvc_bigru_batched(const float* gi, int64_t gi_bs, const float* whh, const float* bhh, float* y,
+                                 int64_t y_bs, void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream) {
+    RVC_CHECK_ARG(gi && whh && bhh && y && gran_ws && err && T > 0 && T < (1ll << 31) && B > 0, "bigru: bad args");
+    RVC_CHECK_ARG(B == 1 || (gi_bs >= 2 * 3 * GRU_H * T && y_bs >= 2 * GRU_H * T), "bigru: batch strides too small");
     hipStream_t s = (hipStream_t)stream;
-    RVC_HIP(hipMemsetAsync(gran_ws, 0, 2 * 2 * GRU_H * sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(bigru_kernel, dim3(2 * GRU_WG_PER_DIR), dim3(256), 0, s, gi, whh, bhh, y,
-                       (unsigned long long*)gran_ws, err, T, g_bigru_spin_limit);
-    RVC_HIP(hipGetLastError());
+    for (int64_t b0 = 0; b0 < B; b0 += GRU_B_MAX) {
+        const int64_t nb = B - b0 < GRU_B_MAX ? B - b0 : GRU_B_MAX;
+        RVC_HIP(hipMemsetAsync(gran_ws, 0, (size_t)nb * 2 * 2 * GRU_H * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(bigru_kernel, dim3(2 * GRU_WG_PER_DIR, (unsigned)nb), dim3(256), 0, s, gi + b0 * gi_bs, whh,
+                           bhh, y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, g_bigru_spin_limit, gi_bs, y_bs);
+        RVC_HIP(hipGetLastError());
+    }
     return RVC_OK;
 }
 

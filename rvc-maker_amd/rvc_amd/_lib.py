@@ -93,6 +93,8 @@ SIGNATURES = {
     "rvc_img_to_seq": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_bigru": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "rvc_bigru_set_spin_limit": [ctypes.c_uint],
+    "rvc_bigru_batched": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64,
+                          c_void_p],
     "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, POINTER(F0Post), c_void_p, c_void_p,
                          c_void_p, c_void_p],
     "rvc_filtfilt_work_bytes": [c_int64],

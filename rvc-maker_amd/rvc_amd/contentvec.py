@@ -88,37 +88,41 @@ class ContentVecAMD:
         self.device = dev
 
     def features_cf(self, wav: torch.Tensor, output_layer: int = 12) -> torch.Tensor:
-        """wav: device f32 [N] (16 kHz) -> encoder output after ``output_layer`` layers, [768][T_f]."""
+        """wav: device f32 [N] (16 kHz) -> encoder output after ``output_layer`` layers, [768][T_f];
+        or B equal-length signals [B][N] -> [B][768][T_f] (every conv / norm / attention batched)."""
         dev = wav.device
-        N = wav.numel()
-        x = wav.view(1, N)
+        batched = wav.dim() == 2
+        B, N = (wav.shape[0], wav.shape[1]) if batched else (1, wav.numel())
+        x = wav.reshape(B, 1, N) if batched else wav.view(1, N)
         for i, (c, k, s) in enumerate(FE_LAYERS):
             if i == 0:
                 x = self.fe[0](x, stride=s)
-                ops.chnorm_gelu(x, self.gn[0], self.gn[1], x, 1, c, x.shape[-1])
+                ops.chnorm_gelu(x, self.gn[0], self.gn[1], x, B, c, x.shape[-1])
             else:
                 x = self.fe[i](x, stride=s, out_act=ACT_GELU)
         T = x.shape[-1]
-        ops.layernorm_cf(x, None, self.ln[0], self.ln[1], x, 1, 512, T)
-        x = self.proj(x)  # [768][T]
+        ops.layernorm_cf(x, None, self.ln[0], self.ln[1], x, B, 512, T)
+        x = self.proj(x)  # [(B)][768][T]
         E = self.E
-        x2 = torch.empty(E, T, device=dev)
+        bs = (B,) if batched else ()
+        x2 = torch.empty(*bs, E, T, device=dev)
         self.pos_conv(x, pad=self.pos_k // 2, Lout=T, out=x2, out_act=ACT_GELU, res=x)  # SamePad drops the last col
         x = x2
-        ops.layernorm_cf(x, None, self.enc_ln[0], self.enc_ln[1], x, 1, E, T)
+        ops.layernorm_cf(x, None, self.enc_ln[0], self.enc_ln[1], x, B, E, T)
         H = self.heads
         D = E // H
-        o = torch.empty(E, T, device=dev)
-        y = torch.empty(E, T, device=dev)
+        o = torch.empty(*bs, E, T, device=dev)
+        y = torch.empty(*bs, E, T, device=dev)
         for L in self.layers[:output_layer]:
             qkv = L["qkv"](x)
-            ops.attention(qkv, qkv[E:], qkv[2 * E:], o, B=1, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
-                          o_hs=D * T, scale=D ** -0.5)
+            k, v = (qkv[:, E:], qkv[:, 2 * E:]) if batched else (qkv[E:], qkv[2 * E:])
+            ops.attention(qkv, k, v, o, B=B, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
+                          o_hs=D * T, scale=D ** -0.5, q_bs=3 * E * T, k_bs=3 * E * T, v_bs=3 * E * T, o_bs=E * T)
             L["o"](o, out=y)
-            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, 1, E, T)
+            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, E, T)
             h = L["fc1"](x, out_act=ACT_GELU)
             L["fc2"](h, out=y)
-            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, 1, E, T)
+            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, B, E, T)
         return x
 
     # ------------------------------------------------------------------ reference API

@@ -190,6 +190,12 @@ def _workspace(device, nbytes, kind="conv"):
     return buf
 
 
+def _room(t):
+    """Elements addressable from t.data_ptr() to the end of its storage (views of batched buffers are
+    strided: their numel understates what a kernel with batch strides may touch)."""
+    return t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+
+
 def _shape3(x):
     if x.dim() == 2:
         return 1, x.shape[0], x.shape[1]
@@ -224,10 +230,12 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
     if out is None:
         out = torch.empty(B, Co, Lout, device=x.device, dtype=torch.float32) if B > 1 else \
             torch.empty(Co, Lout, device=x.device, dtype=torch.float32)
-    elif out.numel() < (B - 1) * (y_bstride or Co * Lout) + Co * Lout:
+    elif _room(out) < (B - 1) * (y_bstride or Co * Lout) + Co * Lout:
         raise ValueError("conv1d: output buffer too small")
-    if res is not None and res.numel() < (B - 1) * (res_bstride or Co * Lout) + Co * Lout:
+    if res is not None and _room(res) < (B - 1) * (res_bstride or Co * Lout) + Co * Lout:
         raise ValueError("conv1d: residual too small")
+    if _room(x) < (B - 1) * (x_bstride or Ci * Lin) + Ci * Lin:
+        raise ValueError("conv1d: input buffer too small")
     if bias is not None and bias.numel() < Co:
         raise ValueError("conv1d: bias too small")
     a = _lib.Conv1dArgs()
@@ -437,6 +445,20 @@ def bigru(gi, whh, bhh, y, gran, err, T):
     if gi.numel() < 2 * 768 * T or whh.numel() < 2 * 768 * 256 or y.numel() < 512 * T or gran.numel() < 1024:
         raise ValueError("bigru: size mismatch")
     check(_lib.load().rvc_bigru(_p(gi), _p(whh), _p(bhh), _p(y), _p(gran), _p(err), T, _stream()), "bigru")
+    return y
+
+
+GRU_B_MAX = 16  # sequences per bigru launch (rvc_bigru_batched); gran scratch is 1024 int64 per sequence
+
+
+def bigru_batched(gi, whh, bhh, y, gran, err, B, T):
+    """B independent BiGRU recurrences: gi [B][1536][T], y [B][512][T] (batch strides from the tensors)."""
+    if gi.dim() != 3 or y.dim() != 3 or gi.shape[0] < B or y.shape[0] < B or gi.shape[1] != 1536 or y.shape[1] != 512:
+        raise ValueError("bigru_batched: gi [B][1536][T], y [B][512][T] expected")
+    if gi.shape[2] < T or y.shape[2] < T or gran.numel() < 1024 * min(B, GRU_B_MAX) or whh.numel() < 2 * 768 * 256:
+        raise ValueError("bigru_batched: size mismatch")
+    check(_lib.load().rvc_bigru_batched(_p(gi), gi.stride(0), _p(whh), _p(bhh), _p(y), y.stride(0), _p(gran), _p(err),
+                                        B, T, _stream()), "bigru_batched")
     return y
 
 

@@ -164,6 +164,55 @@ class VC:
         return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index,
                                         index_rate, f0_method, f0_opts, volume_envelope, src64)
 
+    def pipeline_device_batch(self, model, net_g, sid, audios, pitch, version, protect, index=None, index_rate=0.0,
+                              f0_method="rmvpe"):
+        """``pipeline_device`` over B equal-length clips at once (the chunk loop of convert.py:506-507 for
+        equal-length chunks, BASELINE configs[2]): RMVPE (U-Net, W_ih, the B BiGRU recurrences side by side)
+        and ContentVec run as B-batched launches on their two streams; the synthesizer -- whose generator
+        already fills the chip at one clip -- then runs per clip.  Clip b draws its noise with seed
+        ``self.seed + b``: it equals ``pipeline_device`` of that clip with ``seed = self.seed + b``, up to the
+        summation order of the batched GEMMs (split-K follows the batched grid).  Clips must fit one segment
+        (N + window <= t_max, 41 s)."""
+        B = len(audios)
+        audios = [a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(
+            self.device) for a in audios]
+        N = audios[0].numel()
+        if any(a.numel() != N for a in audios) or N + self.window > self.t_max:
+            raise ValueError("pipeline_device_batch: equal-length clips of at most t_max samples")
+        xpb = torch.stack([self.filt(a.contiguous(), self.t_pad)[0] for a in audios])  # [B][Np]
+        p_len = xpb.shape[1] // self.window
+        main = torch.cuda.current_stream(xpb.device)
+        side = self._side_stream(xpb.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            if f0_method == "rmvpe":
+                coarse, pitchf = self._rmvpe().f0_device_batch(xpb, 0.03, float(pitch))
+            else:
+                pairs = [self.f0_device(xpb[b], pitch, f0_method) for b in range(B)]
+                coarse, pitchf = torch.stack([c for c, _ in pairs]), torch.stack([f for _, f in pairs])
+            f0_done = torch.cuda.Event()
+            f0_done.record(side)
+        feats = model.features_cf(xpb, 9 if version == "v1" else 12)
+        if version == "v1":
+            feats = model.final_proj.conv(feats)
+        main.wait_event(f0_done)
+        for t in (coarse, pitchf):
+            t.record_stream(main)
+        xpb.record_stream(side)
+        tp = self.t_pad_tgt
+        if self._ws is None:
+            self._ws = torch.zeros(4, dtype=torch.int32, device=xpb.device)
+        outs = []
+        for b in range(B):
+            o = self.voice_conversion_device(model, net_g, sid, xpb[b], coarse[b, :p_len], pitchf[b, :p_len], version,
+                                             protect, b, feats=feats[b], index=index, index_rate=index_rate)
+            out = o[tp: o.numel() - tp]
+            ops.peak_normalize(out, self._ws)
+            outs.append(out)
+        return outs
+
     def _side_stream(self, device):
         # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a high-priority
         # stream so that its launches are dispatched ahead of the ContentVec ones: +1.5 % eager (603 ->

@@ -46,6 +46,7 @@ class _Conv2d:
         self.wx, self.wx_nmf = ops.pack_x6(self.w, 1, Ci, kh * kw, Co)
 
     def __call__(self, x, H, W, out, **kw):
+        """x / out: bordered images [C][H+2][W+2], or [B][C][H+2][W+2] views (batch strides from the views)."""
         wrap = W + 2
         L = (H + 2) * wrap
         if self.k == 3:
@@ -53,8 +54,17 @@ class _Conv2d:
             pad = wrap + 1
         else:
             toff, pad = [0], 0
-        return ops.conv1d(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L, B=1,
-                          out=out, toff=toff, wrap=wrap, wx=self.wx, wx_nmf=self.wx_nmf, **kw)
+        return ops.conv1d(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L,
+                          out=out, toff=toff, wrap=wrap, wx=self.wx, wx_nmf=self.wx_nmf, **_batch_kw(x, out, kw), **kw)
+
+
+def _batch_kw(x, out, kw):
+    """conv1d batch arguments for [B][C][H+2][W+2] image views (B = 1 for [C][H+2][W+2])."""
+    if x.dim() != 4:
+        return {"B": 1}
+    res = kw.get("res")
+    return {"B": x.shape[0], "x_bstride": x.stride(0), "y_bstride": out.stride(0),
+            "res_bstride": res.stride(0) if res is not None else 0}
 
 
 class _ConvT2d:
@@ -77,15 +87,20 @@ class _ConvT2d:
                 self.phases.append((wkm, [(dy, dx) for _, _, dy, dx in taps]) + ops.pack_x6(wkm, 1, Ci, len(taps), Co))
 
     def __call__(self, x, H, W, out_cat):
-        """x bordered [Ci][H+2][W+2] -> first Co channels of bordered out_cat [*][2H+2][2W+2]."""
+        """x bordered [Ci][H+2][W+2] -> first Co channels of bordered out_cat [*][2H+2][2W+2]
+        (or [B][...] views of both)."""
         wrap = W + 2
         L = (H + 2) * wrap
-        ph = torch.empty(4, self.Co, H + 2, W + 2, device=x.device)  # the phase convs write the zero border
+        B = x.shape[0] if x.dim() == 4 else None
+        # the phase convs write the zero border
+        ph = torch.empty((B or 1), 4, self.Co, H + 2, W + 2, device=x.device)
         for i, (wp, taps, wx, wx_nmf) in enumerate(self.phases):
             toff = [dy * wrap + dx for dy, dx in taps]
-            ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, B=1, out=ph[i],
-                       toff=toff, wrap=wrap, out_act=ACT_RELU, wx=wx, wx_nmf=wx_nmf)
-        ops.interleave4(ph, out_cat, self.Co, H, W)
+            out = ph[:, i] if B else ph[0, i]
+            ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, out=out,
+                       toff=toff, wrap=wrap, out_act=ACT_RELU, wx=wx, wx_nmf=wx_nmf, **_batch_kw(x, out, {}))
+        for b in range(B or 1):
+            ops.interleave4(ph[b], out_cat[b] if B else out_cat, self.Co, H, W)
 
 
 class RMVPEAMD:
@@ -156,14 +171,29 @@ class RMVPEAMD:
         ops.spec_mag(spec, mag, NFFT // 2 + 1, F)
         return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
 
+    def mel_spectrogram_batch(self, xb: torch.Tensor) -> torch.Tensor:
+        """B equal-length signals [B][N] -> log-mel [B][128][F] (the GEMMs batched, framing per signal)."""
+        B, N = xb.shape
+        F = 1 + N // HOP
+        dev = xb.device
+        frames = torch.empty(B, NFFT, F, device=dev)
+        for b in range(B):
+            ops.stft_frames(xb[b], self.window, frames[b], N, F, NFFT, HOP)
+        spec = self.dft(frames, flops=2.5 * NFFT * math.log2(NFFT) * F * B)
+        mag = torch.empty(B, NFFT // 2 + 1, F, device=dev)
+        for b in range(B):
+            ops.spec_mag(spec[b], mag[b], NFFT // 2 + 1, F)
+        return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
+
     def _cbr(self, blk, x, H, W, out):
         dev = x.device
         Co = blk["conv.0"].Co
+        bshape = (x.shape[0],) if x.dim() == 4 else ()
         # 2-D convs cover the whole bordered image and write its border as 0: no zero-fill needed
-        h = torch.empty(Co, H + 2, W + 2, device=dev)
+        h = torch.empty(*bshape, Co, H + 2, W + 2, device=dev)
         blk["conv.0"](x, H, W, h, out_act=ACT_RELU)
         if "sc" in blk:
-            sc = torch.empty(Co, H + 2, W + 2, device=dev)
+            sc = torch.empty(*bshape, Co, H + 2, W + 2, device=dev)
             blk["sc"](x, H, W, sc)
             res = sc
         else:
@@ -208,6 +238,63 @@ class RMVPEAMD:
         y = torch.empty(512, Tp, device=dev)
         ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran, self.err, Tp)
         return self.fc(y, out_act=ACT_SIGMOID), Tp
+
+    def salience_batch(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
+        """salience for B clips at once: mel [B][128][F] -> [B][360][Tp].  Every conv of the U-Net, the
+        W_ih / fc GEMMs and the BiGRU (B recurrences side by side) run batched; the per-image glue
+        kernels (mel image, pooling, phase interleave, image->sequence) run per clip."""
+        dev = mel.device
+        B, _, F = mel.shape
+        Tp = 32 * ((F - 1) // 32 + 1)
+        H, W = Tp, N_MELS
+        x = torch.zeros(B, 1, H + 2, W + 2, device=dev)
+        for b in range(B):
+            ops.mel_image(mel[b], x[b], N_MELS, F, Tp, self.in_scale, self.in_shift)
+        cats = []
+        C = 16
+        for l in range(5):
+            cat = torch.zeros(B, 2 * C, H + 2, W + 2, device=dev)
+            for bi, blk in enumerate(self.enc[l]):
+                out = cat[:, C:] if bi == self.nb - 1 else torch.empty(B, C, H + 2, W + 2, device=dev)
+                x = self._cbr(blk, x, H, W, out)
+            cats.append((cat, C, H, W))
+            pooled = torch.zeros(B, C, H // 2 + 2, W // 2 + 2, device=dev)
+            for b in range(B):
+                ops.avgpool2(x[b], pooled[b], C, H, W)
+            x, H, W = pooled, H // 2, W // 2
+            C *= 2
+        for layer in self.inter:
+            for blk in layer:
+                x = self._cbr(blk, x, H, W, torch.empty(B, blk["conv.0"].Co, H + 2, W + 2, device=dev))
+        for i, (convt, blocks) in enumerate(self.dec):
+            cat, C, Ho, Wo = cats[-1 - i]
+            convt(x, H, W, cat)
+            x, H, W = cat, Ho, Wo
+            for blk in blocks:
+                x = self._cbr(blk, x, H, W, torch.empty(B, blk["conv.0"].Co, H + 2, W + 2, device=dev))
+        img = torch.empty(B, 3, H + 2, W + 2, device=dev)
+        self.cnn(x, H, W, img)
+        seq = torch.empty(B, 3 * W, H, device=dev)
+        for b in range(B):
+            ops.img_to_seq(img[b], seq[b], 3, H, W)
+        gi = self.w_ih(seq)  # [B][1536][Tp]
+        y = torch.empty(B, 512, Tp, device=dev)
+        gran = self.gran if B == 1 else torch.zeros(1024 * min(B, ops.GRU_B_MAX), dtype=torch.int64, device=dev)
+        ops.bigru_batched(gi, self.w_hh, self.b_hh, y, gran, self.err, B, Tp)
+        return self.fc(y, out_act=ACT_SIGMOID), Tp
+
+    def f0_device_batch(self, xb: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, post=None):
+        """B equal-length signals [B][N] -> (coarse int64 [B][F], pitchf f32 [B][F]); same per-clip result as
+        ``f0_device`` up to the summation order of the batched GEMMs (split-K follows the batched grid)."""
+        with ops.precision(self.precision or ops.get_precision()):
+            mel = self.mel_spectrogram_batch(xb)
+            B, _, F = mel.shape
+            sal, Tp = self.salience_batch(mel)
+        coarse = torch.empty(B, F, dtype=torch.int64, device=xb.device)
+        pitchf = torch.empty(B, F, device=xb.device)
+        for b in range(B):
+            ops.rmvpe_decode(sal[b], Tp, F, thred, math.pow(2, pitch_shift / 12), None, coarse[b], pitchf[b], post)
+        return coarse, pitchf
 
     def f0_device(self, audio: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, want_f0=False,
                   post=None):
