@@ -118,7 +118,7 @@ def pmc_traffic(kernel_family="x6"):
     """Per-launch HBM bytes of a conv family from the committed PMC summary of this same bench step
     (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled
     per MI355X_MICROARCH.md), or None when absent."""
-    path = os.path.join(REPO, "profiles", "r1_pmc_traffic.json")
+    path = os.path.join(REPO, "profiles", "r2_pmc_traffic.json")
     try:
         with open(path) as f:
             return json.load(f)[kernel_family]["traffic_bytes_per_launch"]
@@ -319,7 +319,7 @@ def main():
                 # algorithmic bytes per launch measured here
                 "traffic": (pmc_traffic("x6") if (args.sr, args.f0, args.precision, args.index_rate, args.seconds)
                             == (48000, "rmvpe", "fp32", 0.0, 30.0) else None),
-                "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r1_pmc_traffic.json)",
+                "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r2_pmc_traffic.json)",
                 "algorithmic_bytes_per_launch": round(probe.algorithmic_bytes(engine=1)),
                 "kernel": f"conv_x6_kernel<*> + resblock_x6_kernel<*> (implicit-GEMM convs / fused ResBlock conv "
                           f"pairs, {npass} split-bf16 MFMA pass(es) per product); "

@@ -201,14 +201,20 @@ class RMVPEAMD:
         blk["conv.3"](h, H, W, out, out_act=ACT_RELU, res=res)
         return out
 
-    def salience(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
-        """mel2hidden + E2E (RMVPE.py:210-215, 143-144): mel [128][F] -> salience [360][Tp] (Tp = F rounded up to 32)."""
-        dev = mel.device
+    def mel_image(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
+        """mel2hidden's input (RMVPE.py:210-213): mel [128][F] -> bordered image [1][Tp+2][130] (reflect-padded
+        to Tp = F rounded up to 32, input BatchNorm applied), Tp."""
         F = mel.shape[-1]
         Tp = 32 * ((F - 1) // 32 + 1)
-        H, W = Tp, N_MELS
-        x = torch.zeros(1, H + 2, W + 2, device=dev)
+        x = torch.zeros(1, Tp + 2, N_MELS + 2, device=mel.device)
         ops.mel_image(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
+        return x, Tp
+
+    def unet_seq(self, x: torch.Tensor, H: int) -> torch.Tensor:
+        """E2E up to the GRU input (RMVPE.py:143-144, 254): bordered image [1][H+2][130] (H % 32 == 0)
+        -> cnn head rows [384][H]."""
+        dev = x.device
+        W = N_MELS
         cats = []
         C = 16
         for l in range(5):
@@ -234,10 +240,29 @@ class RMVPEAMD:
         self.cnn(x, H, W, img)
         seq = torch.empty(3 * W, H, device=dev)
         ops.img_to_seq(img, seq, 3, H, W)
+        return seq
+
+    def head(self, seq: torch.Tensor) -> torch.Tensor:
+        """BiGRU + Linear + Sigmoid (RMVPE.py:254-260, 141): seq [384][Tp] -> salience [360][Tp]."""
+        Tp = seq.shape[-1]
         gi = self.w_ih(seq)  # [1536][Tp]
-        y = torch.empty(512, Tp, device=dev)
+        y = torch.empty(512, Tp, device=seq.device)
         ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran, self.err, Tp)
-        return self.fc(y, out_act=ACT_SIGMOID), Tp
+        return self.fc(y, out_act=ACT_SIGMOID)
+
+    def salience(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
+        """mel2hidden + E2E (RMVPE.py:210-215, 143-144): mel [128][F] -> salience [360][Tp] (Tp = F rounded up to 32)."""
+        x, Tp = self.mel_image(mel)
+        return self.head(self.unet_seq(x, Tp)), Tp
+
+    def decode(self, sal, Tp, F, thred=0.03, pitch_shift=0.0, want_f0=False, post=None):
+        """rmvpe_decode over the first F frames of salience [360][Tp] -> (coarse, pitchf, f0 | None)."""
+        dev = sal.device
+        coarse = torch.empty(F, dtype=torch.int64, device=dev)
+        pitchf = torch.empty(F, device=dev)
+        f0 = torch.empty(F, dtype=torch.float64, device=dev) if want_f0 else None
+        ops.rmvpe_decode(sal, Tp, F, thred, math.pow(2, pitch_shift / 12), f0, coarse, pitchf, post)
+        return coarse, pitchf, f0
 
     def salience_batch(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
         """salience for B clips at once: mel [B][128][F] -> [B][360][Tp].  Every conv of the U-Net, the
@@ -304,12 +329,7 @@ class RMVPEAMD:
             mel = self.mel_spectrogram(audio)
             F = mel.shape[-1]
             sal, Tp = self.salience(mel)
-        dev = audio.device
-        coarse = torch.empty(F, dtype=torch.int64, device=dev)
-        pitchf = torch.empty(F, device=dev)
-        f0 = torch.empty(F, dtype=torch.float64, device=dev) if want_f0 else None
-        ops.rmvpe_decode(sal, Tp, F, thred, math.pow(2, pitch_shift / 12), f0, coarse, pitchf, post)
-        return coarse, pitchf, f0
+        return self.decode(sal, Tp, F, thred, pitch_shift, want_f0, post)
 
     def check_error(self):
         """Raise if a BiGRU launch since the last check timed out (its f0 is then garbage); clears the flag."""

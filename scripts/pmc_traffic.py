@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
-fam = {"conv_x6_kernel": "x6", "conv1d_mfma_kernel": "f32"}
+fam = {"conv_x6_kernel": "x6", "resblock_x6_kernel": "x6", "conv1d_mfma_kernel": "f32"}
 out = {}
 for counter in ("FETCH_SIZE", "WRITE_SIZE"):
     per = defaultdict(list)
