@@ -4,6 +4,7 @@
 // The 3x3 / 1x1 convolutions and the dense projections run on the implicit-GEMM MFMA
 // engine (conv1d.hip) over zero-bordered images.
 #include "rvc_common.h"
+#include <stdlib.h>
 
 // ---------------------------------------------------------------- STFT framing
 // framesT[n][f] = xr[f*hop + n - nfft/2] * win[n], centred reflect padding (torch.stft center=True,
@@ -167,7 +168,9 @@ __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float
     const int tid = threadIdx.x;
     const int ul = tid >> 4, s = tid & 15;
     const int u = j * 16 + ul;
-    __shared__ float hs[GRU_H];
+    // h of the previous step, double-buffered by step parity: step t reads hs[t & 1] and the next step
+    // writes hs[(t + 1) & 1], so one barrier per step orders both
+    __shared__ float hs[2][GRU_H];
     __shared__ int abort_flag;
     if (tid == 0) abort_flag = 0;
     const float* W = whh + (int64_t)d * 3 * GRU_H * GRU_H;
@@ -183,18 +186,21 @@ __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float
     const float* G = gi + (int64_t)d * 3 * GRU_H * T;
     unsigned long long* GR = gran + (int64_t)d * 2 * GRU_H;
     float hprev = 0.f;
+    // input projections of the current step, loaded one step ahead (after the poll, so that the poll's
+    // wait does not queue behind them in vmcnt order)
+    float gxr = 0.f, gxz = 0.f, gxn = 0.f;
+    if (s == 0) {
+        const int64_t tau0 = d ? T - 1 : 0;
+        gxr = G[(int64_t)u * T + tau0];
+        gxz = G[(int64_t)(GRU_H + u) * T + tau0];
+        gxn = G[(int64_t)(2 * GRU_H + u) * T + tau0];
+    }
+    hs[0][tid] = 0.f;
     __syncthreads();
     for (int64_t t = 0; t < T; ++t) {
         const int64_t tau = d ? T - 1 - t : t;
-        float gxr = 0.f, gxz = 0.f, gxn = 0.f;
-        if (s == 0) {
-            gxr = G[(int64_t)u * T + tau];
-            gxz = G[(int64_t)(GRU_H + u) * T + tau];
-            gxn = G[(int64_t)(2 * GRU_H + u) * T + tau];
-        }
-        if (t == 0) {
-            hs[tid] = 0.f;
-        } else {
+        const int cur = (int)(t & 1);
+        if (t > 0) {
             unsigned long long* g = GR + ((t - 1) & 1) * GRU_H + tid;
             unsigned long long v;
             unsigned spins = 0;
@@ -208,14 +214,21 @@ __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            hs[tid] = __uint_as_float((uint32_t)v);
+            hs[cur][tid] = __uint_as_float((uint32_t)v);
+            __syncthreads();
+            if (abort_flag) break;
         }
-        __syncthreads();
-        if (abort_flag) break;
+        float nxr = 0.f, nxz = 0.f, nxn = 0.f;
+        if (s == 0 && t + 1 < T) {
+            const int64_t tn = d ? T - 2 - t : t + 1;
+            nxr = G[(int64_t)u * T + tn];
+            nxz = G[(int64_t)(GRU_H + u) * T + tn];
+            nxn = G[(int64_t)(2 * GRU_H + u) * T + tn];
+        }
         float pr = 0.f, pz = 0.f, pn = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const float h = hs[16 * s + i];
+            const float h = hs[cur][16 * s + i];
             pr += wr[i] * h;
             pz += wz[i] * h;
             pn += wn[i] * h;
@@ -232,11 +245,13 @@ __global__ __launch_bounds__(256) void bigru_kernel(const float* gi, const float
             const float n = tanhf(gxn + r * (pn + bhn));
             const float h = (hprev - n) * z + n;
             hprev = h;
-            y[(int64_t)(d * GRU_H + u) * T + tau] = h;
             const unsigned long long gv = ((unsigned long long)(uint32_t)(t + 1) << 32) | __float_as_uint(h);
             __hip_atomic_store(GR + (t & 1) * GRU_H + u, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            y[(int64_t)(d * GRU_H + u) * T + tau] = h;
         }
-        __syncthreads();
+        gxr = nxr;
+        gxz = nxz;
+        gxn = nxn;
     }
 }
 

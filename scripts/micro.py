@@ -78,7 +78,7 @@ def branches():
     print(f"full pipeline_device: {timeit(lambda: vc.pipeline_device(hub, net_g, 0, audio, 0, 'v2', 0.33), 3):9.1f} us")
 
 
-if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] in ("retrieval", "synth")):
+if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] in ("retrieval", "synth", "bigru")):
     if len(sys.argv) > 1 and sys.argv[1] == "branches":
         branches()
         sys.exit(0)
@@ -120,3 +120,23 @@ def synth_stages():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "synth":
     synth_stages()
+
+
+def bigru_bench():
+    """The BiGRU recurrence alone at the 30 s shape (Tp = 3232), 1 and 16 sequences."""
+    from rvc_amd import ops, synthetic
+    from rvc_amd.rmvpe import RMVPEAMD
+    rm = RMVPEAMD(synthetic.rmvpe_state_dict(1236), "cuda")
+    T = 3232
+    g = torch.Generator().manual_seed(0)
+    for B in (1, 16):
+        gi = (torch.randn(B, 1536, T, generator=g) * 0.5).cuda()
+        y = torch.empty(B, 512, T, device="cuda")
+        gran = torch.zeros(1024 * B, dtype=torch.int64, device="cuda")
+        us = timeit(lambda: ops.bigru_batched(gi, rm.w_hh, rm.b_hh, y, gran, rm.err, B, T), 5)
+        print(f"bigru B={B:2d} T={T}: {us:9.1f} us  ({us / T * 1e3:.0f} ns per step)")
+    rm.check_error()
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bigru":
+    bigru_bench()
