@@ -7,6 +7,10 @@
 // segments), 16 threads reduce each column (two-pass mean / variance, as F.layer_norm),
 // then the tile is written back.  Covers synthesizers.py:170-181 and the fairseq
 // LayerNorms (fairseq.py:700, 1418, 1104) on this build's [C][T] layout.
+// The staging loop issues LN_UNROLL rows' loads before it uses any (C is a runtime value, so an
+// un-unrolled loop waited one HBM latency per row: 28 us for a 768 x 1599 tile set).
+constexpr int LN_UNROLL = 24;
+
 __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const float* res, const float* gamma,
                                                            const float* beta, float* out, int C, int64_t T,
                                                            float eps) {
@@ -17,17 +21,28 @@ __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const
     const int64_t t0 = (int64_t)blockIdx.x * 16;
     const int64_t t = t0 + col;
     const bool ok = t < T;
-    const float* xb = x + (int64_t)b * C * T;
-    const float* rb = res ? res + (int64_t)b * C * T : nullptr;
+    const int64_t tc = ok ? t : T - 1;  // clamped: every load is issued, masked at use
+    const float* xb = x + (int64_t)b * C * T + tc;
+    const float* rb = res ? res + (int64_t)b * C * T + tc : nullptr;
     float s = 0.f;
-    for (int c = grp; c < C; c += 16) {
-        float v = 0.f;
-        if (ok) {
-            v = xb[(int64_t)c * T + t];
-            if (rb) v += rb[(int64_t)c * T + t];
+    for (int c0 = grp; c0 < C; c0 += 16 * LN_UNROLL) {
+        float v[LN_UNROLL], r[LN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < LN_UNROLL; ++u) {
+            const int c = c0 + 16 * u;
+            const int cc = c < C ? c : C - 1;
+            v[u] = xb[(int64_t)cc * T];
+            r[u] = rb ? rb[(int64_t)cc * T] : 0.f;
         }
-        tile[c * 17 + col] = v;
-        s += v;
+#pragma unroll
+        for (int u = 0; u < LN_UNROLL; ++u) {
+            const int c = c0 + 16 * u;
+            if (c < C) {
+                const float w = ok ? (rb ? v[u] + r[u] : v[u]) : 0.f;
+                tile[c * 17 + col] = w;
+                s += w;
+            }
+        }
     }
     float* red = tile + C * 17;  // [16][17]
     red[grp * 17 + col] = s;
@@ -64,34 +79,60 @@ extern "C" int rvc_layernorm_cf(const float* x, const float* res, const float* g
 
 // ---------------------------------------------------------------- per-channel norm (+GELU)
 // GroupNorm(C, C) over time, affine, then exact GELU: the ContentVec conv feature
-// extractor's first block (fairseq.py:1149-1155, 1183-1185).  One block per (b, c).
+// extractor's first block (fairseq.py:1149-1155, 1183-1185).  One block per (b, c): the row's mean
+// and variance in one pass over it (sums of x - x[0] and its square: the shift keeps the
+// E[d^2] - E[d]^2 form well conditioned for a row whose mean is small against its spread), then the
+// normalise + GELU pass; every pass issues CN_UNROLL loads per thread before using them.
+constexpr int CN_UNROLL = 8;
+
 __global__ __launch_bounds__(256) void chnorm_gelu_kernel(const float* x, const float* gamma, const float* beta,
                                                           float* out, int C, int64_t L, float eps, int gelu) {
     const int c = blockIdx.x, b = blockIdx.y;
     const float* xr = x + ((int64_t)b * C + c) * L;
     float* orow = out + ((int64_t)b * C + c) * L;
-    __shared__ float red[4];
+    __shared__ float red[2][4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    float s = 0.f;
-    for (int64_t i = tid; i < L; i += 256) s += xr[i];
-    s = wave_sum(s);
-    if (lane == 0) red[w] = s;
-    __syncthreads();
-    const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)L;
-    __syncthreads();
-    float q = 0.f;
-    for (int64_t i = tid; i < L; i += 256) {
-        float d = xr[i] - mean;
-        q += d * d;
+    const float shift = xr[0];
+    float s = 0.f, q = 0.f;
+    for (int64_t i0 = tid; i0 < L; i0 += 256 * CN_UNROLL) {
+        float v[CN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < CN_UNROLL; ++u) {
+            const int64_t i = i0 + 256 * u;
+            v[u] = xr[i < L ? i : L - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < CN_UNROLL; ++u) {
+            const float d = i0 + 256 * u < L ? v[u] - shift : 0.f;
+            s += d;
+            q += d * d;
+        }
     }
+    s = wave_sum(s);
     q = wave_sum(q);
-    if (lane == 0) red[w] = q;
+    if (lane == 0) {
+        red[0][w] = s;
+        red[1][w] = q;
+    }
     __syncthreads();
-    const float rstd = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)L + eps);
+    const float ms = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)L;  // mean of x - shift
+    const float mq = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)L;
+    const float mean = shift + ms;
+    const float rstd = 1.0f / sqrtf(fmaxf(mq - ms * ms, 0.f) + eps);
     const float g = gamma[c], bt = beta[c];
-    for (int64_t i = tid; i < L; i += 256) {
-        float v = (xr[i] - mean) * rstd * g + bt;
-        orow[i] = gelu ? act_apply(v, RVC_ACT_GELU, 0.f) : v;
+    for (int64_t i0 = tid; i0 < L; i0 += 256 * CN_UNROLL) {
+        float v[CN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < CN_UNROLL; ++u) {
+            const int64_t i = i0 + 256 * u;
+            v[u] = xr[i < L ? i : L - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < CN_UNROLL; ++u) {
+            const int64_t i = i0 + 256 * u;
+            const float y = (v[u] - mean) * rstd * g + bt;
+            if (i < L) orow[i] = gelu ? act_apply(y, RVC_ACT_GELU, 0.f) : y;
+        }
     }
 }
 

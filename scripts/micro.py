@@ -78,7 +78,7 @@ def branches():
     print(f"full pipeline_device: {timeit(lambda: vc.pipeline_device(hub, net_g, 0, audio, 0, 'v2', 0.33), 3):9.1f} us")
 
 
-if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] in ("retrieval", "synth", "bigru")):
+if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] in ("retrieval", "synth", "bigru", "norms")):
     if len(sys.argv) > 1 and sys.argv[1] == "branches":
         branches()
         sys.exit(0)
@@ -140,3 +140,26 @@ def bigru_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bigru":
     bigru_bench()
+
+
+def norms():
+    """layernorm_cf / chnorm_gelu at the bench's shapes: time and HBM GB/s (bytes: read x (+res), write)."""
+    from rvc_amd import ops
+    g = torch.Generator().manual_seed(0)
+    for C, T, res in ((768, 1599, True), (192, 3198, True), (512, 1599, False)):
+        x = torch.randn(C, T, generator=g).cuda()
+        r = torch.randn(C, T, generator=g).cuda() if res else None
+        gm, bt = torch.ones(C).cuda(), torch.zeros(C).cuda()
+        out = torch.empty(C, T, device="cuda")
+        us = timeit(lambda: ops.layernorm_cf(x, r, gm, bt, out, 1, C, T), 20)
+        nb = 4 * C * T * (3 if res else 2)
+        print(f"layernorm_cf C={C} T={T} res={int(res)}: {us:7.1f} us  {nb / us / 1e3:7.1f} GB/s")
+    x = torch.randn(512, 102399, generator=g).cuda()
+    out = torch.empty_like(x)
+    us = timeit(lambda: ops.chnorm_gelu(x, torch.ones(512).cuda(), torch.zeros(512).cuda(), out, 1, 512, 102399), 10)
+    nb = 4 * 512 * 102399 * 3
+    print(f"chnorm_gelu C=512 L=102399: {us:7.1f} us  {nb / us / 1e3:7.1f} GB/s (2 reads + 1 write)")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "norms":
+    norms()
