@@ -2,7 +2,11 @@
 per GPU per step (BASELINE.json configs[1]; N>1 = configs[3]-style utterance sharding with the
 output waveforms gathered to rank 0 over RCCL).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--no-cpu-baseline] [--no-stream]
+
+Default: a clip stream (VC.pipeline_device_stream) -- K steps are K clips per GPU, clip k+1's front end
+(filtfilt, RMVPE, ContentVec) running on its own streams under clip k's synthesizer; the line also carries
+"per_call", the same K clips as one finished pipeline_device call each.
 
 --gpus N without WORLD_SIZE in the environment starts N ranks itself (torch.distributed.run as a
 child process, one rank per GPU); under an external launcher WORLD_SIZE must equal N.
@@ -205,6 +209,11 @@ def main():
                          "length clips); --chunks must be a multiple")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one hipGraph per clip (rvc_amd.graph.ClipGraph, BASELINE configs[4])")
+    ap.add_argument("--no-stream", dest="stream", action="store_false",
+                    help="per-call passes (one VC.pipeline_device per clip, each finished before the next) instead of "
+                         "the default clip stream (VC.pipeline_device_stream: clip k+1's filtfilt / f0 / features on "
+                         "a front stream while clip k's synthesizer runs on a back stream; K steps = K clips per GPU, "
+                         "all issued inside the timed region)")
     ap.add_argument("--index-rate", type=float, default=0.0,
                     help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
@@ -258,6 +267,8 @@ def main():
         from rvc_amd.graph import ClipGraph
         clip_graph = ClipGraph(vc, hub, net_g, 0, audio_dev.numel(), 0, "v2", 0.33, index, args.index_rate, args.f0)
 
+    if args.graph or args.batch > 1:
+        args.stream = False  # the graph replays and the batched passes are their own chunk loops
     if args.batch > 1 and (args.graph or len(clips) % args.batch):
         raise SystemExit("bench.py: --batch needs eager mode and --chunks a multiple of it")
 
@@ -282,16 +293,33 @@ def main():
                 gathered[0] += sum(len(g) for g in got)
         return outs[-1]
 
+    def run_stream(nsteps):
+        # one stream over nsteps x chunks clips: every clip's whole pass is issued inside the call, and the
+        # call returns after the last clip's output is ordered on this stream
+        order = [clips[i % len(clips)] for i in range(nsteps * len(clips))]
+        outs = vc.pipeline_device_stream(hub, net_g, 0, order, 0, "v2", 0.33, index, args.index_rate, args.f0)
+        if dist is not None:
+            got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0)
+            if got is not None:
+                gathered[0] += sum(len(g) for g in got)
+        return outs[-1]
+
     gathered = [0]
 
-    for _ in range(args.warmup):
-        step()
+    if args.stream:
+        if args.warmup:
+            run_stream(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if args.stream:
+        out = run_stream(args.steps)
+    for _ in range(0 if args.stream else args.steps):
         out = step()
     torch.cuda.synchronize()
     if dist is not None:
@@ -302,6 +330,18 @@ def main():
         t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
+    per_call = None
+    if args.stream and world == 1:
+        # the same K steps as one pipeline_device call per clip, each finished before the next (the
+        # reference's loop): the stream's gain over it, measured on the same box right after
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dt1 = time.perf_counter() - t1
+        per_call = {"value": round(args.steps * len(clips) * (out.numel() / float(args.sr)) / dt1, 3),
+                    "ms_per_step": round(dt1 / args.steps * 1e3, 3)}
     audio_s = out.numel() / float(args.sr)  # every clip has the same length
     value = world * args.steps * len(clips) * audio_s / dt  # whole job: every rank's clips over the max time
     gathered_per_step = gathered[0] / max(args.warmup + args.steps, 1) if dist is not None else len(clips)
@@ -345,13 +385,15 @@ def main():
                                        f"{args.seconds:g} s clip per GPU per step, "
                                        + (f"IVF-Flat index_rate {args.index_rate:g}" if index is not None else "no index")
                                        + ", protect 0.33" + (", hipGraph replay per clip" if args.graph else "")
+                                       + (", clip stream (clip k+1 f0/features under clip k synthesizer)"
+                                          if args.stream else "")
                                        + (f", RMVPE + ContentVec batched {args.batch} clips per pass"
                                           if args.batch > 1 else ""),
                            "model": f"RVC v2 {args.sr // 1000}k (NSF-HiFiGAN) + ContentVec + {args.f0}",
                            "global_batch": world * len(clips),
                            "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",
                            "output_seconds_per_clip": round(audio_s, 4)},
-                "roofline": roof, "cpu_baseline": cpu}
+                "per_call": per_call, "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -342,8 +342,12 @@ int launch_rb(const RbParams& p, hipStream_t s) {
                                     160 * 1024));
         attr = true;
     }
+    // workgroups per CU: 1 = persistent; more = shorter tile runs that the dispatcher hands to CUs as they free
+    // up (a CU held by a concurrent stream's kernel then delays fewer tiles)
+    static const int per_cu = getenv("RVC_RB_PER_CU") ? atoi(getenv("RVC_RB_PER_CU")) : 1;
     const int ntiles = (p.L + RbGeom<C>::N - 1) / RbGeom<C>::N;
-    hipLaunchKernelGGL((resblock_x6_kernel<C, NP>), dim3(ntiles < ncu ? ntiles : ncu), dim3(768), lds, s, p);
+    const int nwg = ncu * (per_cu > 0 ? per_cu : 1);
+    hipLaunchKernelGGL((resblock_x6_kernel<C, NP>), dim3(ntiles < nwg ? ntiles : nwg), dim3(768), lds, s, p);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }

@@ -48,7 +48,9 @@ class ClipGraph:
         # The graph owns its scratch: every split-K / split-KV / decode workspace its kernels point at
         # lives in self.workspaces for the graph's lifetime, shared with no eager pass or other graph.
         self.workspaces = {}
-        s = torch.cuda.Stream(device=dev)
+        # warm-up and capture on a pooled normal-priority stream (no extra stream: the process has 4 hardware
+        # queues, pipeline._pooled_stream)
+        s = vc._pooled_stream(dev, 0, vc.STREAM_SLOT["front"])
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s), ops.device_seed(self.seed), ops.private_workspaces(self.workspaces):
             for _ in range(max(1, warmup)):
@@ -56,7 +58,7 @@ class ClipGraph:
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph), ops.device_seed(self.seed), ops.private_workspaces(self.workspaces):
+        with torch.cuda.graph(self.graph, stream=s), ops.device_seed(self.seed), ops.private_workspaces(self.workspaces):
             self.out = vc.pipeline_device(*args, **kw)
 
     def __call__(self, audio: torch.Tensor, seed: int | None = None) -> torch.Tensor:

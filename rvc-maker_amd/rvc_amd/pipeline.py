@@ -213,18 +213,114 @@ class VC:
             outs.append(out)
         return outs
 
+    def pipeline_device_stream(self, model, net_g, sid, audios, pitch, version, protect, index=None, index_rate=0.0,
+                               f0_method="rmvpe"):
+        """``pipeline_device`` over a sequence of clips (the file / chunk loops of convert.py:129-135 and
+        :506-507) with clip k+1's front end -- filtfilt, f0 on the side stream, ContentVec features -- issued
+        on a front stream while clip k's synthesizer runs on a back stream.  The two are independent, so the
+        front end's small, latency-bound launches (the U-Net's deep levels, the BiGRU's 32 workgroups, the
+        ContentVec GEMMs) fill the CUs the generator's kernels leave between blocks and launches instead of
+        running as a phase of their own.
+
+        Clip k draws its noise with seed ``self.seed + k`` (as ``pipeline_device_batch``): its waveform is
+        bit-identical to ``pipeline_device`` of that clip at ``seed = self.seed + k`` -- every launch is the
+        same launch on the same data, only its stream differs.  Clips must fit one segment (N + window <=
+        t_max, 41 s; longer inputs go through ``pipeline_device``'s host quiet-point search).  Returns the
+        list of device waveforms, ordered on the caller's current stream."""
+        audios = [a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(
+            self.device) for a in audios]
+        if any(a.numel() + self.window > self.t_max for a in audios):
+            raise ValueError("pipeline_device_stream: clips of at most t_max samples (one segment each)")
+        if not audios:
+            return []
+        dev = audios[0].device
+        caller = torch.cuda.current_stream(dev)
+        front, back = self._aux_stream(dev, "front"), self._aux_stream(dev, "back")
+        if self._ws is None:
+            self._ws = torch.zeros(4, dtype=torch.int32, device=dev)
+        seed0, tp = self.seed, self.t_pad_tgt
+
+        def issue_front(a):
+            with torch.cuda.stream(front):
+                front.wait_stream(caller)  # the caller wrote the input on its own stream
+                a.record_stream(front)
+                xp, _ = self.filt(a.contiguous(), self.t_pad)
+                side = self._aux_stream(dev, "fside")
+                ready = torch.cuda.Event()
+                ready.record(front)
+                with torch.cuda.stream(side):
+                    side.wait_event(ready)
+                    coarse, pitchf = self.f0_device(xp, pitch, f0_method)
+                    f0_done = torch.cuda.Event()
+                    f0_done.record(side)
+                feats = self.features_device(model, xp, version)
+                front.wait_event(f0_done)
+                for t in (coarse, pitchf):
+                    t.record_stream(front)
+                xp.record_stream(side)
+                done = torch.cuda.Event()
+                done.record(front)
+            return (xp, coarse, pitchf, feats), done
+
+        outs = []
+        nxt = issue_front(audios[0])
+        try:
+            for k in range(len(audios)):
+                (xp, coarse, pitchf, feats), done = nxt
+                if k + 1 < len(audios):
+                    nxt = issue_front(audios[k + 1])  # queued ahead of clip k's synthesizer
+                with torch.cuda.stream(back):
+                    back.wait_event(done)
+                    for t in (xp, coarse, pitchf, feats):
+                        t.record_stream(back)
+                    p_len = xp.numel() // self.window
+                    self.seed = seed0 + k
+                    o = self.voice_conversion_device(model, net_g, sid, xp, coarse[:p_len], pitchf[:p_len], version,
+                                                     protect, 0, feats=feats, index=index, index_rate=index_rate)
+                    out = o[tp: o.numel() - tp]
+                    ops.peak_normalize(out, self._ws)
+                    outs.append(out)
+        finally:
+            self.seed = seed0
+        caller.wait_stream(back)
+        for o in outs:
+            o.record_stream(caller)
+        return outs
+
+    # clip-stream priorities (measured on one MI355X, 10 x 30 s clips: synthesizer stream high, front end
+    # normal: 808 xRT; front end high: 781; per-call pipeline_device: 678)
+    STREAM_PRIORITY = {"front": 0, "fside": 0, "back": -1}
+    # pool slot per role: streams of equal priority and slot are one stream object
+    STREAM_SLOT = {"front": 1, "fside": 0, "back": 0, "side": 0}
+
+    def _aux_stream(self, device, role):
+        """The clip stream's streams: "front" (filtfilt, ContentVec), "fside" (its f0 branch) and "back" (the
+        synthesizer).  The back stream runs at high priority: the synthesizers form the critical chain of
+        the stream, and the front end's few-block, latency-bound launches fill the CUs between them
+        (RVC_AMD_{FRONT,FSIDE,BACK}_PRIORITY override)."""
+        prio = int(os.environ.get(f"RVC_AMD_{role.upper()}_PRIORITY", str(self.STREAM_PRIORITY[role])))
+        return self._pooled_stream(device, prio, self.STREAM_SLOT[role])
+
+    def _pooled_stream(self, device, prio, slot):
+        """Streams are pooled by (priority, slot) and shared between roles that never run at once (the
+        per-call side stream is the clip stream's back stream, ClipGraph's normal-priority fork its fside
+        stream).  The device has GPU_MAX_HW_QUEUES = 4 hardware queues per process: with the default stream,
+        these three fill them, and a fifth stream would share a queue -- serialising, for example, RMVPE
+        behind ContentVec (measured: a per-call pass 30 % slower once a fifth stream existed)."""
+        key = f"{device}/{prio}/{slot}"
+        if getattr(self, "_streams", None) is None:
+            self._streams = {}
+        if key not in self._streams:
+            self._streams[key] = torch.cuda.Stream(device=device, priority=prio)
+        return self._streams[key]
+
     def _side_stream(self, device):
         # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a high-priority
         # stream so that its launches are dispatched ahead of the ContentVec ones: +1.5 % eager (603 ->
         # 612 xRT).  A captured graph runs 17 % slower with it, so ClipGraph sets side_priority = 0.
         prio = self.side_priority if getattr(self, "side_priority", None) is not None \
             else int(os.environ.get("RVC_AMD_SIDE_PRIORITY", "-1"))
-        key = f"{device}/{prio}"
-        if getattr(self, "_streams", None) is None:
-            self._streams = {}
-        if key not in self._streams:
-            self._streams[key] = torch.cuda.Stream(device=device, priority=prio)
-        return self._streams[key]
+        return self._pooled_stream(device, prio, self.STREAM_SLOT["side"])
 
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index=None,
                             index_rate=0.0, f0_method="rmvpe", f0_opts=None, volume_envelope=1.0, src64=None):

@@ -87,3 +87,21 @@ def test_pipeline_batch_matches_per_clip(models):
         rel = ((outs[b] - ref).double().pow(2).mean().sqrt() / ref.double().pow(2).mean().sqrt()).item()
         assert rel <= 1e-4, (b, rel)
     vc.check_errors()
+
+
+def test_stream_bit_identical_to_per_clip(models):
+    """VC.pipeline_device_stream (clip k+1's front end under clip k's synthesizer, three streams) gives every
+    clip exactly the waveform of pipeline_device at seed + k: same launches on the same data."""
+    hub, _, net_g, vc = models
+    xs = clips(3, 5.0, 700)
+    vc.seed = 40
+    outs = vc.pipeline_device_stream(hub, net_g, 0, xs, 0, "v2", 0.33)
+    torch.cuda.synchronize()
+    assert vc.seed == 40
+    for k, x in enumerate(xs):
+        vc.seed = 40 + k
+        ref = vc.pipeline_device(hub, net_g, 0, x, 0, "v2", 0.33)
+        assert outs[k].shape == ref.shape
+        assert torch.equal(outs[k], ref), (k, (outs[k] - ref).abs().max().item())
+    vc.seed = 0
+    vc.check_errors()
