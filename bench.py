@@ -267,8 +267,8 @@ def main():
         from rvc_amd.graph import ClipGraph
         clip_graph = ClipGraph(vc, hub, net_g, 0, audio_dev.numel(), 0, "v2", 0.33, index, args.index_rate, args.f0)
 
-    if args.graph or args.batch > 1:
-        args.stream = False  # the graph replays and the batched passes are their own chunk loops
+    if args.graph:
+        args.stream = False  # the graph replays are their own chunk loop
     if args.batch > 1 and (args.graph or len(clips) % args.batch):
         raise SystemExit("bench.py: --batch needs eager mode and --chunks a multiple of it")
 
@@ -297,7 +297,8 @@ def main():
         # one stream over nsteps x chunks clips: every clip's whole pass is issued inside the call, and the
         # call returns after the last clip's output is ordered on this stream
         order = [clips[i % len(clips)] for i in range(nsteps * len(clips))]
-        outs = vc.pipeline_device_stream(hub, net_g, 0, order, 0, "v2", 0.33, index, args.index_rate, args.f0)
+        outs = vc.pipeline_device_stream(hub, net_g, 0, order, 0, "v2", 0.33, index, args.index_rate, args.f0,
+                                         batch=args.batch)
         if dist is not None:
             got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0)
             if got is not None:

@@ -976,9 +976,11 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
 
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
 void split_k(ConvParams& p, int64_t tiles, int nch) {
+    // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU
+    static const int target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
     int ks = 1;
-    if (tiles < 512 && nch >= 4) {
-        ks = (int)((512 + tiles - 1) / tiles);
+    if (tiles < target && nch >= 4) {
+        ks = (int)((target + tiles - 1) / tiles);
         if (ks > 16) ks = 16;
         if (ks > nch / 2) ks = nch / 2;
         if (ks < 1) ks = 1;

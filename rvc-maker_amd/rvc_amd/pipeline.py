@@ -214,18 +214,21 @@ class VC:
         return outs
 
     def pipeline_device_stream(self, model, net_g, sid, audios, pitch, version, protect, index=None, index_rate=0.0,
-                               f0_method="rmvpe"):
+                               f0_method="rmvpe", batch=1):
         """``pipeline_device`` over a sequence of clips (the file / chunk loops of convert.py:129-135 and
         :506-507) with clip k+1's front end -- filtfilt, f0 on the side stream, ContentVec features -- issued
         on a front stream while clip k's synthesizer runs on a back stream.  The two are independent, so the
         front end's small, latency-bound launches (the U-Net's deep levels, the BiGRU's 32 workgroups, the
         ContentVec GEMMs) fill the CUs the generator's kernels leave between blocks and launches instead of
-        running as a phase of their own.
+        running as a phase of their own.  ``batch`` > 1 runs the front end over groups of that many
+        equal-length clips at once (``pipeline_device_batch``'s batched RMVPE and ContentVec), group g+1's
+        under group g's synthesizers.
 
-        Clip k draws its noise with seed ``self.seed + k`` (as ``pipeline_device_batch``): its waveform is
-        bit-identical to ``pipeline_device`` of that clip at ``seed = self.seed + k`` -- every launch is the
-        same launch on the same data, only its stream differs.  Clips must fit one segment (N + window <=
-        t_max, 41 s; longer inputs go through ``pipeline_device``'s host quiet-point search).  Returns the
+        Clip k draws its noise with seed ``self.seed + k`` (as ``pipeline_device_batch``): at batch 1 its
+        waveform is bit-identical to ``pipeline_device`` of that clip at ``seed = self.seed + k`` -- every
+        launch is the same launch on the same data, only its stream differs (batched groups: up to the
+        batched GEMMs' split-K order, as ``pipeline_device_batch``).  Clips must fit one segment (N + window
+        <= t_max, 41 s; longer inputs go through ``pipeline_device``'s host quiet-point search).  Returns the
         list of device waveforms, ordered on the caller's current stream."""
         audios = [a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(
             self.device) for a in audios]
@@ -233,6 +236,9 @@ class VC:
             raise ValueError("pipeline_device_stream: clips of at most t_max samples (one segment each)")
         if not audios:
             return []
+        groups = [audios[i:i + max(1, batch)] for i in range(0, len(audios), max(1, batch))]
+        if any(len({a.numel() for a in g}) > 1 for g in groups):
+            raise ValueError("pipeline_device_stream: a batched group needs equal-length clips")
         dev = audios[0].device
         caller = torch.cuda.current_stream(dev)
         front, back = self._aux_stream(dev, "front"), self._aux_stream(dev, "back")
@@ -240,17 +246,26 @@ class VC:
             self._ws = torch.zeros(4, dtype=torch.int32, device=dev)
         seed0, tp = self.seed, self.t_pad_tgt
 
-        def issue_front(a):
+        def issue_front(group):
+            """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event)"""
             with torch.cuda.stream(front):
-                front.wait_stream(caller)  # the caller wrote the input on its own stream
-                a.record_stream(front)
-                xp, _ = self.filt(a.contiguous(), self.t_pad)
+                front.wait_stream(caller)  # the caller wrote the inputs on its own stream
+                for a in group:
+                    a.record_stream(front)
+                xps = [self.filt(a.contiguous(), self.t_pad)[0] for a in group]
+                xp = xps[0] if len(group) == 1 else torch.stack(xps)
                 side = self._aux_stream(dev, "fside")
                 ready = torch.cuda.Event()
                 ready.record(front)
                 with torch.cuda.stream(side):
                     side.wait_event(ready)
-                    coarse, pitchf = self.f0_device(xp, pitch, f0_method)
+                    if len(group) == 1:
+                        coarse, pitchf = self.f0_device(xp, pitch, f0_method)
+                    elif f0_method == "rmvpe":
+                        coarse, pitchf = self._rmvpe().f0_device_batch(xp, 0.03, float(pitch))
+                    else:
+                        pairs = [self.f0_device(xp[b], pitch, f0_method) for b in range(len(group))]
+                        coarse, pitchf = torch.stack([c for c, _ in pairs]), torch.stack([f for _, f in pairs])
                     f0_done = torch.cuda.Event()
                     f0_done.record(side)
                 feats = self.features_device(model, xp, version)
@@ -260,26 +275,30 @@ class VC:
                 xp.record_stream(side)
                 done = torch.cuda.Event()
                 done.record(front)
-            return (xp, coarse, pitchf, feats), done
+            if len(group) == 1:
+                return [(xp, coarse, pitchf, feats)], done
+            return [(xp[b], coarse[b], pitchf[b], feats[b]) for b in range(len(group))], done
 
         outs = []
-        nxt = issue_front(audios[0])
+        nxt = issue_front(groups[0])
         try:
-            for k in range(len(audios)):
-                (xp, coarse, pitchf, feats), done = nxt
-                if k + 1 < len(audios):
-                    nxt = issue_front(audios[k + 1])  # queued ahead of clip k's synthesizer
+            for g in range(len(groups)):
+                items, done = nxt
+                if g + 1 < len(groups):
+                    nxt = issue_front(groups[g + 1])  # queued ahead of group g's synthesizers
                 with torch.cuda.stream(back):
                     back.wait_event(done)
-                    for t in (xp, coarse, pitchf, feats):
-                        t.record_stream(back)
-                    p_len = xp.numel() // self.window
-                    self.seed = seed0 + k
-                    o = self.voice_conversion_device(model, net_g, sid, xp, coarse[:p_len], pitchf[:p_len], version,
-                                                     protect, 0, feats=feats, index=index, index_rate=index_rate)
-                    out = o[tp: o.numel() - tp]
-                    ops.peak_normalize(out, self._ws)
-                    outs.append(out)
+                    for xp, coarse, pitchf, feats in items:
+                        for t in (xp, coarse, pitchf, feats):
+                            t.record_stream(back)
+                        p_len = xp.numel() // self.window
+                        self.seed = seed0 + len(outs)
+                        o = self.voice_conversion_device(model, net_g, sid, xp, coarse[:p_len], pitchf[:p_len],
+                                                         version, protect, 0, feats=feats, index=index,
+                                                         index_rate=index_rate)
+                        out = o[tp: o.numel() - tp]
+                        ops.peak_normalize(out, self._ws)
+                        outs.append(out)
         finally:
             self.seed = seed0
         caller.wait_stream(back)

@@ -105,3 +105,22 @@ def test_stream_bit_identical_to_per_clip(models):
         assert torch.equal(outs[k], ref), (k, (outs[k] - ref).abs().max().item())
     vc.seed = 0
     vc.check_errors()
+
+
+def test_batched_stream_bit_identical_to_batch(models):
+    """pipeline_device_stream(batch=3) over 5 clips = pipeline_device_batch of groups [0:3], [3:5] (same
+    batched front-end launches, seeds self.seed + k)."""
+    hub, _, net_g, vc = models
+    xs = clips(5, 4.0, 800)
+    vc.seed = 7
+    outs = vc.pipeline_device_stream(hub, net_g, 0, xs, 0, "v2", 0.33, batch=3)
+    torch.cuda.synchronize()
+    ref = vc.pipeline_device_batch(hub, net_g, 0, xs[:3], 0, "v2", 0.33)
+    vc.seed = 10
+    ref += vc.pipeline_device_batch(hub, net_g, 0, xs[3:], 0, "v2", 0.33)
+    vc.seed = 0
+    torch.cuda.synchronize()
+    assert len(outs) == 5
+    for k in range(5):
+        assert torch.equal(outs[k], ref[k]), (k, (outs[k] - ref[k]).abs().max().item())
+    vc.check_errors()
