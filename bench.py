@@ -197,6 +197,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-call", action="store_true", help="skip the per-call comparison after a clip stream")
+    ap.add_argument("--no-roofline", action="store_true", help="skip the instrumented roofline pass (profiling)")
     # variants beyond the headline config (BASELINE configs 3/5 ingredients); defaults = configs[1]
     ap.add_argument("--sr", type=int, default=48000, choices=[32000, 40000, 48000])
     ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
@@ -332,7 +334,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     per_call = None
-    if args.stream and world == 1:
+    if args.stream and world == 1 and not args.no_per_call:
         # the same K steps as one pipeline_device call per clip, each finished before the next (the
         # reference's loop): the stream's gain over it, measured on the same box right after
         torch.cuda.synchronize()
@@ -348,7 +350,7 @@ def main():
     gathered_per_step = gathered[0] / max(args.warmup + args.steps, 1) if dist is not None else len(clips)
 
     roof = None
-    if rank == 0:
+    if rank == 0 and not args.no_roofline:
         with ConvProbe() as probe:  # one eager pass (a graph replay launches no host-side conv calls)
             vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
         n, ms, flops = probe.summary(engine=1)  # dominant family: the split-bf16 conv engine

@@ -591,289 +591,6 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
 }
 
-// Persistent form of the split-bf16 engine (no split-K, >= 2 chunks per tile): one block per CU
-// walks tiles blockIdx.x, +gridDim.x, ...  The chunk stream runs on across tiles (the loader waves
-// stage the next tile's first chunks while the current tile's last chunk computes; the compute
-// waves' weight ring prefetches across the tile seam), and the epilogue moves off the compute
-// waves: at a tile's last k-step they drop the raw accumulators into an LDS tile (Cbuf) and go on
-// to the next tile, while the loader waves -- otherwise idle between two chunk stagings -- apply
-// bias / activation / residual / accumulate and store the tile with row-contiguous accesses.
-//
-// Barrier schedule (one per chunk, as the non-persistent kernel): compute chunk g runs between
-// barriers g and g+1 on X buffer g&1; the loaders stage chunk g+1 into buffer (g+1)&1 in the same
-// interval.  A tile whose last chunk is g publishes Cbuf at barrier g+1; the loaders consume it
-// before barrier g+2; the next Cbuf write comes after barrier g+nch >= g+2 (nch >= 2).
-template <int FM, int FN, int WM, int WN, int X6_NI, int NP>
-__global__ __launch_bounds__(512) void conv_x6p_kernel(ConvParams p, int ntiles, int gx, int gy) {
-    static_assert(WM * WN == 4, "4 compute waves");
-    constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
-    constexpr int BM = 16 * FM * WM;
-    constexpr int BN = 16 * FN * WN;
-    constexpr int CST = BN + 4;  // Cbuf row stride (floats)
-    constexpr int EPT = BM * BN / 256;  // epilogue elements per loader thread
-    static_assert(256 % BN == 0, "epilogue: a loader thread owns one column");
-    extern __shared__ uint4 xs[];  // [2][span][NPL][4] X buffers, then Cbuf [BM][CST] f32
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int K = p.K, span = p.span, nch = p.wx_nch, nmf = p.wx_nmf;
-    const int bufsz = NPL * span * 4;
-    float* cbuf = reinterpret_cast<float*>(xs + 2 * bufsz);
-    const int Cog = (int)p.Co, Cig = (int)p.Ci;
-    const int ntm = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // my tiles
-    const int G = ntm * nch;  // my chunks
-    // tile k of this block -> (column tile, row tile, batch*phase)
-    auto tile = [&](int k, int& nx, int& my, int& zb) __attribute__((always_inline)) {
-        const int tt = (int)blockIdx.x + k * (int)gridDim.x;
-        nx = tt % gx;
-        const int r = tt / gx;
-        my = r % gy;
-        zb = r / gy;
-    };
-    auto rots = [&](int nx, int& rt, int& rc) __attribute__((always_inline)) {
-        const int rseed = p.rot ? (nx >> 3) : 0;
-        rt = rseed % K;
-        rc = (rseed / K) % nch;
-    };
-
-    if (wave >= 4) {
-        // ---------------- loader waves: chunk staging + the epilogue of the previous tile
-        const int ltid = tid - 256;
-        const int lin = (int)p.Lin;
-        int ipos[X6_NI], ig8[X6_NI];
-#pragma unroll
-        for (int it = 0; it < X6_NI; ++it) {
-            const int idx = ltid + 256 * it;
-            const int g8 = idx / span;
-            ig8[it] = g8 < 4 ? g8 : 3;
-            ipos[it] = idx - g8 * span;
-        }
-        // chunk g -> (x batch base, first input position, physical chunk)
-        auto chunk = [&](int g, const float*& xb, int& base, int& ch) __attribute__((always_inline)) {
-            g = g < G ? g : G - 1;
-            const int k = g / nch, i = g - k * nch;
-            int nx, my, zb, rt, rc;
-            tile(k, nx, my, zb);
-            rots(nx, rt, rc);
-            xb = p.x + (int64_t)(zb / p.nphase) * p.x_bstride;
-            base = nx * BN - p.pad;
-            ch = (i + rc) % nch;
-        };
-        float xr[2][X6_NI][8];
-        auto xload = [&](int g, float (&r)[X6_NI][8]) __attribute__((always_inline)) {
-            const float* xb;
-            int base, ch;
-            chunk(g, xb, base, ch);
-#pragma unroll
-            for (int it = 0; it < X6_NI; ++it) {
-                const int q = base + ipos[it];
-                const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    int c = ch * 32 + ig8[it] * 8 + e;
-                    c = c < Cig ? c : Cig - 1;
-                    r[it][e] = xb[(int64_t)c * lin + qc];
-                }
-            }
-        };
-        auto xstore = [&](int g, const float (&r)[X6_NI][8], uint4* dst) __attribute__((always_inline)) {
-            const float* xb;
-            int base, ch;
-            chunk(g, xb, base, ch);
-#pragma unroll
-            for (int it = 0; it < X6_NI; ++it) {
-                if (ltid + 256 * it < 4 * span) {
-                    const int q = base + ipos[it];
-                    const bool qok = q >= 0 && q < lin;
-                    uint32_t hw[4], mw[4], lw[4];
-#pragma unroll
-                    for (int e2 = 0; e2 < 4; ++e2) {
-                        uint32_t h2[2], m2[2], l2[2];
-#pragma unroll
-                        for (int u = 0; u < 2; ++u) {
-                            const int e = 2 * e2 + u;
-                            const bool ok = qok && ch * 32 + ig8[it] * 8 + e < Cig;
-                            float v = r[it][e] * p.in_scale;
-                            if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
-                            split3(ok ? v : 0.f, h2[u], m2[u], l2[u]);
-                        }
-                        hw[e2] = h2[0] | (h2[1] << 16);
-                        mw[e2] = m2[0] | (m2[1] << 16);
-                        lw[e2] = l2[0] | (l2[1] << 16);
-                    }
-                    const int pos = ipos[it];
-                    dst[x_slot<NPL>(pos, 0, ig8[it])] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-                    if constexpr (NPL >= 2) dst[x_slot<NPL>(pos, 1, ig8[it])] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
-                    if constexpr (NPL >= 3) dst[x_slot<NPL>(pos, 2, ig8[it])] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-                }
-            }
-        };
-        // epilogue of tile k from Cbuf: row-contiguous (a wave covers 64 consecutive columns of a row);
-        // every load is issued from a clamped address before any arithmetic
-        auto epilogue_act = [&](int k, auto actc) __attribute__((always_inline)) {
-            constexpr int ACT = decltype(actc)::value;
-            int nx, my, zb;
-            tile(k, nx, my, zb);
-            const int phase = zb % p.nphase, b = zb / p.nphase;
-            const int m0g = my * BM;
-            const int64_t n0 = (int64_t)nx * BN;
-            float* yb = p.y + (int64_t)b * p.y_bstride;
-            const float* rb = p.res ? p.res + (int64_t)b * p.res_bstride : nullptr;
-            const int Lo = (int)p.Lout;
-            // thread -> one column n (256 % BN == 0) and rows m = it * RPI + m1
-            constexpr int RPI = 256 / BN;
-            const int n = ltid % BN, m1 = ltid / BN;
-            const int tcol = out_pos(p, n0 + n, phase);
-            const int tc = tcol >= 0 ? tcol : 0;
-            // in passes of at most 32 rows per thread (register budget); each pass issues all of its
-            // residual loads before any use
-            constexpr int EP = EPT < 32 ? EPT : 32;
-#pragma unroll 1
-            for (int it0 = 0; it0 < EPT; it0 += EP) {
-            float v[EP];
-#pragma unroll
-            for (int ii = 0; ii < EP; ++ii) {
-                const int o = min(m0g + (it0 + ii) * RPI + m1, Cog - 1) * Lo + tc;
-                v[ii] = (rb ? rb[o] : 0.f) + (p.accumulate ? yb[o] : 0.f);
-            }
-#pragma unroll
-            for (int ii = 0; ii < EP; ++ii) {
-                const int it = it0 + ii;
-                const int m = it * RPI + m1;
-                const int mr = min(m0g + m, Cog - 1);
-                float c = cbuf[m * CST + n];
-                if (p.bias) c += p.bias[mr];
-                if (p.bias2) c += p.bias2[mr];
-                c = act_apply(c, ACT, p.out_slope) * p.out_scale + v[ii];
-                if (m0g + m < Cog && tcol >= 0) yb[mr * Lo + tcol] = c;
-                else if (m0g + m < Cog && tcol <= -2) yb[mr * Lo + (-tcol - 2)] = 0.f;  // 2-D border cell
-            }
-            }
-        };
-        auto epilogue = [&](int k) __attribute__((always_inline)) {  // activation dispatched once per tile
-            switch (p.out_act) {
-                case RVC_ACT_LRELU: epilogue_act(k, std::integral_constant<int, RVC_ACT_LRELU>{}); break;
-                case RVC_ACT_RELU: epilogue_act(k, std::integral_constant<int, RVC_ACT_RELU>{}); break;
-                case RVC_ACT_TANH: epilogue_act(k, std::integral_constant<int, RVC_ACT_TANH>{}); break;
-                case RVC_ACT_GELU: epilogue_act(k, std::integral_constant<int, RVC_ACT_GELU>{}); break;
-                case RVC_ACT_SIGMOID: epilogue_act(k, std::integral_constant<int, RVC_ACT_SIGMOID>{}); break;
-                case RVC_ACT_LOGCLAMP: epilogue_act(k, std::integral_constant<int, RVC_ACT_LOGCLAMP>{}); break;
-                default: epilogue_act(k, std::integral_constant<int, RVC_ACT_NONE>{}); break;
-            }
-        };
-        xload(0, xr[0]);
-        xload(1, xr[1]);
-        xstore(0, xr[0], xs);
-        __syncthreads();  // barrier 0
-        auto iter = [&](int g, float (&nxt)[X6_NI][8], float (&fre)[X6_NI][8]) __attribute__((always_inline)) {
-            xload(g + 2, fre);
-            if (g + 1 < G) xstore(g + 1, nxt, xs + ((g + 1) & 1) * bufsz);
-            if (g > 0 && g % nch == 0) epilogue(g / nch - 1);
-            __syncthreads();  // barrier g + 1
-        };
-        for (int g = 0; g < G; g += 2) {
-            iter(g, xr[1], xr[0]);
-            if (g + 1 < G) iter(g + 1, xr[0], xr[1]);
-        }
-        epilogue(ntm - 1);
-        return;
-    }
-
-    // ---------------- compute waves
-    const int wm = wave / WN, wn = wave % WN;
-    const int SPT = nch * K;  // k-steps per tile
-    const int S_end = ntm * SPT;
-    // global k-step S -> (tile, chunk-in-tile i, physical chunk, physical tap, tap-in-chunk tl)
-    auto kstep = [&](int S, int& k, int& i, int& ch, int& t, int& tl) __attribute__((always_inline)) {
-        k = S / SPT;
-        const int sl = S - k * SPT;
-        i = sl / K;
-        tl = sl - i * K;
-        int nx, my, zb, rt, rc;
-        tile(k, nx, my, zb);
-        rots(nx, rt, rc);
-        ch = (i + rc) % nch;
-        t = tl + rt < K ? tl + rt : tl + rt - K;
-    };
-    auto aload = [&](int S, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
-        int k, i, ch, t, tl;
-        kstep(S, k, i, ch, t, tl);
-        int nx, my, zb;
-        tile(k, nx, my, zb);
-        const int phase = zb % p.nphase;
-        const int mf0 = my * BM / 16 + wm * FM;
-        const int frag0 = __builtin_amdgcn_readfirstlane(((phase * K + t) * nch + ch) * nmf + mf0);
-        const uint4* src = p.wx + (int64_t)frag0 * 3 * 64;
-#pragma unroll
-        for (int i2 = 0; i2 < FM; ++i2)
-#pragma unroll
-            for (int q = 0; q < NPL; ++q) a[q][i2] = src[(i2 * 3 + q) * 64 + lane];
-    };
-    floatx4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int ln = lane & 15, lg = lane >> 4;
-    const int pb = wn * 16 * FN + ln;
-    auto compute = [&](int t, const uint4* xbuf, const uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
-        const int tof = tap_off(p, t);
-        auto bload = [&](int j, uint4 (&bq)[NPL]) __attribute__((always_inline)) {
-            const int pos = pb + 16 * j + tof;
-#pragma unroll
-            for (int q = 0; q < NPL; ++q) bq[q] = xbuf[x_slot<NPL>(pos, q, lg)];
-        };
-        uint4 bb[2][NPL];
-        bload(0, bb[0]);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            if (j + 1 < FN) bload(j + 1, bb[(j + 1) & 1]);
-            const uint4 (&bq)[NPL] = bb[j & 1];
-            constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
-            constexpr int PB[6] = {0, 1, 0, 2, 1, 0};
-#pragma unroll
-            for (int ps = 0; ps < NP; ++ps)
-#pragma unroll
-                for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
-        }
-    };
-    constexpr int PD_FIT = 24 / (NPL * FM) - 1;
-    constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > 4 ? 4 : PD_FIT);
-    constexpr int NB = PD + 1;
-    uint4 abuf[NB][NPL][FM];
-#pragma unroll
-    for (int i = 0; i < PD; ++i)
-        if (i < S_end) aload(i, abuf[i]);
-    __syncthreads();  // barrier 0: chunk 0 staged
-    const int lr = lg * 4;
-    for (int S0 = 0; S0 < S_end; S0 += NB) {
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int S = S0 + u;
-            if (S < S_end) {
-                int k, i, ch, t, tl;
-                kstep(S, k, i, ch, t, tl);
-                if (S + PD < S_end) aload(S + PD, abuf[(u + PD) % NB]);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(t, xs + ((S / K) & 1) * bufsz, abuf[u]);
-                if (tl == K - 1) {
-                    if (i == nch - 1) {  // tile done: raw accumulators -> Cbuf, then the next tile
-#pragma unroll
-                        for (int i2 = 0; i2 < FM; ++i2)
-#pragma unroll
-                            for (int j = 0; j < FN; ++j)
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) {
-                                    cbuf[(wm * 16 * FM + i2 * 16 + lr + r) * CST + wn * 16 * FN + j * 16 + ln] =
-                                        acc[i2][j][r];
-                                    acc[i2][j][r] = 0.f;
-                                }
-                    }
-                    __syncthreads();  // chunk done
-                }
-            }
-        }
-    }
-}
-
 __global__ void conv_splitk_reduce(ConvParams p) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = blockIdx.y;
@@ -905,43 +622,8 @@ void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP>), grid, blk, lds, s, p);
 }
 
-template <int FM, int FN, int WM, int WN, int NP>
-void launch_x6p_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (ncu <= 0) ncu = 256;
-    }
-    const int ntiles = (int)(grid.x * grid.y * grid.z);
-    const dim3 pg(ntiles < ncu ? ntiles : ncu);
-    if (4 * p.span <= 256 * 3)
-        hipLaunchKernelGGL((conv_x6p_kernel<FM, FN, WM, WN, 3, NP>), pg, dim3(512), lds, s, p, ntiles, (int)grid.x,
-                           (int)grid.y);
-    else
-        hipLaunchKernelGGL((conv_x6p_kernel<FM, FN, WM, WN, 6, NP>), pg, dim3(512), lds, s, p, ntiles, (int)grid.x,
-                           (int)grid.y);
-}
-
-// persistent form: whole chunks per tile (no split-K), >= 2 chunks, Cbuf beside the X buffers in LDS
-size_t x6p_lds(const ConvParams& p, int BM, int BN, size_t lds) { return lds + (size_t)BM * (BN + 4) * 4; }
-
-bool x6p_ok(const ConvParams& p, int BM, int BN, size_t lds) {
-    static const int on = getenv("RVC_X6_PERSIST") ? atoi(getenv("RVC_X6_PERSIST")) : 0;
-    return on && p.ksplit == 1 && p.stride == 1 && p.wx_nch >= 2 && x6p_lds(p, BM, BN, lds) <= 160 * 1024;
-}
-
 template <int FM, int FN, int WM, int WN>
 hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
-    if constexpr (WM * WN == 4) if (x6p_ok(p, BM, BN, lds)) {
-        const size_t l2 = x6p_lds(p, BM, BN, lds);
-        if (p.wx_passes == 1) launch_x6p_np<FM, FN, WM, WN, 1>(p, grid, l2, s);
-        else if (p.wx_passes == 3) launch_x6p_np<FM, FN, WM, WN, 3>(p, grid, l2, s);
-        else launch_x6p_np<FM, FN, WM, WN, 6>(p, grid, l2, s);
-        return hipGetLastError();
-    }
     if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
     else if (p.wx_passes == 3) launch_x6_np<FM, FN, WM, WN, 3>(p, grid, lds, s);
     else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);

@@ -214,7 +214,7 @@ class VC:
         return outs
 
     def pipeline_device_stream(self, model, net_g, sid, audios, pitch, version, protect, index=None, index_rate=0.0,
-                               f0_method="rmvpe", batch=1):
+                               f0_method="rmvpe", batch=1, events=None):
         """``pipeline_device`` over a sequence of clips (the file / chunk loops of convert.py:129-135 and
         :506-507) with clip k+1's front end -- filtfilt, f0 on the side stream, ContentVec features -- issued
         on a front stream while clip k's synthesizer runs on a back stream.  The two are independent, so the
@@ -229,7 +229,15 @@ class VC:
         launch is the same launch on the same data, only its stream differs (batched groups: up to the
         batched GEMMs' split-K order, as ``pipeline_device_batch``).  Clips must fit one segment (N + window
         <= t_max, 41 s; longer inputs go through ``pipeline_device``'s host quiet-point search).  Returns the
-        list of device waveforms, ordered on the caller's current stream."""
+        list of device waveforms, ordered on the caller's current stream.  ``events`` (a list) collects
+        timing events (role, group, torch.cuda.Event) at each group's front / back start and end."""
+
+        def mark(role, g, stream):
+            if events is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(stream)
+                events.append((role, g, ev))
+
         audios = [a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(
             self.device) for a in audios]
         if any(a.numel() + self.window > self.t_max for a in audios):
@@ -246,10 +254,11 @@ class VC:
             self._ws = torch.zeros(4, dtype=torch.int32, device=dev)
         seed0, tp = self.seed, self.t_pad_tgt
 
-        def issue_front(group):
+        def issue_front(group, g):
             """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event)"""
             with torch.cuda.stream(front):
                 front.wait_stream(caller)  # the caller wrote the inputs on its own stream
+                mark("front_start", g, front)
                 for a in group:
                     a.record_stream(front)
                 xps = [self.filt(a.contiguous(), self.t_pad)[0] for a in group]
@@ -275,19 +284,21 @@ class VC:
                 xp.record_stream(side)
                 done = torch.cuda.Event()
                 done.record(front)
+                mark("front_end", g, front)
             if len(group) == 1:
                 return [(xp, coarse, pitchf, feats)], done
             return [(xp[b], coarse[b], pitchf[b], feats[b]) for b in range(len(group))], done
 
         outs = []
-        nxt = issue_front(groups[0])
+        nxt = issue_front(groups[0], 0)
         try:
             for g in range(len(groups)):
                 items, done = nxt
                 if g + 1 < len(groups):
-                    nxt = issue_front(groups[g + 1])  # queued ahead of group g's synthesizers
+                    nxt = issue_front(groups[g + 1], g + 1)  # queued ahead of group g's synthesizers
                 with torch.cuda.stream(back):
                     back.wait_event(done)
+                    mark("back_start", g, back)
                     for xp, coarse, pitchf, feats in items:
                         for t in (xp, coarse, pitchf, feats):
                             t.record_stream(back)
@@ -299,6 +310,7 @@ class VC:
                         out = o[tp: o.numel() - tp]
                         ops.peak_normalize(out, self._ws)
                         outs.append(out)
+                    mark("back_end", g, back)
         finally:
             self.seed = seed0
         caller.wait_stream(back)
