@@ -35,7 +35,10 @@ import torch  # noqa: E402
 METRIC = "audio-seconds/sec/GPU (xRT) end-to-end VC, 48k v2; 1/2/4/8 GPU scaling"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 PEAK_X6_TFLOPS = 2500.0 / 6  # bf16 dense MFMA peak (~2.5 PF) over the six split-bf16 passes per f32 product
-DTYPES = {"fp32": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
+DTYPES = {"fp32": "f32-equivalent (split-bf16 6-pass MFMA; split-fp16 3-pass MFMA for k >= 7 convs and ResBlock "
+                  "pairs; f32 accumulate)",
+          "fp32x6": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
+          "f16x3": "f32-equivalent (split-fp16 3-pass MFMA convs, power-of-2 scaled 22-bit operands, f32 accumulate)",
           "bf16x3": "bf16x3 (3-pass split-bf16 MFMA convs, f32 accumulate; f32 elsewhere)",
           "bf16": "bf16 (bf16-operand MFMA convs, f32 accumulate; f32 elsewhere)"}
 
@@ -202,7 +205,7 @@ def main():
     # variants beyond the headline config (BASELINE configs 3/5 ingredients); defaults = configs[1]
     ap.add_argument("--sr", type=int, default=48000, choices=[32000, 40000, 48000])
     ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"],
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32x6", "f16x3", "bf16x3", "bf16"],
                     help="split-bf16 conv engine arithmetic: 6 / 3 / 1 bf16 MFMA passes per product")
     ap.add_argument("--chunks", type=int, default=1,
                     help="clips per GPU per step (BASELINE configs[2]: 64 x 10 s chunks; each a distinct clip)")
@@ -248,8 +251,8 @@ def main():
     from rvc_amd import ops, synthetic
     from rvc_amd.shard import gather_waveforms
     ops.set_precision(args.precision)
-    npass = ops.PASSES[args.precision]
-    peak = 2500.0 / npass  # bf16 dense MFMA peak over the passes per product
+    npass = 3 if ops.PASSES[args.precision] == ops.F16X3 else ops.PASSES[args.precision]
+    peak = 2500.0 / npass  # bf16 / fp16 dense MFMA peak over the passes per product
     vc, hub, net_g = build_models(dev, sr=args.sr)
     index = None
     if args.index_rate > 0:

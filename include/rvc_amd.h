@@ -61,6 +61,8 @@ int rvc_version(void);
  *   y[b][m][t] = v  or  y[b][m][t] += v     (accumulate),   t = col*ostride + ooffset + phase
  *   pre(v) = in_act(v * in_scale)
  */
+#define RVC_ARITH_F16X3 16 /* rvc_conv1d_args.wx_passes / rvc_resblock_args.passes: split-fp16, 3 passes */
+
 typedef struct rvc_conv1d_args {
     const float* x;    /* [B][Ci][Lin] with batch stride x_bstride           */
     const float* w;    /* KM packed: [nphase][groups][Ci/g*K][Co/g]            */
@@ -85,7 +87,10 @@ typedef struct rvc_conv1d_args {
        rvc_conv1d_pack_x6 (NULL = f32 MFMA engine).  Used for stride-1, ungrouped, 1-D convs;
        other shapes ignore it.  wx_nmf = its padded 16-row fragment count.
        wx_passes: bf16 MFMA passes per product -- 0 or 6 = f32-accurate (hH+hM+mH+hL+mM+lH),
-       3 = hH+hM+mH (16-bit operand mantissas), 1 = hH (bf16 operands); f32 accumulation always. */
+       3 = hH+hM+mH (16-bit operand mantissas), 1 = hH (bf16 operands); f32 accumulation always.
+       RVC_ARITH_F16X3: wx is an rvc_conv1d_pack_f16 image instead -- split-fp16 operands (per-row
+       weight and per-tile activation power-of-2 scales, 11 + 11 significant bits each), hH + hL + lH
+       on the fp16 MFMA: ~2^-20 relative per product, f32 accumulation. */
     const void* wx;
     int wx_nmf, wx_passes;
 } rvc_conv1d_args;
@@ -101,6 +106,12 @@ int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_
 int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co);
 int rvc_conv1d_pack_x6(const float* w_km, int64_t nphase, int64_t Ci, int K, int64_t Co, void* out, int* nmf_out,
                        rvc_stream_t stream);
+/* The split-fp16 image (wx with wx_passes = RVC_ARITH_F16X3): the x6 fragment layout holding the fp16 h / l
+ * planes of each output row's weights scaled by a power of 2 (max |w| below 2^14), followed by the rows'
+ * reciprocal scales (f32 [wx_nmf * 16]); rvc_conv1d_f16_bytes(...) bytes, *nmf_out as for pack_x6. */
+int64_t rvc_conv1d_f16_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co);
+int rvc_conv1d_pack_f16(const float* w_km, int64_t nphase, int64_t Ci, int K, int64_t Co, void* out, int* nmf_out,
+                        rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ fused ResBlock pair
  * One (convs1[i], convs2[i]) pair of the NSF-HiFiGAN ResBlock (residuals.py:22-44) in one launch:

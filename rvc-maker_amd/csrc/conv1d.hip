@@ -387,11 +387,17 @@ constexpr int X6_NI_MAX = 6;  // staged (position, 8-channel group) items per lo
 template <int FM, int FN, int NCW, int NP>
 constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2 : 1; }
 
-template <int FM, int FN, int WM, int WN, int X6_NI, int NP>
+// F16 (with NP = 3): the split-fp16 arithmetic (x6_common.h split2h): wx is an rvc_conv1d_pack_f16 image
+// (h / l fp16 planes of per-row-scaled weights, then the rows' reciprocal scales); the loader waves first
+// take the tile's |max| over every chunk of the block's k range (the chunks beyond the first two are
+// loaded for it alone; they stay in L2 for the staging pass), agree on a power-of-2 scale through LDS, and
+// stage the scaled activations as h / l planes; the epilogue multiplies by both reciprocal scales (exact).
+template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
     constexpr int NCW = WM * WN;  // compute waves; 4 loader waves follow them
     static_assert(NP == 6 || NP == 3 || NP == 1, "6, 3 or 1 passes");
+    static_assert(!F16 || NP == 3, "split-fp16: 3 passes");
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
@@ -412,6 +418,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     const int ch_end = min(nch, ch_beg + p.chunks_per_split);
     const int nck = ch_end - ch_beg;
     const int bufsz = NPL * span * 4;  // uint4 per buffer
+    float* tmax = reinterpret_cast<float*>(xs + 2 * bufsz);  // F16: the 4 loader waves' tile |max|
     // Blocks co-resident on one XCD (ids = x mod 8) walk the k-steps from different starting
     // (chunk, tap): in lockstep they would all read the same few weight lines, i.e. the same L2 channels.
     const int rseed = p.rot ? (int)(blockIdx.x >> 3) : 0;
@@ -450,6 +457,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 }
             }
         };
+        float sc = 1.f;  // F16: the tile's activation scale (power of 2)
         auto xstore = [&](int ch, const float (&r)[X6_NI][8], uint4* dst) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < X6_NI; ++it) {
@@ -464,7 +472,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                             const bool ok = ((iok >> it) & 1u) && ch * 32 + ig8[it] * 8 + e < Cig;
                             float v = r[it][e] * p.in_scale;
                             if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
-                            split3(ok ? v : 0.f, h2[u], m2[u], l2[u]);
+                            if constexpr (F16) split2h(ok ? v * sc : 0.f, h2[u], m2[u]);
+                            else split3(ok ? v : 0.f, h2[u], m2[u], l2[u]);
                         }
                         hw[e2] = h2[0] | (h2[1] << 16);
                         mw[e2] = m2[0] | (m2[1] << 16);
@@ -478,8 +487,33 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             }
         };
         // prologue: chunk 0 -> LDS buffer 0, chunk 1 in flight
-        xload(pchunk(0), xr[0]);
-        xload(pchunk(1), xr[1]);
+        if constexpr (F16) {
+            // tile |max| over the raw loads (clamped addresses read real elements of x, and lrelu only
+            // shrinks: an upper bound of |pre(x)| over the staged tile); chunks 0 and 1 are loaded last and kept
+            auto rmax = [&](const float (&r)[X6_NI][8]) __attribute__((always_inline)) {
+                float m = 0.f;
+#pragma unroll
+                for (int it = 0; it < X6_NI; ++it)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(r[it][e]));
+                return m;
+            };
+            float am = 0.f;
+            for (int i = 2; i < nck; i += 2) {
+                xload(pchunk(i), xr[0]);
+                xload(pchunk(i + 1 < nck ? i + 1 : i), xr[1]);
+                am = fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])));
+            }
+            xload(pchunk(0), xr[0]);
+            xload(pchunk(1), xr[1]);
+            am = wave_max(fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])))) * fabsf(p.in_scale);
+            if (lane == 0) tmax[wave - NCW] = am;
+            __syncthreads();  // tile max published
+            sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+        } else {
+            xload(pchunk(0), xr[0]);
+            xload(pchunk(1), xr[1]);
+        }
         xstore(pchunk(0), xr[0], xs);
         __syncthreads();
         // iteration i (chunk ch_beg + i computing): regs slot (i+1)&1 holds chunk i+1; slot i&1 is free
@@ -552,7 +586,10 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
 #pragma unroll
             for (int ps = 0; ps < NP; ++ps)
 #pragma unroll
-                for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                for (int i = 0; i < FM; ++i) {
+                    if constexpr (F16) acc[i][j] = mfma_f16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                    else acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                }
         }
     };
     // Weight fragments are prefetched PD k-steps ahead through a ring of NB = PD + 1 register buffers
@@ -569,6 +606,11 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
 #pragma unroll
     for (int i = 0; i < PD; ++i)
         if (s_beg + i < s_end) aload(s_beg + i, abuf[i]);
+    float tile_rs = 1.f;
+    if constexpr (F16) {
+        __syncthreads();  // tile max published by the loaders
+        tile_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+    }
     __syncthreads();  // chunk 0 staged
     for (int s0 = s_beg; s0 < s_end; s0 += NB) {
 #pragma unroll
@@ -587,6 +629,19 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     if (p.dbg & 1) {
         if (acc[0][0][0] == 1234.5f) p.y[lane] = acc[FM - 1][FN - 1][3];  // keep the loop live
         return;
+    }
+    if constexpr (F16) {
+        // undo both scales: row m's reciprocal weight scale (stored after the image) x the tile's (exact:
+        // powers of 2), before split-K partials or the epilogue see the sums
+        const float* rs = reinterpret_cast<const float*>(p.wx + (int64_t)p.nphase * K * nch * nmf * 3 * 64);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float f = rs[m0g + wm * 16 * FM + i * 16 + lg * 4 + r] * tile_rs;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j][r] *= f;
+            }
     }
     conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
 }
@@ -614,17 +669,18 @@ hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int FM, int FN, int WM, int WN, int NP>
+template <int FM, int FN, int WM, int WN, int NP, bool F16 = false>
 void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     // loader items per thread sized to the staged span (unused items would still issue loads)
     const dim3 blk(64 * (WM * WN + 4));
-    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP>), grid, blk, lds, s, p);
+    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16>), grid, blk, lds, s, p);
 }
 
 template <int FM, int FN, int WM, int WN>
 hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
+    if (p.wx_passes == RVC_ARITH_F16X3) launch_x6_np<FM, FN, WM, WN, 3, true>(p, grid, lds, s);
+    else if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
     else if (p.wx_passes == 3) launch_x6_np<FM, FN, WM, WN, 3>(p, grid, lds, s);
     else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);
     return hipGetLastError();
@@ -692,7 +748,7 @@ bool x6_eligible(const rvc_conv1d_args* a) {
            a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= X6_K_MAX &&
            (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
            (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 || a->wx_passes == 3 ||
-                                                a->wx_passes == 1);
+                                                a->wx_passes == 1 || a->wx_passes == RVC_ARITH_F16X3);
 }
 
 int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& lds) {
@@ -737,7 +793,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
         const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
         split_k(p, tiles, p.wx_nch);
-        lds = (size_t)2 * (p.wx_passes == 6 ? 3 : (p.wx_passes == 3 ? 2 : 1)) * p.span * 64;
+        lds = (size_t)2 * (p.wx_passes == 6 ? 3 : (p.wx_passes == 1 ? 1 : 2)) * p.span * 64 + 16;  // + F16 tile max
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         return RVC_OK;
@@ -812,6 +868,48 @@ __global__ __launch_bounds__(256) void pack_x6_kernel(const float* w, int64_t to
 
 int64_t x6_nmf(int64_t Co) { return (Co + 127) / 128 * 8; }
 
+// Split-fp16 image: per output row m, the power-of-2 scale 2^E_m that maps max |w[.][m]| (over every
+// phase, input channel and tap) below 2^14; rs[m] = 2^-E_m.
+__global__ __launch_bounds__(256) void rowscale_f16_kernel(const float* w, int64_t nrow, int Co, int npad, float* rs) {
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= npad) return;
+    float am = 0.f;
+    if (m < Co)
+        for (int64_t i = 0; i < nrow; ++i) am = fmaxf(am, fabsf(w[i * Co + m]));
+    rs[m] = ldexpf(1.f, -f16_exp(am));
+}
+
+// KM weights -> the x6 fragment layout [nphase][K][nch][nmf][3][64] x 16 B with plane 0 = fp16 h and
+// plane 1 = fp16 l of w[.][m] / rs[m] (plane 2 zero: same strides as the bf16 image)
+__global__ __launch_bounds__(256) void pack_f16_kernel(const float* w, int64_t total, int Ci, int K, int Co, int nch,
+                                                       int nmf, const float* rs, uint4* out) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    int64_t r = idx;
+    const int lane = (int)(r % 64); r /= 64;
+    const int q = (int)(r % 3); r /= 3;
+    const int mf = (int)(r % nmf); r /= nmf;
+    const int ch = (int)(r % nch); r /= nch;
+    const int t = (int)(r % K); r /= K;
+    const int64_t ph = r;
+    const int m = mf * 16 + (lane & 15);
+    uint32_t wd[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+        uint32_t hv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = ch * 32 + 8 * (lane >> 4) + 2 * e2 + u;
+            const float v = (c < Ci && m < Co) ? w[((ph * Ci + c) * K + t) * Co + m] / rs[m] : 0.f;
+            uint32_t h, l;
+            split2h(v, h, l);
+            hv[u] = q == 0 ? h : (q == 1 ? l : 0u);
+        }
+        wd[e2] = hv[0] | (hv[1] << 16);
+    }
+    out[idx] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+}
+
 }  // namespace
 
 extern "C" int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co) {
@@ -826,6 +924,27 @@ extern "C" int rvc_conv1d_pack_x6(const float* w_km, int64_t nphase, int64_t Ci,
     const int64_t total = nphase * K * nch * nmf * 3 * 64;
     hipLaunchKernelGGL(pack_x6_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, w_km, total,
                        (int)Ci, K, (int)Co, nch, nmf, (uint4*)out);
+    RVC_HIP(hipGetLastError());
+    *nmf_out = nmf;
+    return RVC_OK;
+}
+
+extern "C" int64_t rvc_conv1d_f16_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co) {
+    if (nphase <= 0 || Ci <= 0 || K <= 0 || Co <= 0) return -1;
+    return nphase * K * ((Ci + 31) / 32) * x6_nmf(Co) * 3 * 64 * 16 + x6_nmf(Co) * 16 * 4;
+}
+
+extern "C" int rvc_conv1d_pack_f16(const float* w_km, int64_t nphase, int64_t Ci, int K, int64_t Co, void* out,
+                                   int* nmf_out, rvc_stream_t stream) {
+    RVC_CHECK_ARG(w_km && out && nmf_out && nphase > 0 && Ci > 0 && K > 0 && Co > 0, "pack_f16: bad args");
+    const int nch = (int)((Ci + 31) / 32), nmf = (int)x6_nmf(Co);
+    const int64_t total = nphase * K * nch * nmf * 3 * 64;
+    float* rs = reinterpret_cast<float*>(reinterpret_cast<uint4*>(out) + total);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(rowscale_f16_kernel, dim3(cdiv(nmf * 16, 256)), dim3(256), 0, s, w_km, nphase * Ci * K, (int)Co,
+                       nmf * 16, rs);
+    hipLaunchKernelGGL(pack_f16_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, w_km, total, (int)Ci, K, (int)Co, nch,
+                       nmf, (const float*)rs, (uint4*)out);
     RVC_HIP(hipGetLastError());
     *nmf_out = nmf;
     return RVC_OK;

@@ -64,12 +64,17 @@ size_t rb_lds_bytes(int K, int dil) {
     using G = RbGeom<C>;
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     const int Wx = G::TW + (K - 1) * dil;
-    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (size_t)C * G::RSTR * 4;
+    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (size_t)C * G::RSTR * 4 + 64;  // + split-fp16 scale slots
 }
 
-template <int C, int NP>
+// F16 (with NP = 3): split-fp16 operands (x6_common.h split2h).  The loader waves take each staged x tile's
+// |max| (they hold the whole tile in registers) and publish it per wave in LDS (slots by tile parity); c1's
+// epilogue takes the T tile's |max| over the 8 compute waves (one extra barrier per tile, B_T) before
+// splitting T; the c1 / c2 epilogues undo the weight-row and tile scales (powers of 2: exact).
+template <int C, int NP, bool F16>
 __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     using G = RbGeom<C>;
+    static_assert(!F16 || NP == 3, "split-fp16: 3 passes");
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int N = G::N, TW = G::TW, NCH = G::NCH, NF1 = G::NF1, NF2 = G::NF2, RSTR = G::RSTR;
     constexpr int FM = RB_FM, FN = RB_FN;
@@ -81,6 +86,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     uint4* Xs = lds;                          // [NCH][Wx][NPL][4]
     uint4* Ts = Xs + NCH * Wx * NPL * 4;      // [NCH][TW][NPL][4]
     float* Rs = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [C][RSTR]
+    float* xmax = Rs + C * RSTR;  // F16: [2 tile parities][4 loader waves] x tile |max|
+    float* tmaxs = xmax + 8;      // F16: [8 compute waves] T tile |max|
     const int ntiles = (L + N - 1) / N;
     const int my_n = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -113,6 +120,20 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                 for (int e = 0; e < 8; ++e) xr[it][e] = src[(int64_t)e * L];
             }
         };
+        float sc = 1.f;  // F16: the staged tile's activation scale
+        auto publish_max = [&](int par) __attribute__((always_inline)) {  // F16: this wave's |max| of the tile
+            float m = 0.f;
+#pragma unroll
+            for (int it = 0; it < G::NI; ++it)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(xr[it][e]));
+            m = wave_max(m);
+            if (lane == 0) xmax[par * 4 + wave - 8] = m;
+        };
+        auto take_scale = [&](int par) __attribute__((always_inline)) {
+            sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(xmax[par * 4], xmax[par * 4 + 1]),
+                                           fmaxf(xmax[par * 4 + 2], xmax[par * 4 + 3]))));
+        };
         auto xstore = [&](int tile) __attribute__((always_inline)) {
             const int base = tile * N - H;
 #pragma unroll
@@ -129,7 +150,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #pragma unroll
                         for (int u = 0; u < 2; ++u) {
                             const float v = ok ? xr[it][2 * e2 + u] : 0.f;
-                            split3(v >= 0.f ? v : v * p.slope, h2[u], m2[u], l2[u]);
+                            if constexpr (F16) split2h((v >= 0.f ? v : v * p.slope) * sc, h2[u], m2[u]);
+                            else split3(v >= 0.f ? v : v * p.slope, h2[u], m2[u], l2[u]);
                         }
                         hw[e2] = h2[0] | (h2[1] << 16);
                         mw[e2] = m2[0] | (m2[1] << 16);
@@ -156,16 +178,24 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                 }
             }
         };
-        if (my_n > 0) {
-            xload(blockIdx.x);
-            xstore(blockIdx.x);
+        if (my_n > 0) xload(blockIdx.x);
+        if constexpr (F16) {
+            if (my_n > 0) publish_max(0);
+            __syncthreads();  // B_pre: tile 0's x max published
+            take_scale(0);
         }
+        if (my_n > 0) xstore(blockIdx.x);
         for (int k = 0; k < my_n; ++k) {
             __syncthreads();  // S0(k): X(k) staged; R free
             rstore();         // R(k) from the registers still holding tile k
             const bool more = k + 1 < my_n;
             if (more) xload(blockIdx.x + (k + 1) * gridDim.x);
+            if constexpr (F16) {
+                __syncthreads();  // B_T(k): the compute waves' T max (c1 epilogue)
+                if (more) publish_max((k + 1) & 1);
+            }
             __syncthreads();  // S1(k): c1 of tile k done -> X free
+            if constexpr (F16) take_scale((k + 1) & 1);
             if (more) xstore(blockIdx.x + (k + 1) * gridDim.x);
         }
         return;
@@ -211,7 +241,10 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #pragma unroll
                 for (int ps = 0; ps < NP; ++ps)
 #pragma unroll
-                    for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                    for (int i = 0; i < FM; ++i) {
+                        if constexpr (F16) acc[i][j] = mfma_f16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                        else acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                    }
             }
         }
     };
@@ -227,6 +260,11 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
         if (i < S_end) aload(i, abuf[i]);
     float yold[FM][FN][4];
     int n0 = 0;
+    // F16: row reciprocal scales of both images (after each image), the x tile's and T tile's reciprocals
+    const float* rs1 = reinterpret_cast<const float*>(p.w1x + (int64_t)K * NCH * p.nmf1 * 3 * 64);
+    const float* rs2 = reinterpret_cast<const float*>(p.w2x + (int64_t)K * NCH * p.nmf2 * 3 * 64);
+    float t_rs = 1.f;
+    if constexpr (F16) __syncthreads();  // B_pre
     // One loop over the block's k-steps (tile k: c1 steps [k SPT, k SPT + SPH), c2 steps after), unrolled by
     // the ring size so every ring slot index is a compile-time constant; the tile / phase seams (barriers,
     // epilogues) are uniform branches inside it and the weight prefetch runs on across them.
@@ -253,6 +291,39 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                 else compute(Ts + ch * (TW * NPL * 4), t, NF2, abuf[u]);        // c2 over T
                 if (ss == SPH - 1) {
                     // ---- c1 epilogue: + bias, lrelu, zero outside [0, L) (c2's padding) -> T (split planes)
+                    float tsc = 1.f;
+                    if constexpr (F16) {
+                        // T values in place (unscaled), their |max| over the 8 compute waves, T's scale
+                        const int par = k & 1;
+                        const float x_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(xmax[par * 4], xmax[par * 4 + 1]),
+                                                                      fmaxf(xmax[par * 4 + 2], xmax[par * 4 + 3]))));
+                        float m = 0.f;
+#pragma unroll
+                        for (int i = 0; i < FM; ++i) {
+                            const int m0 = (rg * FM + i) * 16 + 4 * lg;
+#pragma unroll
+                            for (int j = 0; j < FN; ++j) {
+                                const int q = n0 - hk + (cg * FN + j) * 16 + ln;
+                                const bool ok = q >= 0 && q < L;
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    float v = acc[i][j][r] * (rs1[m0 + r] * x_rs) + p.b1[m0 + r];
+                                    v = v >= 0.f ? v : v * p.slope;
+                                    acc[i][j][r] = ok ? v : 0.f;
+                                    m = fmaxf(m, fabsf(acc[i][j][r]));
+                                }
+                            }
+                        }
+                        m = wave_max(m);
+                        if (lane == 0) tmaxs[wave] = m;
+                        __syncthreads();  // B_T(k)
+                        float tm = 0.f;
+#pragma unroll
+                        for (int w = 0; w < 8; ++w) tm = fmaxf(tm, tmaxs[w]);
+                        const int Et = f16_exp(tm);
+                        tsc = ldexpf(1.f, Et);
+                        t_rs = ldexpf(1.f, -Et);
+                    }
 #pragma unroll
                     for (int i = 0; i < FM; ++i) {
                         const int mf = rg * FM + i;
@@ -270,9 +341,13 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                                 uint32_t h2[2], m2[2], l2[2];
 #pragma unroll
                                 for (int e = 0; e < 2; ++e) {
-                                    float v = acc[i][j][2 * r2 + e] + p.b1[m0 + 2 * r2 + e];
-                                    v = v >= 0.f ? v : v * p.slope;
-                                    split3(ok ? v : 0.f, h2[e], m2[e], l2[e]);
+                                    if constexpr (F16) {
+                                        split2h(acc[i][j][2 * r2 + e] * tsc, h2[e], m2[e]);
+                                    } else {
+                                        float v = acc[i][j][2 * r2 + e] + p.b1[m0 + 2 * r2 + e];
+                                        v = v >= 0.f ? v : v * p.slope;
+                                        split3(ok ? v : 0.f, h2[e], m2[e], l2[e]);
+                                    }
                                 }
                                 hw[r2] = h2[0] | (h2[1] << 16);
                                 mw[r2] = m2[0] | (m2[1] << 16);
@@ -312,7 +387,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                             if (cg * FN + j < NF2 && col < N && q < L) {
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
-                                    float v = acc[i][j][r] + p.b2[m0 + r];
+                                    float v = (F16 ? acc[i][j][r] * (rs2[m0 + r] * t_rs) : acc[i][j][r]) + p.b2[m0 + r];
                                     v = v + Rs[(m0 + r) * RSTR + col];
                                     if (p.accumulate) v += RB_YREG ? yold[i][j][r] : p.y[(int64_t)(m0 + r) * L + q];
                                     p.y[(int64_t)(m0 + r) * L + q] = v;
@@ -326,7 +401,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     }
 }
 
-template <int C, int NP>
+template <int C, int NP, bool F16 = false>
 int launch_rb(const RbParams& p, hipStream_t s) {
     static int ncu = 0;
     if (!ncu) {
@@ -338,7 +413,7 @@ int launch_rb(const RbParams& p, hipStream_t s) {
     const size_t lds = rb_lds_bytes<C, NP>(p.K, p.dil);
     static bool attr = false;
     if (!attr) {
-        RVC_HIP(hipFuncSetAttribute((const void*)resblock_x6_kernel<C, NP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        RVC_HIP(hipFuncSetAttribute((const void*)resblock_x6_kernel<C, NP, F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     160 * 1024));
         attr = true;
     }
@@ -347,7 +422,7 @@ int launch_rb(const RbParams& p, hipStream_t s) {
     static const int per_cu = getenv("RVC_RB_PER_CU") ? atoi(getenv("RVC_RB_PER_CU")) : 1;
     const int ntiles = (p.L + RbGeom<C>::N - 1) / RbGeom<C>::N;
     const int nwg = ncu * (per_cu > 0 ? per_cu : 1);
-    hipLaunchKernelGGL((resblock_x6_kernel<C, NP>), dim3(ntiles < nwg ? ntiles : nwg), dim3(768), lds, s, p);
+    hipLaunchKernelGGL((resblock_x6_kernel<C, NP, F16>), dim3(ntiles < nwg ? ntiles : nwg), dim3(768), lds, s, p);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }
@@ -358,7 +433,8 @@ int rb_check(const rvc_resblock_args* a) {
     RVC_CHECK_ARG(a->L > 0 && a->C * a->L < (1ll << 31), "resblock: bad length");
     RVC_CHECK_ARG(a->K >= 1 && a->K % 2 == 1 && a->K <= 15 && a->dil >= 1 && (a->K - 1) * a->dil <= RB_MAXSPAN,
                   "resblock: odd K <= 15 with (K-1)*dil <= %d expected", RB_MAXSPAN);
-    RVC_CHECK_ARG(a->passes == 6 || a->passes == 3 || a->passes == 1, "resblock: passes must be 6, 3 or 1");
+    RVC_CHECK_ARG(a->passes == 6 || a->passes == 3 || a->passes == 1 || a->passes == RVC_ARITH_F16X3,
+                  "resblock: passes must be 6, 3, 1 or RVC_ARITH_F16X3");
     RVC_CHECK_ARG(a->nmf1 * 16 >= a->C && a->nmf2 * 16 >= a->C, "resblock: weight image too small");
     RVC_CHECK_ARG(a->x != a->y, "resblock: x and y must not alias (tiles read x halos other tiles overwrite)");
     return RVC_OK;
@@ -367,6 +443,7 @@ int rb_check(const rvc_resblock_args* a) {
 }  // namespace
 
 extern "C" int64_t rvc_resblock_lds_bytes(int64_t C, int K, int dil, int passes) {
+    if (passes == RVC_ARITH_F16X3) passes = 3;  // same planes
     if (C == 32) return passes == 6 ? rb_lds_bytes<32, 6>(K, dil) : passes == 3 ? rb_lds_bytes<32, 3>(K, dil)
                                                                                 : rb_lds_bytes<32, 1>(K, dil);
     if (C == 64) return passes == 6 ? rb_lds_bytes<64, 6>(K, dil) : passes == 3 ? rb_lds_bytes<64, 3>(K, dil)
@@ -393,10 +470,12 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     p.slope = a->slope;
     hipStream_t s = (hipStream_t)stream;
     if (a->C == 32) {
+        if (a->passes == RVC_ARITH_F16X3) return launch_rb<32, 3, true>(p, s);
         if (a->passes == 6) return launch_rb<32, 6>(p, s);
         if (a->passes == 3) return launch_rb<32, 3>(p, s);
         return launch_rb<32, 1>(p, s);
     }
+    if (a->passes == RVC_ARITH_F16X3) return launch_rb<64, 3, true>(p, s);
     if (a->passes == 6) return launch_rb<64, 6>(p, s);
     if (a->passes == 3) return launch_rb<64, 3>(p, s);
     return launch_rb<64, 1>(p, s);

@@ -4,10 +4,38 @@
 #include "rvc_common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 
 RVC_DEV floatx4 mfma_bf16(const uint4& a, const uint4& b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
+}
+
+RVC_DEV floatx4 mfma_f16(const uint4& a, const uint4& b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), c,
+                                                  0, 0, 0);
+}
+
+// Split-fp16 arithmetic (RVC_ARITH_F16X3): operands scaled by a power of 2 into fp16's range and split
+// exactly into two fp16 pieces v = h + l + r, |r| <= 2^-22 |v| (11 + 11 significant bits); the product
+// keeps hH + hL + lH (3 f16 MFMAs, f32 accumulation): ~3 x 2^-22 relative per product, below the f32
+// accumulation error of any k-sum longer than ~16 terms.  Weights are scaled per output row at pack time,
+// activations per staged tile (its |max|), both undone exactly in the epilogue.
+RVC_DEV void split2h(float v, uint32_t& h, uint32_t& l) {
+    const _Float16 hh = (_Float16)v;
+    const float r = v - (float)hh;  // exact: h is v rounded to 11 significant bits
+    const _Float16 ll = (_Float16)r;
+    h = __builtin_bit_cast(uint16_t, hh);
+    l = __builtin_bit_cast(uint16_t, ll);
+}
+
+// exponent E of the power-of-2 scale for values |v| <= amax: amax * 2^E < 2^14 (4x below fp16's 65504)
+RVC_DEV int f16_exp(float amax) {
+    if (!(amax > 0.f) || !(amax < 3.0e38f)) return 0;
+    int e;
+    (void)frexpf(amax, &e);  // amax = f 2^e, f in [0.5, 1)
+    const int E = 14 - e;
+    return E < -100 ? -100 : (E > 100 ? 100 : E);
 }
 
 // v -> (h, m, l) bf16 bit patterns, v == h + m + (exactly representable rest), l = bf16(rest)

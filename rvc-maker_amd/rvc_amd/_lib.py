@@ -69,6 +69,8 @@ SIGNATURES = {
     "rvc_conv1d_engine": [POINTER(Conv1dArgs)],
     "rvc_conv1d_x6_bytes": [c_int64, c_int64, c_int, c_int64],
     "rvc_conv1d_pack_x6": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
+    "rvc_conv1d_f16_bytes": [c_int64, c_int64, c_int, c_int64],
+    "rvc_conv1d_pack_f16": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
     "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],
     "rvc_attention": [POINTER(AttnArgs), c_void_p, c_int64, c_void_p],
     "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
@@ -124,6 +126,7 @@ SIGNATURES = {
     "rvc_denoise": [c_void_p, c_int64, POINTER(DenoiseArgs), c_void_p, c_int64, c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
+             "rvc_conv1d_f16_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}

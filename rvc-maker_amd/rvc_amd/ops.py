@@ -54,11 +54,24 @@ def pack_convT(w: torch.Tensor, u: int) -> tuple[torch.Tensor, int]:
 # Split-bf16 engine switch (the f32-MFMA engine runs when off); RVC_AMD_X6=0 disables it.
 X6 = os.environ.get("RVC_AMD_X6", "1") != "0"
 
-# Arithmetic of the split-bf16 engine (bf16 MFMA passes per product, f32 accumulation):
-#   "fp32"   6 passes, f32-accurate products (the default; BASELINE configs 1-2, 4)
-#   "bf16x3" 3 passes, 16-bit operand mantissas (~2^-16 relative per product)
+# Arithmetic of the split-operand MFMA engine (f32 accumulation always):
+#   "fp32"   f32-equivalent (the default; BASELINE configs 1-2, 4): "fp32x6" everywhere except the convs where
+#            "f16x3" measured faster -- stride-1 1-D convs with k >= 7 taps over <= 256 input channels, and the
+#            fused ResBlock pairs with k >= 7 (F16_MIX; RVC_AMD_F16MIX=0 turns it off)
+#   "fp32x6" 6 bf16 passes, f32-accurate products (~2^-22 relative per product)
+#   "f16x3"  3 fp16 passes over power-of-2-scaled 22-bit operands (~2^-20 relative per product)
+#   "bf16x3" 3 bf16 passes, 16-bit operand mantissas (~2^-16 relative per product)
 #   "bf16"   1 pass, bf16 operands (BASELINE configs 3 and 5)
-PASSES = {"fp32": 6, "bf16x3": 3, "bf16": 1}
+F16X3 = 16  # RVC_ARITH_F16X3
+PASSES = {"fp32": 6, "fp32x6": 6, "f16x3": F16X3, "bf16x3": 3, "bf16": 1}
+F16_MIX = os.environ.get("RVC_AMD_F16MIX", "1") != "0"
+
+
+def conv_passes(K, Ci, stride=1, two_d=False):
+    """The pass set a conv launch runs at under the current precision (see PASSES)."""
+    if _PRECISION == "fp32" and F16_MIX and K >= 7 and Ci <= 256 and stride == 1 and not two_d:
+        return F16X3
+    return PASSES[_PRECISION]
 _PRECISION = os.environ.get("RVC_AMD_PRECISION", "fp32")
 if _PRECISION not in PASSES:
     raise ValueError(f"RVC_AMD_PRECISION must be one of {sorted(PASSES)}")
@@ -91,20 +104,39 @@ class precision:
         set_precision(self.prev)
 
 
+class SplitImages:
+    """The two operand images of one weight for the split-operand engine: ``bf`` (rvc_conv1d_pack_x6, the
+    bf16 planes every bf16 pass count reads) and ``hf`` (rvc_conv1d_pack_f16, fp16 planes + row scales)."""
+
+    def __init__(self, bf, hf):
+        self.bf, self.hf = bf, hf
+
+    def for_passes(self, passes):
+        return self.hf if passes == F16X3 else self.bf
+
+    def data_ptr(self, passes=None):
+        return self.for_passes(PASSES[_PRECISION] if passes is None else passes).data_ptr()
+
+
 def pack_x6(w_km: torch.Tensor, nphase: int, Ci: int, K: int, Co: int):
-    """Device KM weights [nphase][Ci*K][Co] -> split-bf16 fragment image for the x6 engine
-    (rvc_conv1d_pack_x6), or (None, 0) when the engine is off."""
+    """Device KM weights [nphase][Ci*K][Co] -> (SplitImages, nmf): the split-bf16 image
+    (rvc_conv1d_pack_x6) and the split-fp16 image (rvc_conv1d_pack_f16) for the split-operand engine, or
+    (None, 0) when the engine is off."""
     if not X6:
         return None, 0
     lib = _lib.load()
-    nbytes = lib.rvc_conv1d_x6_bytes(nphase, Ci, K, Co)
-    if nbytes <= 0:
-        raise ValueError("pack_x6: bad shape")
-    out = torch.empty(nbytes, dtype=torch.uint8, device=w_km.device)
-    nmf = ctypes.c_int(0)
-    check(lib.rvc_conv1d_pack_x6(_p(w_km), nphase, Ci, K, Co, ctypes.c_void_p(out.data_ptr()), ctypes.byref(nmf),
-                                 _stream()), "conv1d_pack_x6")
-    return out, nmf.value
+    imgs = []
+    for size_fn, pack_fn in ((lib.rvc_conv1d_x6_bytes, lib.rvc_conv1d_pack_x6),
+                             (lib.rvc_conv1d_f16_bytes, lib.rvc_conv1d_pack_f16)):
+        nbytes = size_fn(nphase, Ci, K, Co)
+        if nbytes <= 0:
+            raise ValueError("pack_x6: bad shape")
+        out = torch.empty(nbytes, dtype=torch.uint8, device=w_km.device)
+        nmf = ctypes.c_int(0)
+        check(pack_fn(_p(w_km), nphase, Ci, K, Co, ctypes.c_void_p(out.data_ptr()), ctypes.byref(nmf), _stream()),
+              "conv1d_pack")
+        imgs.append(out)
+    return SplitImages(*imgs), nmf.value
 
 
 class Conv:
@@ -254,7 +286,8 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
             a.toff[i] = int(v)
     a.wrap = wrap
     if wx is not None:
-        a.wx, a.wx_nmf, a.wx_passes = ctypes.c_void_p(wx.data_ptr()), wx_nmf, PASSES[_PRECISION]
+        passes = conv_passes(K, Ci // groups, stride, toff is not None)
+        a.wx, a.wx_nmf, a.wx_passes = ctypes.c_void_p(wx.data_ptr(passes)), wx_nmf, passes
     if flops is None:
         valid = (Lout // wrap - 2) * (wrap - 2) if wrap else (ncols or Lout) * nphase
         flops = 2.0 * B * Co * Cig * K * min(valid, Lout)
@@ -271,10 +304,20 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
 
 # Fused ResBlock pairs for the 32/64-channel generator stages (RVC_AMD_FUSED_RB=0: two conv launches each)
 FUSED_RB = os.environ.get("RVC_AMD_FUSED_RB", "1") != "0"
+RB_PASSES = (6, 3, 1, F16X3)  # pass sets the fused kernel takes
+
+
+def rb_passes(K):
+    """The fused ResBlock pair's pass set under the current precision: "fp32" mixes in split-fp16 for k >= 7
+    (measured 7-8 % faster there, slower at k = 3)."""
+    if _PRECISION == "fp32" and F16_MIX and K >= 7:
+        return F16X3
+    return PASSES[_PRECISION]
 
 
 def resblock_fusable(c1: "Conv", c2: "Conv", dil: int) -> bool:
-    return (FUSED_RB and c1.wx is not None and c2.wx is not None and c1.Ci == c1.Co == c2.Ci == c2.Co
+    return (FUSED_RB and rb_passes(c1.K) in RB_PASSES and c1.wx is not None and c2.wx is not None
+            and c1.Ci == c1.Co == c2.Ci == c2.Co
             and c1.Co in (32, 64) and c1.K == c2.K and c1.K % 2 == 1 and c1.K <= 15 and (c1.K - 1) * dil <= 64)
 
 
@@ -285,11 +328,12 @@ def resblock_pair(x, y, c1: "Conv", c2: "Conv", dil: int, slope: float, accumula
         raise ValueError("resblock_pair: x, y must be distinct contiguous [C][L] buffers")
     a = _lib.ResblockArgs()
     a.x, a.y = _p(x), _p(y)
-    a.w1x, a.w2x = ctypes.c_void_p(c1.wx.data_ptr()), ctypes.c_void_p(c2.wx.data_ptr())
+    passes = rb_passes(c1.K)
+    a.w1x, a.w2x = ctypes.c_void_p(c1.wx.data_ptr(passes)), ctypes.c_void_p(c2.wx.data_ptr(passes))
     a.b1, a.b2 = _p(c1.b), _p(c2.b)
     a.C, a.L, a.K, a.dil = C, L, c1.K, dil
     a.nmf1, a.nmf2 = c1.wx_nmf, c2.wx_nmf
-    a.passes, a.accumulate, a.slope = PASSES[_PRECISION], int(bool(accumulate)), slope
+    a.passes, a.accumulate, a.slope = passes, int(bool(accumulate)), slope
     check(_lib.load().rvc_resblock_pair(ctypes.byref(a), _stream()), "resblock_pair")
     return y
 

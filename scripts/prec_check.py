@@ -22,7 +22,7 @@ for name in sys.argv[1:] or ["pipeline_48k_v2"]:
     vc = VC(sr, Config(DEV), rmvpe=RMVPEAMD(synthetic.rmvpe_state_dict(seed + 2), DEV))
     vc.noise_fn = lambda s, k, sh: torch.from_numpy(g[f"{'z' if k == 'z' else 'sine'}_noise_{s}"]).to(DEV)
     ref = g["out"].astype(np.float64)
-    for prec in ("fp32", "bf16x3", "bf16"):
+    for prec in ("fp32", "fp32x6", "f16x3", "bf16x3", "bf16"):
         with ops.precision(prec):
             out = vc.pipeline_device(hub, net_g, 0, g["audio"], float(g["pitch"]), version, float(g["protect"]))
         o = out.cpu().numpy().astype(np.float64)

@@ -266,3 +266,36 @@ def test_conv2d_bordered_image_writes_zero_border(ops, engine, Ci, Co, H, W):
     border = torch.ones(H + 2, W + 2, dtype=torch.bool)
     border[1:-1, 1:-1] = False
     assert torch.equal(o[:, border], torch.zeros(Co, int(border.sum())))
+
+
+F16_CASES = [c for c in CONV_CASES if c[6] == 1 and c[2] <= 64 and (c[3] == 1 or (c[3] == 2 and c[0] >= 32))]
+
+
+@pytest.mark.parametrize("case", F16_CASES)
+@pytest.mark.parametrize("spread", ["unit", "wide"])
+def test_conv1d_f16x3(ops, case, spread):
+    """Split-fp16 (3 fp16 MFMA passes over power-of-2-scaled 22-bit operands): error vs an f64 reference, per
+    output row, measured against the row's sum of |products| (conv(|x|, |w|): the scale of any floating-point
+    conv's error): below 2^-18 of it, and of the order of torch's own f32 conv error (<= 8x + 1e-6 of it),
+    also when channels span 1e-6..1e6 ("wide": the per-tile activation and per-row weight scales must keep
+    the small ones)."""
+    Ci, Co, K, s, d, p, g, L = case
+    x = torch.randn(Ci, L, generator=gen(11))
+    w = torch.randn(Co, Ci, K, generator=gen(12)) / math.sqrt(Ci * K)
+    b = torch.randn(Co, generator=gen(13)) * 0.1
+    if spread == "wide":
+        x = x * torch.logspace(-6, 6, Ci).unsqueeze(1)
+        w = w * torch.logspace(3, -3, Co).view(Co, 1, 1)
+    ref = F.conv1d(x.unsqueeze(0).double(), w.double(), b.double(), s, p, d)[0]
+    mag = F.conv1d(x.unsqueeze(0).double().abs(), w.double().abs(), b.double().abs(), s, p, d)[0]
+    f32 = F.conv1d(x.unsqueeze(0), w, b, s, p, d)[0].double()
+    c = ops.Conv(w, b)
+    with ops.precision("f16x3"):
+        y = c(x.to(DEV), stride=s, pad=p, dil=d)
+    assert ops.LAST_CONV_ENGINE == 1
+    y = y.cpu().double()
+    # per output row (rows differ by up to 1e6 in scale under "wide")
+    rms = lambda e: e.pow(2).mean(1).sqrt() / mag.pow(2).mean(1).sqrt().clamp_min(1e-300)  # noqa: E731
+    rel, rel32 = rms(y - ref), rms(f32 - ref)
+    assert float(rel.max()) < 2.0 ** -18, float(rel.max())
+    assert bool((rel <= 8 * rel32 + 1e-6).all()), (float(rel.max()), float(rel32.max()))

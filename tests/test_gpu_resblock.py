@@ -39,7 +39,7 @@ def torch_ref(x, w, K, d):
 
 @pytest.mark.parametrize("C", [32, 64])
 @pytest.mark.parametrize("K,d", [(3, 1), (3, 5), (7, 3), (11, 1), (11, 5)])
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32x6", "bf16x3", "bf16"])
 def test_fused_pair_bit_identical_to_two_launches(C, K, d, precision):
     w, c1, c2 = make_pair(C, K, seed=C * 100 + K * 10 + d)
     L = 5003  # several tiles and a partial one
@@ -55,7 +55,7 @@ def test_fused_pair_bit_identical_to_two_launches(C, K, d, precision):
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
     assert torch.equal(ya, yb)
-    if precision == "fp32":
+    if precision == "fp32x6":
         r = torch_ref(x.cpu(), w, K, d)
         err = (y.cpu() - r).abs().max().item()
         assert err <= 2e-5 * max(1.0, r.abs().max().item()), err
@@ -66,12 +66,15 @@ def test_fused_pair_short_and_edge_lengths(L):
     C, K, d = 32, 11, 5
     w, c1, c2 = make_pair(C, K, seed=5)
     x = torch.randn(C, L, generator=torch.Generator().manual_seed(L)).to(DEV)
-    y = torch.empty_like(x)
-    ops.resblock_pair(x, y, c1, c2, d, 0.1)
-    torch.cuda.synchronize()
     r = torch_ref(x.cpu(), w, K, d)
-    assert (y.cpu() - r).abs().max().item() <= 2e-5 * max(1.0, r.abs().max().item())
-    assert torch.equal(y, two_launch(x, c1, c2, K, d))
+    for prec in ("fp32", "fp32x6"):  # the default (split-fp16 at k = 11) and the 6-pass split-bf16 pair
+        with ops.precision(prec):
+            y = torch.empty_like(x)
+            ops.resblock_pair(x, y, c1, c2, d, 0.1)
+            torch.cuda.synchronize()
+            assert (y.cpu() - r).abs().max().item() <= 2e-5 * max(1.0, r.abs().max().item())
+            if prec == "fp32x6":
+                assert torch.equal(y, two_launch(x, c1, c2, K, d))
 
 
 def test_fused_pair_rejects_bad_args():
@@ -84,3 +87,29 @@ def test_fused_pair_rejects_bad_args():
     x16 = torch.randn(16, 100, device=DEV)
     with pytest.raises(RuntimeError):
         ops.resblock_pair(x16, torch.empty_like(x16), c16a, c16b, 1, 0.1)
+
+
+@pytest.mark.parametrize("C", [32, 64])
+@pytest.mark.parametrize("K,d", [(3, 1), (7, 3), (11, 5)])
+@pytest.mark.parametrize("scale", [1.0, 1e-4, 1e4])
+def test_fused_pair_f16x3(C, K, d, scale):
+    """Split-fp16 fused pair: its T scale is per fused tile, so it is not bit-identical to the two-launch form
+    (whose c1 output is scaled per conv tile); both within 2e-5 (relative to the output's max) of torch's fp32
+    pair, at any input magnitude (the power-of-2 scales follow the data), plain and accumulating."""
+    w, c1, c2 = make_pair(C, K, seed=C * 100 + K * 10 + d + 1)
+    L = 5003
+    x = (torch.randn(C, L, generator=torch.Generator().manual_seed(K + d + 1)) * scale).to(DEV)
+    with ops.precision("f16x3"):
+        assert ops.resblock_fusable(c1, c2, d)
+        y = torch.full_like(x, float("nan"))
+        ops.resblock_pair(x, y, c1, c2, d, 0.1)
+        acc0 = (torch.randn(C, L, generator=torch.Generator().manual_seed(7)) * scale).to(DEV)
+        yb = acc0.clone()
+        ops.resblock_pair(x, yb, c1, c2, d, 0.1, accumulate=True)
+        ref2 = two_launch(x, c1, c2, K, d)
+    torch.cuda.synchronize()
+    r = torch_ref(x.cpu(), w, K, d)
+    tol = 2e-5 * r.abs().max().item()
+    assert (y.cpu() - r).abs().max().item() <= tol
+    assert (ref2.cpu() - r).abs().max().item() <= tol
+    assert (yb.cpu() - (r + acc0.cpu())).abs().max().item() <= tol + 2e-6 * acc0.abs().max().item()
