@@ -261,6 +261,54 @@ def gen_pipeline(name, sr, version, seconds, seed, pitch, protect, f0_autotune=F
     print(name, "out", out.shape, float(np.sqrt(np.mean(out ** 2))), "segments", nseg)
 
 
+def gen_convert(seed):
+    """VoiceConverter.convert_audio (convert.py:479-523) -- the reference's own method, run on an instance
+    built around the seeded synthetic models (its __init__ would load checkpoints from disk): load_audio
+    returns the input array, sf.write captures the output.  Two speech bursts above 0.95 peak separated by
+    digital silence, so the 0.95 peak limit, cut() into chunks, one VC.pipeline per chunk (every noise draw
+    recorded, in order), restore() and, in the second case, clean_audio's spectral gate are all exercised."""
+    import main.inference.convert as conv
+    sr, version = 48000, "v2"
+    ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
+    net_g = build_ref_synth(ck)
+    from main.library.architectures import fairseq
+    cpath = os.path.join("assets", "models", "embedders", "contentvec_synth.pt")
+    torch.save(synthetic.make_contentvec_ckpt(seed + 1), cpath)
+    hub = fairseq.load_model(cpath)[0][0].float().eval()
+    torch.save(synthetic.rmvpe_state_dict(seed + 2), os.path.join("assets", "models", "predictors", "rmvpe.pt"))
+    a = synthetic.synthetic_audio(5.5, seed=seed + 3)  # > the slicer's 5 s min_length, so cut() splits after it
+    b = synthetic.synthetic_audio(2.0, seed=seed + 4)
+    audio = np.concatenate([np.zeros(4000), a / np.abs(a).max() * 1.4, np.zeros(16000), b * 0.8,
+                            np.zeros(3000)]).astype(np.float32)
+    out = {"audio": audio, "sr": sr, "seed": seed, "pitch": 1, "protect": 0.33}
+    for tag, clean in (("plain", False), ("clean", True)):
+        vcv = conv.VoiceConverter.__new__(conv.VoiceConverter)
+        vcv.config, vcv.device, vcv.sample_rate, vcv.checkpointing = conv.config, "cpu", 16000, False
+        vcv.hubert_model, vcv.embed_suffix, vcv.suffix = hub, ".pt", ".pth"
+        vcv.tgt_sr, vcv.net_g, vcv.sid, vcv.use_f0, vcv.version = sr, net_g, 0, 1, version
+        vcv.vc = conv.VC(sr, conv.config)
+        conv.load_audio = lambda *a, **k: audio.copy()
+        written = []
+        conv.sf.write = lambda path, data, rate, **k: written.append((data, rate))
+        torch.manual_seed(seed + 5)
+        with NoiseRecorder() as rec:
+            vcv.convert_audio("in.wav", "out.wav", "", "contentvec_base", 1, "rmvpe", 0.0, 1, 0.33, 64, False, 1, 3,
+                              clean, 0.5, "wav", split_audio=True)
+        assert len(written) == 1, "reference convert_audio failed (it logs and returns)"
+        kinds = [k for k, _ in rec.draws]
+        assert len(kinds) % 3 == 0 and kinds[:3] == ["randn_like", "rand", "randn_like"], kinds
+        out[f"{tag}_out"] = np.asarray(written[0][0], dtype=np.float32)
+        out[f"{tag}_rate"] = written[0][1]
+        out["nchunks"] = len(kinds) // 3
+        for c in range(len(kinds) // 3):  # same seed, same draws in both cases: stored once
+            for key, d in ((f"z_noise_{c}", rec.draws[3 * c][1]), (f"sine_noise_{c}", rec.draws[3 * c + 2][1])):
+                if key in out:
+                    assert np.array_equal(out[key], d.numpy())
+                out[key] = d.numpy()
+        print("convert", tag, out[f"{tag}_out"].shape, "chunks", len(kinds) // 3)
+    np.savez_compressed(os.path.join(OUT, "convert.npz"), **out)
+
+
 def gen_filtfilt(seed):
     from scipy import signal
     import main.inference.convert as conv
@@ -404,6 +452,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "denoise":
         gen_denoise(seed=111)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "convert":
+        gen_convert(seed=121)
         return
     if len(sys.argv) > 1 and sys.argv[1] == "edges":
         gen_edges(seed=101)
