@@ -204,7 +204,7 @@ def main():
     ap.add_argument("--no-roofline", action="store_true", help="skip the instrumented roofline pass (profiling)")
     # variants beyond the headline config (BASELINE configs 3/5 ingredients); defaults = configs[1]
     ap.add_argument("--sr", type=int, default=48000, choices=[32000, 40000, 48000])
-    ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full}")
+    ap.add_argument("--f0", default="rmvpe", help="rmvpe | crepe-{tiny,small,medium,large,full} | pm")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32x6", "f16x3", "bf16x3", "bf16"],
                     help="split-bf16 conv engine arithmetic: 6 / 3 / 1 bf16 MFMA passes per product")
     ap.add_argument("--chunks", type=int, default=1,
@@ -257,7 +257,7 @@ def main():
     index = None
     if args.index_rate > 0:
         index = synthetic_index(dev)
-    if args.f0 != "rmvpe":
+    if args.f0.startswith("crepe-"):
         from rvc_amd.crepe import CrepeAMD
         cap = args.f0.split("-", 1)[1]
         vc.crepe[cap] = CrepeAMD(synthetic.crepe_state_dict(1240, cap), cap, dev)

@@ -248,6 +248,19 @@ typedef struct rvc_f0_post {
 int rvc_rmvpe_decode(const float* sal, int64_t ld, int64_t F, double thred, double shift, const rvc_f0_post* post,
                      double* f0, int64_t* coarse, float* pitchf, rvc_stream_t stream);
 
+/* pm f0 (VC.get_f0_pm, convert.py:206-213): Praat's To Pitch (ac) with get_f0_pm's settings on the f64
+ * 16 kHz signal x [n] -> f0 [rvc_pm_frames(n)] (0 = unvoiced); window [958] = Praat's Hann window
+ * 0.5 - 0.5 cos(2 pi i / 959), i = 1..958, window_r [480] its normalised autocorrelation; work:
+ * rvc_pm_work_bytes(n) bytes.  rvc_pm_post: get_f0_pm's zero padding to p_len (when p_len > nf), then
+ * get_f0's autotune / shift / f0 file (post, as rvc_rmvpe_decode) and mel quantiser -> coarse, pitchf
+ * [max(p_len, nf)].  Restated from Boersma (1993) / Praat: parity unpinned (no parselmouth here). */
+int64_t rvc_pm_frames(int64_t n);
+int64_t rvc_pm_work_bytes(int64_t n);
+int rvc_pm_f0(const double* x, int64_t n, const double* window, const double* window_r, void* work,
+              int64_t work_bytes, double* f0, rvc_stream_t stream);
+int rvc_pm_post(const double* f0, int64_t nf, int64_t p_len, double shift, const rvc_f0_post* post,
+                int64_t* coarse, float* pitchf, rvc_stream_t stream);
+
 /* ------------------------------------------------------------------ VC.pipeline glue
  * phone_upsample: nearest x2 + protect blend (convert.py:361-378) -> phone [C][T]
  * peak_normalize: x /= max|x|/0.99 when > 1 (convert.py:450-451); ws: 16 B scratch;

@@ -154,7 +154,8 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
 
 
 def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None, index=None,
-             index_rate=0.0, crepe=None, autotune_strength=None, inp_f0=None, volume_envelope=1.0, f0_track=None):
+             index_rate=0.0, crepe=None, autotune_strength=None, inp_f0=None, volume_envelope=1.0, f0_track=None,
+             pm=False):
     """VC.pipeline (convert.py:388-458): f0 = rmvpe (or crepe), optional index, autotune, f0 file
     (``inp_f0`` [n][2] f32) and volume envelope.
 
@@ -177,6 +178,9 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
         f0 = np.array(f0_track, dtype=np.float64, copy=True)
         if f0.shape != (1 + audio_pad.shape[0] // c.window,):
             raise ValueError(f"f0_track has {f0.shape}, expected {(1 + audio_pad.shape[0] // c.window,)}")
+    elif pm:  # f0_method "pm": get_f0_pm (convert.py:206-213), restated in oracle/pm.py (parity unpinned)
+        from . import pm as opm
+        f0 = opm.get_f0_pm(audio_pad, p_len)
     elif crepe is not None:  # f0_method "crepe-<capacity>": (state dict, capacity, dither cents [T])
         from . import crepe as oc
         csd, capacity, dither = crepe

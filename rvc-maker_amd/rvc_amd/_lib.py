@@ -70,6 +70,10 @@ SIGNATURES = {
     "rvc_conv1d_x6_bytes": [c_int64, c_int64, c_int, c_int64],
     "rvc_conv1d_pack_x6": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
     "rvc_conv1d_f16_bytes": [c_int64, c_int64, c_int, c_int64],
+    "rvc_pm_frames": [c_int64],
+    "rvc_pm_work_bytes": [c_int64],
+    "rvc_pm_f0": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p],
+    "rvc_pm_post": [c_void_p, c_int64, c_int64, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p],
     "rvc_conv1d_pack_f16": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
     "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],
     "rvc_attention": [POINTER(AttnArgs), c_void_p, c_int64, c_void_p],
@@ -126,7 +130,7 @@ SIGNATURES = {
     "rvc_denoise": [c_void_p, c_int64, POINTER(DenoiseArgs), c_void_p, c_int64, c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
-             "rvc_conv1d_f16_bytes": c_int64,
+             "rvc_conv1d_f16_bytes": c_int64, "rvc_pm_frames": c_int64, "rvc_pm_work_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}

@@ -98,9 +98,11 @@ class VC:
                 os.path.join("assets", "models", "predictors", f"crepe_{capacity}.pth"), capacity, self.device)
         return self.crepe[capacity]
 
-    def f0_device(self, xp, pitch, f0_method="rmvpe", f0_autotune=False, f0_autotune_strength=1.0, inp_f0=None):
+    def f0_device(self, xp, pitch, f0_method="rmvpe", f0_autotune=False, f0_autotune_strength=1.0, inp_f0=None,
+                  xp64=None):
         """VC.get_f0 (convert.py:304-323) on the device: (coarse int64 [T], pitchf f32 [T]).  Autotune
-        and the f0-file override run inside the decode kernels, in the reference's order."""
+        and the f0-file override run inside the decode kernels, in the reference's order.  "pm" reads the
+        f64 signal ``xp64`` (the reference hands parselmouth the f64 filtfilt output)."""
         post = None
         if f0_autotune or inp_f0 is not None:
             rep, off = f0_override(inp_f0, self.x_pad) if inp_f0 is not None else (None, 0)
@@ -110,7 +112,14 @@ class VC:
             return coarse, pitchf
         if f0_method in self.CREPE_METHODS:
             return self._crepe(self.CREPE_METHODS[f0_method]).f0_device(xp, float(pitch), post=post)
-        raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe and crepe-* are on the MI355X hot path")
+        if f0_method == "pm":
+            if xp64 is None:
+                raise ValueError("f0 method 'pm' reads the f64 filtered signal (xp64)")
+            if getattr(self, "pm", None) is None:
+                from .pm import PitchPM
+                self.pm = PitchPM(xp64.device)
+            return self.pm.f0_device(xp64, xp.numel() // self.window, float(pitch), post=post)
+        raise NotImplementedError(f"f0 method {f0_method!r}: rmvpe, crepe-* and pm are on the MI355X path")
 
     # ------------------------------------------------------------------ device pieces
     def features_device(self, model, a0, version):
@@ -154,7 +163,8 @@ class VC:
             audio = torch.from_numpy(np.ascontiguousarray(audio, dtype=np.float32)).to(self.device)
         N = audio.numel()
         long_input = N + self.window > self.t_max  # convert.py:406 (audio padded by window/2 each side)
-        xp, xp64 = self.filt(audio.contiguous(), self.t_pad, want_f64=long_input or volume_envelope != 1)
+        xp, xp64 = self.filt(audio.contiguous(), self.t_pad,
+                             want_f64=long_input or volume_envelope != 1 or f0_method == "pm")
         opt_ts = []
         if long_input:  # quiet-point search on the filtered f64 signal, host side as the reference
             opt_ts = self.segment_points(xp64[self.t_pad: self.t_pad + N].cpu().numpy())
@@ -162,7 +172,7 @@ class VC:
         f0_opts = dict(f0_autotune=f0_autotune, f0_autotune_strength=f0_autotune_strength, inp_f0=inp_f0)
         src64 = xp64[self.t_pad: self.t_pad + N] if volume_envelope != 1 else None
         return self._pipeline_on_device(model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index,
-                                        index_rate, f0_method, f0_opts, volume_envelope, src64)
+                                        index_rate, f0_method, f0_opts, volume_envelope, src64, xp64)
 
     def pipeline_device_batch(self, model, net_g, sid, audios, pitch, version, protect, index=None, index_rate=0.0,
                               f0_method="rmvpe"):
@@ -261,7 +271,9 @@ class VC:
                 mark("front_start", g, front)
                 for a in group:
                     a.record_stream(front)
-                xps = [self.filt(a.contiguous(), self.t_pad)[0] for a in group]
+                pm = f0_method == "pm"  # pm reads the f64 filtered signal
+                filtered = [self.filt(a.contiguous(), self.t_pad, want_f64=pm) for a in group]
+                xps, x64s = [f for f, _ in filtered], [f for _, f in filtered]
                 xp = xps[0] if len(group) == 1 else torch.stack(xps)
                 side = self._aux_stream(dev, "fside")
                 ready = torch.cuda.Event()
@@ -269,11 +281,11 @@ class VC:
                 with torch.cuda.stream(side):
                     side.wait_event(ready)
                     if len(group) == 1:
-                        coarse, pitchf = self.f0_device(xp, pitch, f0_method)
+                        coarse, pitchf = self.f0_device(xp, pitch, f0_method, xp64=x64s[0])
                     elif f0_method == "rmvpe":
                         coarse, pitchf = self._rmvpe().f0_device_batch(xp, 0.03, float(pitch))
                     else:
-                        pairs = [self.f0_device(xp[b], pitch, f0_method) for b in range(len(group))]
+                        pairs = [self.f0_device(xp[b], pitch, f0_method, xp64=x64s[b]) for b in range(len(group))]
                         coarse, pitchf = torch.stack([c for c, _ in pairs]), torch.stack([f for _, f in pairs])
                     f0_done = torch.cuda.Event()
                     f0_done.record(side)
@@ -282,6 +294,9 @@ class VC:
                 for t in (coarse, pitchf):
                     t.record_stream(front)
                 xp.record_stream(side)
+                for t in x64s:
+                    if t is not None:
+                        t.record_stream(side)
                 done = torch.cuda.Event()
                 done.record(front)
                 mark("front_end", g, front)
@@ -354,7 +369,7 @@ class VC:
         return self._pooled_stream(device, prio, self.STREAM_SLOT["side"])
 
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index=None,
-                            index_rate=0.0, f0_method="rmvpe", f0_opts=None, volume_envelope=1.0, src64=None):
+                            index_rate=0.0, f0_method="rmvpe", f0_opts=None, volume_envelope=1.0, src64=None, xp64=None):
         # Segments of convert.py:419-440: [s, t + t_pad2 + w) for each quiet point t, then [t, end).
         w, tp = self.window, self.t_pad_tgt
         segs, s = [], 0
@@ -373,7 +388,7 @@ class VC:
         ready.record(main)
         with torch.cuda.stream(side):
             side.wait_event(ready)
-            coarse, pitchf = self.f0_device(xp, pitch, f0_method, **(f0_opts or {}))
+            coarse, pitchf = self.f0_device(xp, pitch, f0_method, xp64=xp64, **(f0_opts or {}))
             f0_done = torch.cuda.Event()
             f0_done.record(side)
         feats = [self.features_device(model, xp[a:b], version) for a, b, _, _ in segs]
@@ -381,6 +396,8 @@ class VC:
         coarse.record_stream(main)
         pitchf.record_stream(main)
         xp.record_stream(side)
+        if xp64 is not None:
+            xp64.record_stream(side)
         coarse, pitchf = coarse[:p_len], pitchf[:p_len]
         outs = []
         for seg, ((a, b, fa, fb), fe) in enumerate(zip(segs, feats)):
@@ -417,8 +434,8 @@ class VC:
     def pipeline(self, model, net_g, sid, audio, pitch, f0_method, file_index, index_rate, pitch_guidance,
                  filter_radius, volume_envelope, version, protect, hop_length, f0_autotune, f0_autotune_strength,
                  suffix, embed_suffix, f0_file=None, f0_onnx=False, pbar=None):
-        if (f0_method != "rmvpe" and f0_method not in self.CREPE_METHODS) or f0_onnx:
-            raise NotImplementedError(f"f0 method {f0_method!r}: only rmvpe and crepe-* are on the MI355X hot path")
+        if (f0_method not in ("rmvpe", "pm") and f0_method not in self.CREPE_METHODS) or f0_onnx:
+            raise NotImplementedError(f"f0 method {f0_method!r}: rmvpe, crepe-* and pm are on the MI355X path")
         index = None
         if file_index != "" and os.path.exists(file_index) and index_rate != 0:  # convert.py:392-399
             index = self._index(file_index)
