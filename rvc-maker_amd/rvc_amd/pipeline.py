@@ -132,6 +132,15 @@ class VC:
     def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats=None,
                                 index=None, index_rate=0.0):
         """VC.voice_conversion (convert.py:328-386) on a device segment a0 [N] -> waveform [T*upp]."""
+        prep = self.prior_device(model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats, index,
+                                 index_rate, self.seed + seg)
+        return self.generate_device(net_g, prep, seg, self.seed + seg)
+
+    def prior_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats=None, index=None,
+                     index_rate=0.0, seed=0):
+        """voice_conversion up to the generator: retrieval, phone upsample + protect (convert.py:347-378),
+        TextEncoder, prior sample and flow^-1 (Synthesizer.infer, synthesizers.py:446-460) -> a dict for
+        generate_device."""
         N = a0.numel()
         if feats is None:
             feats = self.features_device(model, a0, version)
@@ -150,9 +159,13 @@ class VC:
         blend = protect < 0.5
         ops.phone_upsample(feats, feats0, pitchf if blend else None, phone, E, Tf, T, float(protect))
         zn = self.noise_fn(seg, "z", (1, net_g.inter, T)) if self.noise_fn else None
-        sn = self.noise_fn(seg, "sine", (1, T * net_g.upp, 1)) if self.noise_fn else None
-        o, *_ = net_g.infer_cf(phone, pitch.contiguous(), pitchf.contiguous(), sid, zn, sn, self.seed + seg)
-        return o
+        z, _, _, gc = net_g.prior_cf(phone, pitch.contiguous(), sid, zn, seed)
+        return {"z": z, "gc": gc, "pitchf": pitchf.contiguous(), "T": T}
+
+    def generate_device(self, net_g, prep, seg, seed):
+        """The NSF generator on prior_device's z (synthesizers.py:461-465) -> waveform [T*upp]."""
+        sn = self.noise_fn(seg, "sine", (1, prep["T"] * net_g.upp, 1)) if self.noise_fn else None
+        return net_g.decode_cf(prep["z"], prep["pitchf"], prep["gc"], sn, seed)
 
     def pipeline_device(self, model, net_g, sid, audio, pitch, version, protect, index=None, index_rate=0.0,
                         f0_method="rmvpe", f0_autotune=False, f0_autotune_strength=1.0, inp_f0=None,
@@ -265,7 +278,9 @@ class VC:
         seed0, tp = self.seed, self.t_pad_tgt
 
         def issue_front(group, g):
-            """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event)"""
+            """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event).
+            (The synthesizer's TextEncoder / prior / flow stay on the back stream: moved to the front stream they
+            made the front end the critical chain, 705 vs 820 xRT.)"""
             with torch.cuda.stream(front):
                 front.wait_stream(caller)  # the caller wrote the inputs on its own stream
                 mark("front_start", g, front)
@@ -297,12 +312,14 @@ class VC:
                 for t in x64s:
                     if t is not None:
                         t.record_stream(side)
+                if len(group) == 1:
+                    items = [(xp, coarse, pitchf, feats)]
+                else:
+                    items = [(xp[b], coarse[b], pitchf[b], feats[b]) for b in range(len(group))]
                 done = torch.cuda.Event()
                 done.record(front)
                 mark("front_end", g, front)
-            if len(group) == 1:
-                return [(xp, coarse, pitchf, feats)], done
-            return [(xp[b], coarse[b], pitchf[b], feats[b]) for b in range(len(group))], done
+            return items, done
 
         outs = []
         nxt = issue_front(groups[0], 0)

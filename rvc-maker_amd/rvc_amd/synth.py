@@ -224,8 +224,9 @@ class SynthesizerAMD:
         g = self.emb_g[sid].view(self.gin, 1)
         return self.cond(g).view(-1)
 
-    def infer_cf(self, phone_cf, pitch, nsff0, sid: int, z_noise=None, sine_noise=None, seed: int = 0):
-        """Channels-first core: phone [E][T], pitch int64 [T], nsff0 f32 [T] -> (o [T*upp], z, z_p, stats)."""
+    def prior_cf(self, phone_cf, pitch, sid: int, z_noise=None, seed: int = 0):
+        """Synthesizer.infer up to the generator (synthesizers.py:446-460): TextEncoder, prior sample, flow^-1.
+        phone [E][T], pitch int64 [T] -> (z, z_p, stats, gc)."""
         E, T = phone_cf.shape
         dev = phone_cf.device
         if E != self.emb_dim:
@@ -237,11 +238,21 @@ class SynthesizerAMD:
         z_p = torch.empty(self.inter, T, device=dev)
         ops.prior_sample(stats, z_noise.reshape(self.inter, T), z_p, 1, self.inter, T, 0.66666)
         z = self.flow_reverse(z_p, gc, T)
+        return z, z_p, stats, gc
+
+    def decode_cf(self, z, nsff0, gc, sine_noise=None, seed: int = 0):
+        """The NSF generator on z [inter][T] (synthesizers.py:461-465) -> o [T*upp]."""
+        T = z.shape[-1]
         if sine_noise is None:
-            sine_noise = ops.randn(torch.empty(T * self.upp, device=dev), seed, 1 << 40)
+            sine_noise = ops.randn(torch.empty(T * self.upp, device=z.device), seed, 1 << 40)
         o = self.generator(z, nsff0.reshape(T).float().contiguous(), gc[4 * 6 * self.hidden:], T,
                            sine_noise.reshape(T * self.upp))
-        return o.view(-1), z, z_p, stats
+        return o.view(-1)
+
+    def infer_cf(self, phone_cf, pitch, nsff0, sid: int, z_noise=None, sine_noise=None, seed: int = 0):
+        """Channels-first core: phone [E][T], pitch int64 [T], nsff0 f32 [T] -> (o [T*upp], z, z_p, stats)."""
+        z, z_p, stats, gc = self.prior_cf(phone_cf, pitch, sid, z_noise, seed)
+        return self.decode_cf(z, nsff0, gc, sine_noise, seed), z, z_p, stats
 
     def infer(self, phone, phone_lengths, pitch=None, nsff0=None, sid=None, rate=None, z_noise=None,
               sine_noise=None, seed: int = 0):
