@@ -598,7 +598,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     // independent loads below them and every k-step pays the full L2 round trip).
     // depth: as many k-steps as fit a 24-uint4 (96-VGPR) ring, at most 4
     // (8 compute waves = 3 waves per SIMD: an 18-uint4 ring, at most 2 deep)
-    constexpr int PD_FIT = (NCW == 8 ? 18 : 24) / (NPL * FM) - 1;
+    // (a 256-column tile, FN = 8, keeps its 64 accumulators by giving the ring 12 uint4)
+    constexpr int PD_FIT = (FN == 8 ? 12 : (NCW == 8 ? 18 : 24)) / (NPL * FM) - 1;
     constexpr int PD_MAX = x6_min_blocks<FM, FN, NCW, NP>() == 2 ? 1 : (NCW == 8 ? 2 : 4);
     constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > PD_MAX ? PD_MAX : PD_FIT);
     constexpr int NB = PD + 1;
@@ -775,7 +776,17 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         // 4 waves of twice the tile on every 128/256-channel shape, and on 64 channels at >= 3 passes
         static const int w8 = getenv("RVC_X6_W8") ? atoi(getenv("RVC_X6_W8")) : 1;
         const int np = a->wx_passes == 0 ? 6 : a->wx_passes;
-        if (Cog > 64 && w8) cfg = {2, 4, 4, 2, true};  // 128 x 128 on 8 compute waves
+        // 128 x 256 on 8 compute waves for the split-fp16 convs (RVC_X6_BN256: 1 = split-fp16 only, the
+        // default; 2 = every pass set; 0 = off): half the blocks, so half the per-block prologue / epilogue
+        // (~15-25 us each), and each weight fragment feeds twice the MFMAs; stride-1, short tap spans.
+        // Measured (conv_bench, same box): split-fp16 C=128 K=11 762 -> 672 us, K=7 590 -> 534, C=256 K=11
+        // 331 -> 307; end to end 820 -> 850 xRT.  The 6-pass form loses (its weight ring drops to 1 k-step
+        // to fit 64 accumulators: C=128 K=11 883 -> 1113 us).
+        static const int bn256 = getenv("RVC_X6_BN256") ? atoi(getenv("RVC_X6_BN256")) : 1;
+        if (Cog > 64 && w8 && bn256 && a->stride == 1 && 255 + max_tap_off(a) + 1 <= 64 * X6_NI_MAX &&
+            (bn256 == 2 || np == RVC_ARITH_F16X3))
+            cfg = {2, 8, 4, 2, true};
+        else if (Cog > 64 && w8) cfg = {2, 4, 4, 2, true};  // 128 x 128 on 8 compute waves
         else if (Cog > 64) cfg = {4, 4, 2, 2, true};   // 128 x 128 on 4 compute waves
         else if (Cog > 32 && w8 && np >= 3) cfg = {2, 2, 2, 4, true};  // 64 x 128 on 8 compute waves
         else if (Cog > 32) cfg = {2, 4, 2, 2, true};   // 64 x 128
@@ -985,7 +996,8 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     if (cfg.x6) {
-        if (cfg.WM == 4) e = launch_x6<2, 4, 4, 2>(p, grid, lds, s);
+        if (cfg.WM == 4 && cfg.FN == 8) e = launch_x6<2, 8, 4, 2>(p, grid, lds, s);
+        else if (cfg.WM == 4) e = launch_x6<2, 4, 4, 2>(p, grid, lds, s);
         else if (cfg.WM == 2 && cfg.WN == 4) e = launch_x6<2, 2, 2, 4>(p, grid, lds, s);
         else if (cfg.FM == 4) e = launch_x6<4, 4, 2, 2>(p, grid, lds, s);
         else if (cfg.WM == 2) e = launch_x6<2, 4, 2, 2>(p, grid, lds, s);
