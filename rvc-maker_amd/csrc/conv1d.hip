@@ -374,6 +374,14 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
 // B operands are one ds_read_b128 per plane per fragment; A operands (weights) come pre-split
 // and pre-arranged per lane from global memory (L2-resident), prefetched one k-step ahead.
 constexpr int X6_NI_MAX = 6;  // staged (position, 8-channel group) items per loader thread: 4 * span <= 256 NI
+// Profiling ablations (RVC_CONV_DEBUG at run time) exist only in a -DRVC_CONV_ABLATIONS=1 build: a run-time
+// test inside the k-loop made hipcc split every fragment's MFMAs into two paths with register copies,
+// lgkmcnt(0) / vmcnt(0) waits in front of them and a branch per 6 MFMAs, and the loaders' per-element
+// "load or zero" select serialised their loads.
+#ifndef RVC_CONV_ABLATIONS
+#define RVC_CONV_ABLATIONS 0
+#endif
+constexpr bool kAblations = RVC_CONV_ABLATIONS != 0;
 
 // Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
@@ -453,7 +461,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 for (int e = 0; e < 8; ++e) {
                     int c = ch * 32 + ig8[it] * 8 + e;
                     c = c < Cig ? c : Cig - 1;
-                    r[it][e] = (p.dbg & 4) ? 0.f : xb[(int64_t)c * lin + qc];
+                    r[it][e] = (kAblations && (p.dbg & 4)) ? 0.f : xb[(int64_t)c * lin + qc];
                 }
             }
         };
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         for (int j = 0; j < FN; ++j) {
             if (j + 1 < FN) bload(j + 1, bb[(j + 1) & 1]);
             const uint4 (&bq)[NPL] = bb[j & 1];
-            if (p.dbg & 2) {
+            if (kAblations && (p.dbg & 2)) {
 #pragma unroll
                 for (int i = 0; i < FM; ++i) acc[i][j][0] += __builtin_bit_cast(float, (a[0][i].x ^ bq[NPL - 1].y) & 0x3fffffu);
                 continue;
@@ -627,7 +635,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             }
         }
     }
-    if (p.dbg & 1) {
+    if (kAblations && (p.dbg & 1)) {
         if (acc[0][0][0] == 1234.5f) p.y[lane] = acc[FM - 1][FN - 1][3];  // keep the loop live
         return;
     }

@@ -56,8 +56,7 @@ X6 = os.environ.get("RVC_AMD_X6", "1") != "0"
 
 # Arithmetic of the split-operand MFMA engine (f32 accumulation always):
 #   "fp32"   f32-equivalent (the default; BASELINE configs 1-2, 4): "fp32x6" everywhere except the convs where
-#            "f16x3" measured faster -- stride-1 1-D convs with k >= 7 taps over <= 256 input channels, and the
-#            fused ResBlock pairs with k >= 7 (F16_MIX; RVC_AMD_F16MIX=0 turns it off)
+#            "f16x3" measured faster (conv_passes, rb_passes; F16_MIX; RVC_AMD_F16MIX=0 turns it off)
 #   "fp32x6" 6 bf16 passes, f32-accurate products (~2^-22 relative per product)
 #   "f16x3"  3 fp16 passes over power-of-2-scaled 22-bit operands (~2^-20 relative per product)
 #   "bf16x3" 3 bf16 passes, 16-bit operand mantissas (~2^-16 relative per product)
@@ -68,8 +67,11 @@ F16_MIX = os.environ.get("RVC_AMD_F16MIX", "1") != "0"
 
 
 def conv_passes(K, Ci, stride=1, two_d=False):
-    """The pass set a conv launch runs at under the current precision (see PASSES)."""
-    if _PRECISION == "fp32" and F16_MIX and K >= 7 and Ci <= 256 and stride == 1 and not two_d:
+    """The pass set a conv launch runs at under the current precision (see PASSES): in "fp32", split-fp16
+    where it measured faster than 6-pass split-bf16 (scripts/conv_bench.py, same box: k >= 7 up to 256
+    input channels, and k = 3 at 64-128 channels; 6-pass at k = 3 over 256 or 32 channels)."""
+    if _PRECISION == "fp32" and F16_MIX and stride == 1 and not two_d and \
+            ((K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128)):
         return F16X3
     return PASSES[_PRECISION]
 _PRECISION = os.environ.get("RVC_AMD_PRECISION", "fp32")
