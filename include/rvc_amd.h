@@ -346,6 +346,58 @@ int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T,
                             double mel_max, const rvc_f0_post* post, int64_t* coarse, float* pitchf,
                             rvc_stream_t stream);
 
+/* ------------------------------------------------------------------ model-level API
+ * A context per device that owns the weights of a voice model and its scratch, so that a non-Python
+ * host can run Synthesizer.infer (synthesizers.py:446-465) through this header alone: the folding and
+ * packing the Python loader does (rvc_amd/synth.py) and the launch sequence of its infer are native
+ * (csrc/rvc_model.cpp), with the same kernels, pass sets and order -- bit-identical to the Python path
+ * on the same fp32 weights.
+ *   rvc_ctx_create / destroy   one context per HIP device (not re-entrant; calls are stream-ordered).
+ *   rvc_ctx_set_precision      the conv engine's arithmetic: RVC_PREC_FP32 (default: 6-pass split-bf16
+ *                              mixed with split-fp16 where measured faster), _FP32X6, _F16X3, _BF16X3, _BF16.
+ *   rvc_load_synth             params = the .pth "weight" dict (train.py:729-742) as named HOST arrays,
+ *                              f32 or f16; weight-norm pairs (x.weight_g / x.weight_v) are folded at load
+ *                              (torch._weight_norm, dim 0), already-folded x.weight is taken as is.
+ *                              cfg = the .pth "config" list.  Synchronous; replaces a loaded model.
+ *   rvc_synth_infer            phone f32 [B][T][E], pitch int64 [B][T], pitchf f32 [B][T] (device);
+ *                              sid: HOST int64 [B]; z_noise [B][inter][T] / sine_noise [B][T*upp] device
+ *                              or NULL (NULL = device Philox draws from seed + b, as the Python path);
+ *                              wav f32 [B][rvc_synth_out_len(ctx, T)] device.  Scratch grows on demand
+ *                              (a stream sync when it does); nothing else synchronises. */
+typedef struct rvc_ctx rvc_ctx;
+
+enum { RVC_DT_F32 = 0, RVC_DT_F16 = 1 };
+enum { RVC_PREC_FP32 = 0, RVC_PREC_BF16 = 1, RVC_PREC_BF16X3 = 3, RVC_PREC_FP32X6 = 6, RVC_PREC_F16X3 = 16 };
+
+typedef struct rvc_param {
+    const char* name;  /* state-dict key, e.g. "dec.ups.0.weight_v" */
+    const void* data;  /* host, dense row-major                     */
+    int dtype;         /* RVC_DT_F32 / RVC_DT_F16                    */
+    int ndim;
+    int64_t shape[4];
+} rvc_param;
+
+typedef struct rvc_synth_cfg { /* the checkpoint's "config" list (train.py:729-742) */
+    int inter_channels, hidden_channels, filter_channels, n_heads, n_layers, kernel_size;
+    int n_resblocks, n_dilations;          /* len(resblock_kernel_sizes), len(resblock_dilation_sizes[0]) */
+    int resblock_kernel_sizes[4];
+    int resblock_dilation_sizes[4][4];
+    int n_upsamples;
+    int upsample_rates[8];
+    int upsample_kernel_sizes[8];
+    int upsample_initial_channel;
+    int spk_embed_dim, gin_channels, sr;
+} rvc_synth_cfg;
+
+int rvc_ctx_create(int hip_device, rvc_ctx** out);
+void rvc_ctx_destroy(rvc_ctx* ctx);
+int rvc_ctx_set_precision(rvc_ctx* ctx, int prec);
+int rvc_load_synth(rvc_ctx* ctx, const rvc_param* params, int n, const rvc_synth_cfg* cfg);
+int64_t rvc_synth_out_len(const rvc_ctx* ctx, int64_t T);
+int rvc_synth_infer(rvc_ctx* ctx, const float* phone, const int64_t* pitch, const float* pitchf, int64_t B, int64_t T,
+                    const int64_t* sid, const float* z_noise, const float* sine_noise, uint64_t seed, float* wav,
+                    rvc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,21 @@ class DenoiseArgs(ctypes.Structure):
                 ("window", c_void_p), ("filt", c_void_p)]
 
 
+class Param(ctypes.Structure):
+    """rvc_param: one named host array of a checkpoint's weight dict (model-level API)."""
+    _fields_ = [("name", ctypes.c_char_p), ("data", c_void_p), ("dtype", c_int), ("ndim", c_int),
+                ("shape", c_int64 * 4)]
+
+
+class SynthCfg(ctypes.Structure):
+    """rvc_synth_cfg: the .pth "config" list (train.py:729-742)."""
+    _fields_ = [("inter_channels", c_int), ("hidden_channels", c_int), ("filter_channels", c_int), ("n_heads", c_int),
+                ("n_layers", c_int), ("kernel_size", c_int), ("n_resblocks", c_int), ("n_dilations", c_int),
+                ("resblock_kernel_sizes", c_int * 4), ("resblock_dilation_sizes", (c_int * 4) * 4),
+                ("n_upsamples", c_int), ("upsample_rates", c_int * 8), ("upsample_kernel_sizes", c_int * 8),
+                ("upsample_initial_channel", c_int), ("spk_embed_dim", c_int), ("gin_channels", c_int), ("sr", c_int)]
+
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "rvc_last_error": [],
@@ -128,12 +143,20 @@ SIGNATURES = {
     "rvc_resblock_lds_bytes": [c_int64, c_int, c_int, c_int],
     "rvc_resblock_pair": [POINTER(ResblockArgs), c_void_p],
     "rvc_denoise": [c_void_p, c_int64, POINTER(DenoiseArgs), c_void_p, c_int64, c_void_p, c_void_p],
+    "rvc_ctx_create": [c_int, POINTER(c_void_p)],
+    "rvc_ctx_destroy": [c_void_p],
+    "rvc_ctx_set_precision": [c_void_p, c_int],
+    "rvc_load_synth": [c_void_p, POINTER(Param), c_int, POINTER(SynthCfg)],
+    "rvc_synth_out_len": [c_void_p, c_int64],
+    "rvc_synth_infer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
+                        c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
              "rvc_conv1d_f16_bytes": c_int64, "rvc_pm_frames": c_int64, "rvc_pm_work_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
-             "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint}
+             "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint,
+             "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64}
 
 _lib = None
 

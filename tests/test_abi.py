@@ -41,12 +41,44 @@ def test_errors_are_reported_without_gpu():
     assert lib.rvc_version() >= 1
 
 
+def test_model_api_rejects_bad_arguments_without_gpu():
+    import ctypes as C
+    lib = _lib.load()
+    cfg = _lib.SynthCfg()
+    assert lib.rvc_load_synth(None, None, 0, C.byref(cfg)) == -22
+    assert b"null" in lib.rvc_last_error()
+    assert lib.rvc_synth_infer(None, None, None, None, 1, 1, None, None, None, 0, None, None) == -22
+    assert b"no synthesizer" in lib.rvc_last_error()
+    assert lib.rvc_synth_out_len(None, 10) == -1
+    assert lib.rvc_ctx_set_precision(None, 0) == -22
+    lib.rvc_ctx_destroy(None)  # no-op
+
+
+def test_synth_cfg_from_checkpoint_config():
+    from rvc_amd import synthetic
+    from rvc_amd.native import synth_cfg
+    ck = synthetic.make_synth_ckpt(48000, "v2", seed=1)
+    c = synth_cfg(ck)
+    cfg = ck["config"]
+    assert (c.inter_channels, c.hidden_channels, c.filter_channels, c.n_heads, c.n_layers, c.kernel_size) == \
+        tuple(cfg[2:8])
+    assert [c.upsample_rates[i] for i in range(c.n_upsamples)] == list(cfg[12])
+    assert [c.upsample_kernel_sizes[i] for i in range(c.n_upsamples)] == list(cfg[14])
+    assert [c.resblock_kernel_sizes[j] for j in range(c.n_resblocks)] == list(cfg[10])
+    assert [[c.resblock_dilation_sizes[j][m] for m in range(c.n_dilations)] for j in range(c.n_resblocks)] == \
+        [list(d) for d in cfg[11]]
+    assert (c.upsample_initial_channel, c.gin_channels, c.sr) == (cfg[13], cfg[16], cfg[17])
+    assert c.spk_embed_dim == ck["weight"]["emb_g.weight"].shape[0]
+
+
 def test_struct_layouts_match_c_compiler(tmp_path):
     import subprocess
     fields = {"rvc_conv1d_args": [f[0] for f in _lib.Conv1dArgs._fields_],
               "rvc_attn_args": [f[0] for f in _lib.AttnArgs._fields_],
               "rvc_f0_post": [f[0] for f in _lib.F0Post._fields_],
-              "rvc_denoise_args": [f[0] for f in _lib.DenoiseArgs._fields_]}
+              "rvc_denoise_args": [f[0] for f in _lib.DenoiseArgs._fields_],
+              "rvc_param": [f[0] for f in _lib.Param._fields_],
+              "rvc_synth_cfg": [f[0] for f in _lib.SynthCfg._fields_]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rvc_amd.h"', "int main(void){"]
     for st, fs in fields.items():
         lines.append(f'printf("%zu\\n", sizeof({st}));')
@@ -59,7 +91,7 @@ def test_struct_layouts_match_c_compiler(tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = []
-    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs):
+    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs, _lib.Param, _lib.SynthCfg):
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f[0]).offset for f in cls._fields_]
     assert got == want

@@ -1,0 +1,97 @@
+"""The model-level C ABI (rvc_ctx / rvc_load_synth / rvc_synth_infer, csrc/rvc_model.cpp) on the device:
+against the reference's own Synthesizer.infer outputs (golden vectors, fp16 weight-norm checkpoints folded by
+the library) and bit-for-bit against the Python launch sequence (SynthesizerAMD) on the same fp32 weights."""
+import numpy as np
+import pytest
+import torch
+
+from rvc_amd import ops, synthetic
+from rvc_amd.native import NativeSynth
+from rvc_amd.synth import SynthesizerAMD, fold_weight_norm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rms(a, b):
+    a = a.detach().cpu().double().numpy() if torch.is_tensor(a) else np.asarray(a, np.float64)
+    b = b.detach().cpu().double().numpy() if torch.is_tensor(b) else np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+def inputs(T, E=768, seed=0, B=1):
+    g = torch.Generator().manual_seed(seed)
+    phone = torch.randn(B, T, E, generator=g).to(DEV)
+    pitch = torch.randint(1, 255, (B, T), generator=g).to(DEV)
+    pitchf = (torch.rand(B, T, generator=g) * 400).to(DEV)
+    return phone, pitch, pitchf
+
+
+@pytest.mark.parametrize("name", ["synth_48k_v2", "synth_40k_v2", "synth_32k_v1"])
+def test_native_synth_matches_reference_golden(golden, name):
+    g = golden(name)
+    ck = synthetic.make_synth_ckpt(int(g["sr"]), str(g["version"]), seed=int(g["seed"]))
+    net = NativeSynth(ck, DEV)  # fp16 weight_g / weight_v pairs: folded by rvc_load_synth
+    T = int(g["T"])
+    o = net.infer(torch.from_numpy(g["phone"]).to(DEV), torch.tensor([T]), torch.from_numpy(g["pitch"]).to(DEV),
+                  torch.from_numpy(g["pitchf"]).to(DEV), torch.from_numpy(g["sid"]),
+                  z_noise=torch.from_numpy(g["z_noise"]).to(DEV), sine_noise=torch.from_numpy(g["sine_noise"]).to(DEV))[0]
+    torch.cuda.synchronize()
+    # tolerance: 1e-4 RMS on the waveform (BASELINE.json north_star, fp32)
+    assert o.shape == g["o"].shape
+    assert rms(o, g["o"]) < 1e-4
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_native_synth_bit_identical_to_python_sequence(precision):
+    ck = synthetic.make_synth_ckpt(48000, "v2", seed=11)
+    py = SynthesizerAMD(ck, DEV)
+    nat = NativeSynth(ck, DEV, weights=fold_weight_norm(ck["weight"]), precision=precision)
+    T = 300  # 144000 samples: every generator stage, fused 32/64-channel pairs included
+    phone, pitch, pitchf = inputs(T)
+    with ops.precision(precision):
+        a = py.infer(phone, torch.tensor([T]), pitch, pitchf, 0, seed=3)[0]
+    b = nat.infer(phone, torch.tensor([T]), pitch, pitchf, 0, seed=3)[0]
+    torch.cuda.synchronize()
+    assert a.shape == b.shape == (1, 1, T * 480)
+    assert torch.equal(a, b), rms(a, b)
+    # injected noise takes the same route
+    zn = torch.randn(1, 192, T, generator=torch.Generator().manual_seed(5)).to(DEV)
+    sn = torch.randn(1, T * 480, 1, generator=torch.Generator().manual_seed(6)).to(DEV)
+    with ops.precision(precision):
+        a = py.infer(phone, torch.tensor([T]), pitch, pitchf, 0, z_noise=zn, sine_noise=sn)[0]
+    b = nat.infer(phone, torch.tensor([T]), pitch, pitchf, 0, z_noise=zn, sine_noise=sn)[0]
+    assert torch.equal(a, b), rms(a, b)
+
+
+def test_native_synth_batch_and_scratch_growth():
+    ck = synthetic.make_synth_ckpt(40000, "v2", seed=12)
+    nat = NativeSynth(ck, DEV)
+    T = 96
+    phone, pitch, pitchf = inputs(T, B=2, seed=1)
+    sid = torch.tensor([0, 0])
+    both = nat.infer(phone, torch.tensor([T, T]), pitch, pitchf, sid, seed=9)[0]
+    one0 = nat.infer(phone[:1], torch.tensor([T]), pitch[:1], pitchf[:1], 0, seed=9)[0]
+    one1 = nat.infer(phone[1:], torch.tensor([T]), pitch[1:], pitchf[1:], 0, seed=10)[0]  # sequence b draws seed + b
+    assert torch.equal(both[0], one0[0]) and torch.equal(both[1], one1[0])
+    # a longer call grows the scratch; the short call after it is unchanged
+    pl, ql, fl = inputs(700, seed=2)
+    long = nat.infer(pl, torch.tensor([700]), ql, fl, 0, seed=9)[0]
+    again = nat.infer(phone[:1], torch.tensor([T]), pitch[:1], pitchf[:1], 0, seed=9)[0]
+    torch.cuda.synchronize()
+    assert torch.isfinite(long).all() and long.shape == (1, 1, 700 * 400)
+    assert torch.equal(again, one0)
+
+
+def test_native_synth_errors():
+    ck = synthetic.make_synth_ckpt(48000, "v2", seed=13)
+    nat = NativeSynth(ck, DEV)
+    T = 16
+    phone, pitch, pitchf = inputs(T)
+    with pytest.raises(RuntimeError, match="sid"):
+        nat.infer(phone, torch.tensor([T]), pitch, pitchf, 500)  # the synthetic ckpt has 109 speakers
+    bad = dict(ck["weight"])
+    del bad["dec.m_source.l_linear.bias"]
+    with pytest.raises(RuntimeError, match="dec.m_source.l_linear.bias"):
+        NativeSynth(ck, DEV, weights=bad)
