@@ -398,6 +398,37 @@ int rvc_synth_infer(rvc_ctx* ctx, const float* phone, const int64_t* pitch, cons
                     const int64_t* sid, const float* z_noise, const float* sine_noise, uint64_t seed, float* wav,
                     rvc_stream_t stream);
 
+/* ContentVec / HuBERT-base (HubertModel.extract_features, fairseq.py:1459 -> :1412-1431; extractor "default",
+ * post-LN).  params = the fairseq .pt "model" dict (floating entries); encoder.pos_conv's weight-norm pair
+ * (dim 2) is folded at load.  cfg = the .pt "cfg"/"model" fields below.
+ *   rvc_contentvec_forward: wav f32 [B][N] (16 kHz, device) -> feats f32 [B][T][C] time-major like
+ *   extract_features' x (T = rvc_contentvec_frames(N)), after out_layer encoder layers (12 for v2, 9 for v1,
+ *   convert.py:338); final_proj != 0 applies model.final_proj (convert.py:340) and C = its width. */
+typedef struct rvc_contentvec_cfg {
+    int encoder_embed_dim, encoder_attention_heads, conv_pos_groups, _pad0;
+} rvc_contentvec_cfg;
+
+int rvc_load_contentvec(rvc_ctx* ctx, const rvc_param* params, int n, const rvc_contentvec_cfg* cfg);
+int64_t rvc_contentvec_frames(int64_t n16k);
+int rvc_contentvec_forward(rvc_ctx* ctx, const float* wav, int64_t B, int64_t N, int out_layer, int final_proj,
+                           float* feats, rvc_stream_t stream);
+
+/* RMVPE (E2E(4, 1, (2, 2)), RMVPE.py:183-226 as VC.get_f0_rmvpe uses it, convert.py:248-255).
+ * params = the rmvpe.pt state dict; BatchNorm folded at load.  Optional extra params: "mel_basis" f32 [128][513]
+ * (librosa.filters.mel(16000, 1024, 128, 30, 8000, htk=True); default: restated natively, rvc_amd/melbasis.py)
+ * and "window" f32 [1024] (torch.hann_window(1024); default: computed natively).
+ *   rvc_rmvpe_forward: wav f32 [B][N] (device) -> salience f32 [B][360][Tp], Tp = rvc_rmvpe_salience_ld(N)
+ *   (frames rounded up to 32); mel -> U-Net -> BiGRU -> Linear + sigmoid.  The first rvc_rmvpe_frames(N)
+ *   columns decode with rvc_rmvpe_decode (ld = Tp) into f0 / coarse / pitchf.  Always f32-accurate arithmetic
+ *   (the f0 is a per-frame decision, as rvc_amd/rmvpe.py).
+ *   rvc_rmvpe_check: synchronises; returns RVC_EHIP (and clears the flag) if a BiGRU hand-off timed out since
+ *   the last check (that salience is invalid), else RVC_OK. */
+int rvc_load_rmvpe(rvc_ctx* ctx, const rvc_param* params, int n);
+int64_t rvc_rmvpe_frames(int64_t n16k);
+int64_t rvc_rmvpe_salience_ld(int64_t n16k);
+int rvc_rmvpe_forward(rvc_ctx* ctx, const float* wav, int64_t B, int64_t N, float* salience, rvc_stream_t stream);
+int rvc_rmvpe_check(rvc_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

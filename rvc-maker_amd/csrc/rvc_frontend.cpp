@@ -1,0 +1,672 @@
+// Model-level C ABI, front end (include/rvc_amd.h): ContentVec (rvc_amd/contentvec.py) and
+// RMVPE (rvc_amd/rmvpe.py) loaded from their checkpoints' named host arrays and run natively with the same
+// launches, pass sets and order as the Python models -- bit-identical to them on the same weights and
+// constants.  Scratch per model is sized by a dry run of the forward (Scratch / RUN in model_common.h).
+#include "model_common.h"
+
+using namespace rvcm;
+
+namespace fem {
+
+constexpr int kMels = 128, kClass = 360, kNfft = 1024, kHop = 160;
+constexpr int kFeLayers[7][3] = {{512, 10, 5}, {512, 3, 2}, {512, 3, 2}, {512, 3, 2}, {512, 3, 2}, {512, 2, 2}, {512, 2, 2}};
+
+struct CvLayer {
+    ConvW qkv, o, fc1, fc2;
+    float *ln1g = nullptr, *ln1b = nullptr, *ln2g = nullptr, *ln2b = nullptr;
+};
+
+// ConvBlockRes (RMVPE.py:11-44) with BatchNorm folded: conv.0 -> ReLU, conv.3 -> ReLU + shortcut
+struct Cbr {
+    ConvW c0, c3, sc;
+    bool has_sc = false;
+};
+
+struct ConvT2d {  // ConvTranspose2d(3, stride 2, pad 1, out pad 1) + BN + ReLU as 4 phase convs
+    ConvW ph[4];
+    int ntap[4];
+    int dy[4][4], dx[4][4];
+    int64_t Co = 0;
+};
+
+}  // namespace fem
+
+struct ContentVec : ModelBase {
+    int E = 768, heads = 12;
+    ConvW fe[7], proj, pos_conv, final_proj;
+    float *gn_w = nullptr, *gn_b = nullptr, *ln_w = nullptr, *ln_b = nullptr, *enc_ln_w = nullptr, *enc_ln_b = nullptr;
+    std::vector<fem::CvLayer> layers;
+};
+
+struct Rmvpe : ModelBase {
+    ConvW dft, mel, cnn, w_ih, fc;
+    float in_scale = 1.f, in_shift = 0.f;
+    float *window = nullptr, *w_hh = nullptr, *b_hh = nullptr;
+    std::vector<std::vector<fem::Cbr>> enc, inter;  // [level][block]
+    std::vector<fem::ConvT2d> dec_t;
+    std::vector<std::vector<fem::Cbr>> dec;
+    void* gran = nullptr;
+    int* err = nullptr;
+};
+
+void contentvec_delete(ContentVec* m) {
+    if (!m) return;
+    m->release();
+    delete m;
+}
+
+void rmvpe_delete(Rmvpe* m) {
+    if (!m) return;
+    m->release();
+    delete m;
+}
+
+namespace fem {
+
+using rvcm::HostT;
+
+int64_t cv_frames(int64_t n) {
+    for (auto& l : kFeLayers) n = (n - l[1]) / l[2] + 1;
+    return n;
+}
+
+// ------------------------------------------------------------------ ContentVec forward, one sequence
+int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, int out_layer, int final_proj,
+           float* feats, hipStream_t s) {
+    const int64_t E = M.E;
+    // feature extractor (fairseq.py:1165-1195): conv(k10 s5) + GroupNorm + GELU, then conv + GELU
+    int64_t L = N;
+    const float* x = wav;
+    float* bufs[2];
+    const int64_t L0 = (N - kFeLayers[0][1]) / kFeLayers[0][2] + 1;
+    bufs[0] = sc.take(512 * L0);
+    bufs[1] = sc.take(512 * L0);
+    for (int i = 0; i < 7; ++i) {
+        const int k = kFeLayers[i][1], st = kFeLayers[i][2];
+        const int64_t Lo = (L - k) / st + 1;
+        float* y = bufs[i & 1];
+        CallOpts o;
+        o.stride = st;
+        if (i > 0) o.out_act = RVC_ACT_GELU;
+        RUN(conv(c, M, M.fe[i], x, L, y, o, s));
+        if (i == 0) RUN(rvc_chnorm_gelu(y, M.gn_w, M.gn_b, y, 1, 512, Lo, 1e-5f, 1, s));
+        x = y;
+        L = Lo;
+    }
+    const int64_t T = L;
+    float* x512 = bufs[(7 - 1) & 1];  // layer 6's output
+    RUN(rvc_layernorm_cf(x512, nullptr, M.ln_w, M.ln_b, x512, 1, 512, T, 1e-5f, s));
+    float* xp = sc.take(E * T);
+    {
+        CallOpts o;
+        RUN(conv(c, M, M.proj, x512, T, xp, o, s));
+    }
+    float* xe = sc.take(E * T);
+    {
+        CallOpts o;  // pos_conv: SamePad drops the last column; GELU then + x (fairseq.py:585-592)
+        o.pad = M.pos_conv.K / 2;
+        o.Lout = T;
+        o.out_act = RVC_ACT_GELU;
+        o.res = xp;
+        RUN(conv(c, M, M.pos_conv, xp, T, xe, o, s));
+    }
+    RUN(rvc_layernorm_cf(xe, nullptr, M.enc_ln_w, M.enc_ln_b, xe, 1, E, T, 1e-5f, s));
+    const int64_t H = M.heads, D = E / H;
+    float* qkv = sc.take(3 * E * T);
+    float* ob = sc.take(E * T);
+    float* yb = sc.take(E * T);
+    float* hb = sc.take(M.layers[0].fc1.Co * T);
+    const int nl = out_layer < (int)M.layers.size() ? out_layer : (int)M.layers.size();
+    for (int li = 0; li < nl; ++li) {
+        const CvLayer& Ly = M.layers[li];
+        CallOpts o;
+        RUN(conv(c, M, Ly.qkv, xe, T, qkv, o, s));
+        rvc_attn_args at;
+        memset(&at, 0, sizeof(at));
+        at.q = qkv;
+        at.k = qkv + E * T;
+        at.v = qkv + 2 * E * T;
+        at.o = ob;
+        at.B = 1;
+        at.H = H;
+        at.D = D;
+        at.T = T;
+        at.ldc = T;
+        at.q_hs = at.k_hs = at.v_hs = at.o_hs = D * T;
+        at.q_bs = at.k_bs = at.v_bs = 3 * E * T;
+        at.o_bs = E * T;
+        at.scale = (float)pow((double)D, -0.5);
+        if (!sc.dry) {
+            const int64_t need = rvc_attention_workspace_bytes(&at);
+            MCHECK(need >= 0, "rvc_contentvec_forward: attention shape H=%lld D=%lld T=%lld unsupported", (long long)H,
+                   (long long)D, (long long)T);
+            MTRY(ensure_ws(M, need, s));
+            MTRY(rvc_attention(&at, need ? M.ws : nullptr, need, s));
+        }
+        RUN(conv(c, M, Ly.o, ob, T, yb, o, s));
+        RUN(rvc_layernorm_cf(xe, yb, Ly.ln1g, Ly.ln1b, xe, 1, E, T, 1e-5f, s));
+        CallOpts og;
+        og.out_act = RVC_ACT_GELU;
+        RUN(conv(c, M, Ly.fc1, xe, T, hb, og, s));
+        RUN(conv(c, M, Ly.fc2, hb, T, yb, o, s));
+        RUN(rvc_layernorm_cf(xe, yb, Ly.ln2g, Ly.ln2b, xe, 1, E, T, 1e-5f, s));
+    }
+    if (final_proj) {
+        float* fp = sc.take(M.final_proj.Co * T);
+        CallOpts o;
+        RUN(conv(c, M, M.final_proj, xe, T, fp, o, s));
+        RUN(rvc_transpose(fp, feats, 1, M.final_proj.Co, T, s));
+    } else {
+        RUN(rvc_transpose(xe, feats, 1, E, T, s));
+    }
+    return RVC_OK;
+}
+
+// ------------------------------------------------------------------ RMVPE pieces
+// _fold_bn (rmvpe.py): s = g / sqrt(v + eps), shift = b - m s, in f64
+int fold_bn(Params& P, const std::string& name, std::vector<double>& sc, std::vector<double>& sh) {
+    HostT g, b, m, v;
+    MCHECK(P.get(name + ".weight", g) && P.get(name + ".bias", b) && P.get(name + ".running_mean", m) &&
+               P.get(name + ".running_var", v),
+           "rvc_load_rmvpe: missing %s", P.missing.c_str());
+    sc.resize(g.v.size());
+    sh.resize(g.v.size());
+    for (size_t i = 0; i < g.v.size(); ++i) {
+        sc[i] = (double)g.v[i] / sqrt((double)v.v[i] + 1e-5);
+        sh[i] = (double)b.v[i] - (double)m.v[i] * sc[i];
+    }
+    return RVC_OK;
+}
+
+// 3x3 / 1x1 Conv2d weight [Co][Ci][kh][kw] (optionally scaled per output channel) as a K = kh*kw conv
+int make_conv2d(rvc_ctx* c, Rmvpe& M, const HostT& w, const std::vector<double>* scale, const std::vector<float>& bias,
+                ConvW& cw) {
+    HostT w3;
+    w3.shape = {w.dim(0), w.dim(1), w.dim(2) * w.dim(3)};
+    w3.v.resize(w.v.size());
+    const int64_t inner = (int64_t)w.v.size() / w.dim(0);
+    for (int64_t co = 0; co < w.dim(0); ++co)
+        for (int64_t j = 0; j < inner; ++j)
+            w3.v[co * inner + j] = scale ? (float)((double)w.v[co * inner + j] * (*scale)[co]) : w.v[co * inner + j];
+    HostT b;
+    b.v = bias;
+    b.shape = {(int64_t)bias.size()};
+    return make_conv(c, M, w3, &b, cw);
+}
+
+int make_cbr(rvc_ctx* c, Rmvpe& M, Params& P, const std::string& p, Cbr& blk) {
+    const char* convs[2][2] = {{"conv.0", "conv.1"}, {"conv.3", "conv.4"}};
+    for (int i = 0; i < 2; ++i) {
+        std::vector<double> s, t;
+        MTRY(fold_bn(P, p + "." + convs[i][1], s, t));
+        HostT w;
+        MCHECK(P.get(p + "." + convs[i][0] + ".weight", w), "rvc_load_rmvpe: missing %s", P.missing.c_str());
+        std::vector<float> bf(t.begin(), t.end());
+        MTRY(make_conv2d(c, M, w, &s, bf, i == 0 ? blk.c0 : blk.c3));
+    }
+    if (P.has(p + ".shortcut.weight")) {
+        HostT w, b;
+        MCHECK(P.get(p + ".shortcut.weight", w) && P.get(p + ".shortcut.bias", b), "rvc_load_rmvpe: missing %s",
+               P.missing.c_str());
+        MTRY(make_conv2d(c, M, w, nullptr, b.v, blk.sc));
+        blk.has_sc = true;
+    }
+    return RVC_OK;
+}
+
+int make_convT2d(rvc_ctx* c, Rmvpe& M, Params& P, const std::string& p, ConvT2d& ct) {
+    std::vector<double> s, t;
+    MTRY(fold_bn(P, p + ".conv1.1", s, t));
+    HostT w;
+    MCHECK(P.get(p + ".conv1.0.weight", w), "rvc_load_rmvpe: missing %s", P.missing.c_str());
+    const int64_t Ci = w.dim(0), Co = w.dim(1);
+    ct.Co = Co;
+    // per output parity: (kernel index, source offset) -- rmvpe.py _ConvT2d.TAPS
+    const int tk[2][2] = {{1, -1}, {0, 2}}, td[2][2] = {{0, 0}, {1, 0}}, tn[2] = {1, 2};
+    HostT bias;
+    bias.v.assign(t.begin(), t.end());
+    bias.shape = {Co};
+    int ph = 0;
+    for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px, ++ph) {
+            int n = 0;
+            HostT wp;
+            const int nt = tn[py] * tn[px];
+            wp.shape = {Co, Ci, nt};
+            wp.v.resize(Co * Ci * nt);
+            for (int a = 0; a < tn[py]; ++a)
+                for (int b2 = 0; b2 < tn[px]; ++b2, ++n) {
+                    const int ky = tk[py][a], kx = tk[px][b2];
+                    ct.dy[ph][n] = td[py][a];
+                    ct.dx[ph][n] = td[px][b2];
+                    for (int64_t co = 0; co < Co; ++co)
+                        for (int64_t ci = 0; ci < Ci; ++ci)
+                            wp.v[(co * Ci + ci) * nt + n] = (float)((double)w.v[((ci * Co + co) * 3 + ky) * 3 + kx] * s[co]);
+                }
+            ct.ntap[ph] = nt;
+            MTRY(make_conv(c, M, wp, &bias, ct.ph[ph]));
+        }
+    return RVC_OK;
+}
+
+// _Conv2d.__call__ on bordered [C][H+2][W+2] images
+int conv2d(rvc_ctx* c, Rmvpe& M, const ConvW& cw, const float* x, int64_t H, int64_t W, float* out, int out_act,
+           const float* res, hipStream_t s) {
+    const int64_t wrap = W + 2, L = (H + 2) * wrap;
+    CallOpts o;
+    o.Lout = L;
+    o.wrap = (int)wrap;
+    o.out_act = out_act;
+    o.res = res;
+    if (cw.K == 9) {
+        o.ntoff = 9;
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx) o.toff[dy * 3 + dx] = (int)(dy * wrap + dx);
+        o.pad = (int)(wrap + 1);
+    } else {
+        o.ntoff = 1;
+        o.toff[0] = 0;
+        o.pad = 0;
+    }
+    return conv(c, M, cw, x, L, out, o, s);
+}
+
+int cbr_run(rvc_ctx* c, Rmvpe& M, Scratch& sc, const Cbr& blk, const float* x, int64_t H, int64_t W, float* out,
+            hipStream_t s) {
+    const int64_t img = (H + 2) * (W + 2);
+    float* h = sc.take(blk.c0.Co * img);
+    RUN(conv2d(c, M, blk.c0, x, H, W, h, RVC_ACT_RELU, nullptr, s));
+    const float* res = x;
+    if (blk.has_sc) {
+        float* scb = sc.take(blk.c0.Co * img);
+        RUN(conv2d(c, M, blk.sc, x, H, W, scb, RVC_ACT_NONE, nullptr, s));
+        res = scb;
+    }
+    RUN(conv2d(c, M, blk.c3, h, H, W, out, RVC_ACT_RELU, res, s));
+    return RVC_OK;
+}
+
+// mel -> U-Net -> BiGRU -> fc for one sequence (rmvpe.py f0_device up to the decode)
+int rm_one(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, float* sal, hipStream_t s) {
+    const int64_t F = 1 + N / kHop, Tp = 32 * ((F - 1) / 32 + 1);
+    // MelSpectrogram.forward (RMVPE.py:162-181)
+    float* frames = sc.take((int64_t)kNfft * F);
+    RUN(rvc_stft_frames(wav, M.window, frames, N, F, kNfft, kHop, s));
+    float* spec = sc.take((int64_t)(kNfft + 2) * F);
+    {
+        CallOpts o;
+        RUN(conv(c, M, M.dft, frames, F, spec, o, s));
+    }
+    float* mag = sc.take((int64_t)(kNfft / 2 + 1) * F);
+    RUN(rvc_spec_mag(spec, mag, kNfft / 2 + 1, F, s));
+    float* mel = sc.take((int64_t)kMels * F);
+    {
+        CallOpts o;
+        o.out_act = RVC_ACT_LOGCLAMP;
+        o.out_slope = 1e-5f;
+        RUN(conv(c, M, M.mel, mag, F, mel, o, s));
+    }
+    // mel2hidden input image (RMVPE.py:210-213)
+    int64_t H = Tp, W = kMels;
+    float* x = sc.take((H + 2) * (W + 2));
+    RUN(hipMemsetAsync(x, 0, (H + 2) * (W + 2) * 4, s) == hipSuccess ? RVC_OK : RVC_EHIP);
+    RUN(rvc_mel_image(mel, x, kMels, F, Tp, M.in_scale, M.in_shift, s));
+    // encoder (RMVPE.py:64-76): the last block of each level writes into the decoder's concat buffer
+    struct Cat {
+        float* buf;
+        int64_t C, H, W;
+    };
+    std::vector<Cat> cats;
+    int64_t C = M.enc[0][0].c0.Co;
+    const int nb = (int)M.enc[0].size();
+    for (size_t l = 0; l < M.enc.size(); ++l) {
+        const int64_t img = (H + 2) * (W + 2);
+        float* cat = sc.take(2 * C * img);
+        RUN(hipMemsetAsync(cat, 0, 2 * C * img * 4, s) == hipSuccess ? RVC_OK : RVC_EHIP);
+        for (int b = 0; b < nb; ++b) {
+            float* out = b == nb - 1 ? cat + C * img : sc.take(C * img);
+            MTRY(cbr_run(c, M, sc, M.enc[l][b], x, H, W, out, s));
+            x = out;
+        }
+        cats.push_back({cat, C, H, W});
+        float* pooled = sc.take(C * (H / 2 + 2) * (W / 2 + 2));
+        RUN(hipMemsetAsync(pooled, 0, C * (H / 2 + 2) * (W / 2 + 2) * 4, s) == hipSuccess ? RVC_OK : RVC_EHIP);
+        RUN(rvc_avgpool2(x, pooled, C, H, W, s));
+        x = pooled;
+        H /= 2;
+        W /= 2;
+        C *= 2;
+    }
+    for (auto& layer : M.inter)
+        for (auto& blk : layer) {
+            float* out = sc.take(blk.c0.Co * (H + 2) * (W + 2));
+            MTRY(cbr_run(c, M, sc, blk, x, H, W, out, s));
+            x = out;
+        }
+    // decoder (RMVPE.py:78-107)
+    for (size_t i = 0; i < M.dec_t.size(); ++i) {
+        const Cat& ct = cats[cats.size() - 1 - i];
+        const ConvT2d& T2 = M.dec_t[i];
+        const int64_t wrap = W + 2, Lc = (H + 2) * wrap;
+        float* ph = sc.take(4 * T2.Co * Lc);
+        for (int p = 0; p < 4; ++p) {
+            CallOpts o;
+            o.Lout = Lc;
+            o.wrap = (int)wrap;
+            o.out_act = RVC_ACT_RELU;
+            o.ntoff = T2.ntap[p];
+            for (int t = 0; t < T2.ntap[p]; ++t) o.toff[t] = (int)(T2.dy[p][t] * wrap + T2.dx[p][t]);
+            RUN(conv(c, M, T2.ph[p], x, Lc, ph + p * T2.Co * Lc, o, s));
+        }
+        RUN(rvc_interleave4(ph, ct.buf, T2.Co, H, W, s));
+        x = ct.buf;
+        H = ct.H;
+        W = ct.W;
+        for (auto& blk : M.dec[i]) {
+            float* out = sc.take(blk.c0.Co * (H + 2) * (W + 2));
+            MTRY(cbr_run(c, M, sc, blk, x, H, W, out, s));
+            x = out;
+        }
+    }
+    float* img = sc.take(3 * (H + 2) * (W + 2));
+    RUN(conv2d(c, M, M.cnn, x, H, W, img, RVC_ACT_NONE, nullptr, s));
+    float* seq = sc.take(3 * W * H);
+    RUN(rvc_img_to_seq(img, seq, 3, H, W, s));
+    // BiGRU + Linear + sigmoid (RMVPE.py:254-260, 141)
+    float* gi = sc.take(1536 * Tp);
+    {
+        CallOpts o;
+        RUN(conv(c, M, M.w_ih, seq, Tp, gi, o, s));
+    }
+    float* y = sc.take(512 * Tp);
+    RUN(rvc_bigru(gi, M.w_hh, M.b_hh, y, M.gran, M.err, Tp, s));
+    CallOpts o;
+    o.out_act = RVC_ACT_SIGMOID;
+    RUN(conv(c, M, M.fc, y, Tp, sal, o, s));
+    return RVC_OK;
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+// ------------------------------------------------------------------ C ABI
+extern "C" int64_t rvc_contentvec_frames(int64_t n16k) { return n16k >= 400 ? cv_frames(n16k) : 0; }
+
+extern "C" int rvc_load_contentvec(rvc_ctx* c, const rvc_param* params, int n, const rvc_contentvec_cfg* cfg) {
+    MCHECK(c && params && n > 0 && cfg, "rvc_load_contentvec: null argument");
+    MCHECK(cfg->encoder_embed_dim > 0 && cfg->encoder_attention_heads > 0 &&
+               cfg->encoder_embed_dim % cfg->encoder_attention_heads == 0 && cfg->conv_pos_groups > 0,
+           "rvc_load_contentvec: bad cfg");
+    Params P;
+    P.wn_dim = 2;  // encoder.pos_conv: weight_norm(dim=2) (fairseq.py:585-592)
+    MTRY(index_params(params, n, P, "rvc_load_contentvec"));
+    MHIP(hipSetDevice(c->device));
+    contentvec_delete(c->cv);
+    c->cv = new ContentVec();
+    ContentVec& M = *c->cv;
+    M.E = cfg->encoder_embed_dim;
+    M.heads = cfg->encoder_attention_heads;
+    HostT w, b;
+#define GET(k, t) MCHECK(P.get(k, t), "rvc_load_contentvec: missing %s", P.missing.c_str())
+    for (int i = 0; i < 7; ++i) {
+        GET("feature_extractor.conv_layers." + std::to_string(i) + ".0.weight", w);
+        MTRY(make_conv(c, M, w, nullptr, M.fe[i]));
+    }
+    GET("feature_extractor.conv_layers.0.2.weight", w);
+    MTRY(upload(M, w.v, &M.gn_w));
+    GET("feature_extractor.conv_layers.0.2.bias", w);
+    MTRY(upload(M, w.v, &M.gn_b));
+    GET("layer_norm.weight", w);
+    MTRY(upload(M, w.v, &M.ln_w));
+    GET("layer_norm.bias", w);
+    MTRY(upload(M, w.v, &M.ln_b));
+    GET("post_extract_proj.weight", w);
+    GET("post_extract_proj.bias", b);
+    w.shape.push_back(1);
+    MTRY(make_conv(c, M, w, &b, M.proj));
+    GET("encoder.pos_conv.0.weight", w);
+    GET("encoder.pos_conv.0.bias", b);
+    MTRY(make_conv(c, M, w, &b, M.pos_conv, cfg->conv_pos_groups));
+    GET("encoder.layer_norm.weight", w);
+    MTRY(upload(M, w.v, &M.enc_ln_w));
+    GET("encoder.layer_norm.bias", w);
+    MTRY(upload(M, w.v, &M.enc_ln_b));
+    for (int i = 0; P.has("encoder.layers." + std::to_string(i) + ".fc1.weight"); ++i) {
+        const std::string p = "encoder.layers." + std::to_string(i) + ".";
+        CvLayer Ly;
+        HostT wq, wk, wv, bq, bk, bv;
+        GET(p + "self_attn.q_proj.weight", wq);
+        GET(p + "self_attn.k_proj.weight", wk);
+        GET(p + "self_attn.v_proj.weight", wv);
+        GET(p + "self_attn.q_proj.bias", bq);
+        GET(p + "self_attn.k_proj.bias", bk);
+        GET(p + "self_attn.v_proj.bias", bv);
+        wq.v.insert(wq.v.end(), wk.v.begin(), wk.v.end());
+        wq.v.insert(wq.v.end(), wv.v.begin(), wv.v.end());
+        wq.shape = {wq.dim(0) + wk.dim(0) + wv.dim(0), wq.dim(1), 1};
+        bq.v.insert(bq.v.end(), bk.v.begin(), bk.v.end());
+        bq.v.insert(bq.v.end(), bv.v.begin(), bv.v.end());
+        MTRY(make_conv(c, M, wq, &bq, Ly.qkv));
+        const char* lin[3][2] = {{"self_attn.out_proj", "o"}, {"fc1", "fc1"}, {"fc2", "fc2"}};
+        ConvW* dst[3] = {&Ly.o, &Ly.fc1, &Ly.fc2};
+        for (int j = 0; j < 3; ++j) {
+            GET(p + lin[j][0] + ".weight", w);
+            GET(p + lin[j][0] + ".bias", b);
+            w.shape.push_back(1);
+            MTRY(make_conv(c, M, w, &b, *dst[j]));
+        }
+        GET(p + "self_attn_layer_norm.weight", w);
+        MTRY(upload(M, w.v, &Ly.ln1g));
+        GET(p + "self_attn_layer_norm.bias", w);
+        MTRY(upload(M, w.v, &Ly.ln1b));
+        GET(p + "final_layer_norm.weight", w);
+        MTRY(upload(M, w.v, &Ly.ln2g));
+        GET(p + "final_layer_norm.bias", w);
+        MTRY(upload(M, w.v, &Ly.ln2b));
+        M.layers.push_back(Ly);
+    }
+    MCHECK(!M.layers.empty(), "rvc_load_contentvec: no encoder.layers.*");
+    GET("final_proj.weight", w);
+    GET("final_proj.bias", b);
+    w.shape.push_back(1);
+    MTRY(make_conv(c, M, w, &b, M.final_proj));
+#undef GET
+    MHIP(hipDeviceSynchronize());
+    M.loaded = true;
+    return RVC_OK;
+}
+
+extern "C" int rvc_contentvec_forward(rvc_ctx* c, const float* wav, int64_t B, int64_t N, int out_layer, int final_proj,
+                                      float* feats, rvc_stream_t stream) {
+    MCHECK(c && c->cv && c->cv->loaded, "rvc_contentvec_forward: no ContentVec loaded");
+    MCHECK(wav && feats && B >= 1 && out_layer >= 1, "rvc_contentvec_forward: bad arguments");
+    const int64_t T = rvc_contentvec_frames(N);
+    MCHECK(T >= 1, "rvc_contentvec_forward: input of %lld samples is shorter than one frame", (long long)N);
+    hipStream_t s = (hipStream_t)stream;
+    MHIP(hipSetDevice(c->device));
+    ContentVec& M = *c->cv;
+    Scratch sc;
+    MTRY(cv_one(c, M, sc, wav, N, out_layer, final_proj, feats, s));  // dry: size the scratch
+    MTRY(ensure_arena(M, sc.off, s));
+    const int64_t Cout = final_proj ? M.final_proj.Co : M.E;
+    for (int64_t b = 0; b < B; ++b) {
+        Scratch run;
+        run.dry = false;
+        run.base = M.arena;
+        MTRY(cv_one(c, M, run, wav + b * N, N, out_layer, final_proj, feats + b * T * Cout, s));
+    }
+    return RVC_OK;
+}
+
+extern "C" int64_t rvc_rmvpe_frames(int64_t n16k) { return n16k >= 0 ? 1 + n16k / kHop : -1; }
+
+extern "C" int64_t rvc_rmvpe_salience_ld(int64_t n16k) {
+    const int64_t F = rvc_rmvpe_frames(n16k);
+    return F > 0 ? 32 * ((F - 1) / 32 + 1) : -1;
+}
+
+extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
+    MCHECK(c && params && n > 0, "rvc_load_rmvpe: null argument");
+    Params P;
+    MTRY(index_params(params, n, P, "rvc_load_rmvpe"));
+    MHIP(hipSetDevice(c->device));
+    rmvpe_delete(c->rm);
+    c->rm = new Rmvpe();
+    Rmvpe& M = *c->rm;
+    HostT w, b;
+#define GET(k, t) MCHECK(P.get(k, t), "rvc_load_rmvpe: missing %s", P.missing.c_str())
+    // constants: Hann window, DFT basis, mel basis (rmvpe.py __init__, melbasis.py)
+    if (P.has("window")) {
+        GET("window", w);
+        MCHECK((int64_t)w.v.size() == kNfft, "rvc_load_rmvpe: window must have %d entries", kNfft);
+    } else {
+        w.v.resize(kNfft);  // torch.hann_window's float32 steps (periodic: n * 2 pi / N, cos, * -0.5, + 0.5)
+        const float step = (float)(M_PI * 2.0 / kNfft);
+        for (int i = 0; i < kNfft; ++i) {
+#pragma clang fp contract(off)
+            const float cs = (float)cos((double)((float)i * step));
+            const float t = cs * -0.5f;
+            w.v[i] = t + 0.5f;
+        }
+    }
+    MTRY(upload(M, w.v, &M.window));
+    {
+        HostT d;
+        d.shape = {kNfft + 2, kNfft, 1};
+        d.v.resize((size_t)(kNfft + 2) * kNfft);
+        for (int k = 0; k <= kNfft / 2; ++k)
+            for (int i = 0; i < kNfft; ++i) {
+                const double ang = 2.0 * M_PI * (double)((int64_t)k * i) / kNfft;
+                d.v[(size_t)k * kNfft + i] = (float)cos(ang);
+                d.v[(size_t)(k + kNfft / 2 + 1) * kNfft + i] = (float)-sin(ang);
+            }
+        MTRY(make_conv(c, M, d, nullptr, M.dft));
+    }
+    HostT mb;
+    if (P.has("mel_basis")) {
+        GET("mel_basis", mb);
+        MCHECK(mb.dim(0) == kMels && mb.dim(1) == kNfft / 2 + 1, "rvc_load_rmvpe: mel_basis must be [128][513]");
+    } else {  // librosa.filters.mel(16000, 1024, 128, 30, 8000, htk=True), Slaney norm (melbasis.py)
+        const int nb = kNfft / 2 + 1;
+        auto hz2mel = [](double f) { return 2595.0 * log10(1.0 + f / 700.0); };
+        auto mel2hz = [](double m) { return 700.0 * (pow(10.0, m / 2595.0) - 1.0); };
+        const double m0 = hz2mel(30.0), m1 = hz2mel(8000.0), step = (m1 - m0) / (kMels + 1);
+        std::vector<double> mf(kMels + 2), ff(nb);
+        for (int i = 0; i < kMels + 2; ++i) mf[i] = mel2hz(i == kMels + 1 ? m1 : i * step + m0);
+        const double val = 1.0 / (kNfft * (1.0 / 16000.0));
+        for (int k = 0; k < nb; ++k) ff[k] = k * val;
+        mb.shape = {kMels, nb};
+        mb.v.resize((size_t)kMels * nb);
+        for (int i = 0; i < kMels; ++i) {
+            const double enorm = 2.0 / (mf[i + 2] - mf[i]);
+            for (int k = 0; k < nb; ++k) {
+                const double lower = -(mf[i] - ff[k]) / (mf[i + 1] - mf[i]);
+                const double upper = (mf[i + 2] - ff[k]) / (mf[i + 2] - mf[i + 1]);
+                const float wt = (float)fmax(0.0, fmin(lower, upper));
+                mb.v[(size_t)i * nb + k] = (float)((double)wt * enorm);
+            }
+        }
+    }
+    mb.shape.push_back(1);
+    MTRY(make_conv(c, M, mb, nullptr, M.mel));
+    {
+        std::vector<double> s, t;
+        MTRY(fold_bn(P, "unet.encoder.bn", s, t));
+        M.in_scale = (float)s[0];
+        M.in_shift = (float)t[0];
+    }
+    const int nblk = 4;  // E2E(4, 1, (2, 2))
+    for (int l = 0; P.has("unet.encoder.layers." + std::to_string(l) + ".conv.0.conv.0.weight"); ++l) {
+        M.enc.emplace_back(nblk);
+        for (int bb = 0; bb < nblk; ++bb)
+            MTRY(make_cbr(c, M, P, "unet.encoder.layers." + std::to_string(l) + ".conv." + std::to_string(bb),
+                          M.enc.back()[bb]));
+    }
+    for (int l = 0; P.has("unet.intermediate.layers." + std::to_string(l) + ".conv.0.conv.0.weight"); ++l) {
+        M.inter.emplace_back(nblk);
+        for (int bb = 0; bb < nblk; ++bb)
+            MTRY(make_cbr(c, M, P, "unet.intermediate.layers." + std::to_string(l) + ".conv." + std::to_string(bb),
+                          M.inter.back()[bb]));
+    }
+    for (int l = 0; P.has("unet.decoder.layers." + std::to_string(l) + ".conv1.0.weight"); ++l) {
+        const std::string p = "unet.decoder.layers." + std::to_string(l);
+        M.dec_t.emplace_back();
+        MTRY(make_convT2d(c, M, P, p, M.dec_t.back()));
+        M.dec.emplace_back(nblk);
+        for (int bb = 0; bb < nblk; ++bb) MTRY(make_cbr(c, M, P, p + ".conv2." + std::to_string(bb), M.dec.back()[bb]));
+    }
+    MCHECK(M.enc.size() == 5 && M.dec.size() == 5 && M.enc[0][0].c0.Ci == 1,
+           "rvc_load_rmvpe: expected the E2E(4, 1, (2, 2)) U-Net (5 encoder / decoder levels)");
+    GET("cnn.weight", w);
+    GET("cnn.bias", b);
+    MTRY(make_conv2d(c, M, w, nullptr, b.v, M.cnn));
+    const std::string g = "fc.0.gru.";
+    HostT wi, wir, bi, bir;
+    GET(g + "weight_ih_l0", wi);
+    GET(g + "weight_ih_l0_reverse", wir);
+    GET(g + "bias_ih_l0", bi);
+    GET(g + "bias_ih_l0_reverse", bir);
+    MCHECK(wi.dim(0) == 768 && wi.dim(1) == 384, "rvc_load_rmvpe: GRU(384, 256) expected");
+    wi.v.insert(wi.v.end(), wir.v.begin(), wir.v.end());
+    wi.shape = {1536, 384, 1};
+    bi.v.insert(bi.v.end(), bir.v.begin(), bir.v.end());
+    MTRY(make_conv(c, M, wi, &bi, M.w_ih));
+    HostT wh, whr, bh, bhr;
+    GET(g + "weight_hh_l0", wh);
+    GET(g + "weight_hh_l0_reverse", whr);
+    GET(g + "bias_hh_l0", bh);
+    GET(g + "bias_hh_l0_reverse", bhr);
+    wh.v.insert(wh.v.end(), whr.v.begin(), whr.v.end());
+    bh.v.insert(bh.v.end(), bhr.v.begin(), bhr.v.end());
+    MTRY(upload(M, wh.v, &M.w_hh));
+    MTRY(upload(M, bh.v, &M.b_hh));
+    GET("fc.1.weight", w);
+    GET("fc.1.bias", b);
+    MCHECK(w.dim(0) == kClass && w.dim(1) == 512, "rvc_load_rmvpe: fc.1 must be Linear(512, 360)");
+    w.shape.push_back(1);
+    MTRY(make_conv(c, M, w, &b, M.fc));
+#undef GET
+    MTRY(dev_alloc(M, 8192, &M.gran));
+    MTRY(dev_alloc(M, 4, (void**)&M.err));
+    MHIP(hipMemset(M.err, 0, 4));
+    MHIP(hipDeviceSynchronize());
+    M.loaded = true;
+    return RVC_OK;
+}
+
+extern "C" int rvc_rmvpe_forward(rvc_ctx* c, const float* wav, int64_t B, int64_t N, float* salience,
+                                 rvc_stream_t stream) {
+    MCHECK(c && c->rm && c->rm->loaded, "rvc_rmvpe_forward: no RMVPE loaded");
+    MCHECK(wav && salience && B >= 1 && N >= 1, "rvc_rmvpe_forward: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    MHIP(hipSetDevice(c->device));
+    Rmvpe& M = *c->rm;
+    const int prev = c->prec;
+    c->prec = RVC_PREC_FP32;  // f32-accurate whatever the context's precision (rmvpe.py: self.precision)
+    Scratch sc;
+    int rc = rm_one(c, M, sc, wav, N, salience, s);
+    if (rc == RVC_OK) rc = ensure_arena(M, sc.off, s);
+    const int64_t ld = rvc_rmvpe_salience_ld(N);
+    for (int64_t b = 0; b < B && rc == RVC_OK; ++b) {
+        Scratch run;
+        run.dry = false;
+        run.base = M.arena;
+        rc = rm_one(c, M, run, wav + b * N, N, salience + b * kClass * ld, s);
+    }
+    c->prec = prev;
+    return rc;
+}
+
+extern "C" int rvc_rmvpe_check(rvc_ctx* c) {
+    MCHECK(c && c->rm && c->rm->loaded, "rvc_rmvpe_check: no RMVPE loaded");
+    MHIP(hipSetDevice(c->device));
+    int e = 0;
+    MHIP(hipMemcpy(&e, c->rm->err, 4, hipMemcpyDeviceToHost));
+    if (e != 0) {
+        MHIP(hipMemset(c->rm->err, 0, 4));
+        rvc_set_error("rvc_rmvpe_check: bigru recurrence timed out (granule hand-off stalled); salience invalid");
+        return RVC_EHIP;
+    }
+    return RVC_OK;
+}

@@ -8,120 +8,13 @@
 // (:449), flow^-1 (residuals.py:87-137, modules.py:9-59), NSF-HiFiGAN (synthesizers.py:114-168) -- with the
 // same pass-set choices (ops.conv_passes / rb_passes / resblock_fusable), so a model loaded from the same
 // fp32 weights gives bit-identical output to SynthesizerAMD.
-#include <hip/hip_runtime_api.h>
-#include <math.h>
-#include <stdint.h>
-#include <stdlib.h>
-#include <string.h>
+#include "model_common.h"
 
-#include <map>
-#include <string>
-#include <vector>
+using namespace rvcm;
 
-#include "../../include/rvc_amd.h"
-
-void rvc_set_error(const char* fmt, ...);
-
-#define MCHECK(cond, ...)             \
-    do {                              \
-        if (!(cond)) {                \
-            rvc_set_error(__VA_ARGS__); \
-            return RVC_EINVAL;        \
-        }                             \
-    } while (0)
-#define MHIP(call)                                                   \
-    do {                                                             \
-        hipError_t e_ = (call);                                      \
-        if (e_ != hipSuccess) {                                      \
-            rvc_set_error("%s: %s", #call, hipGetErrorString(e_));  \
-            return RVC_EHIP;                                         \
-        }                                                            \
-    } while (0)
-#define MTRY(call)                \
-    do {                          \
-        int rc_ = (call);         \
-        if (rc_ != RVC_OK) return rc_; \
-    } while (0)
-
-namespace {
+namespace synthm {
 
 constexpr float kLreluSlope = 0.1f;  // synthesizers.py LRELU_SLOPE
-
-// ------------------------------------------------------------------ host tensors
-struct HostT {
-    std::vector<float> v;
-    std::vector<int64_t> shape;
-    int64_t dim(int i) const { return i < (int)shape.size() ? shape[i] : 1; }
-};
-
-float half_to_float(uint16_t h) {
-    const uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 31, m = h & 1023;
-    uint32_t bits;
-    if (e == 0) {
-        if (m == 0) {
-            bits = s;
-        } else {  // subnormal: renormalise
-            int ee = -1;
-            uint32_t mm = m;
-            do {
-                ++ee;
-                mm <<= 1;
-            } while (!(mm & 1024));
-            bits = s | ((uint32_t)(127 - 15 - ee) << 23) | ((mm & 1023) << 13);
-        }
-    } else if (e == 31) {
-        bits = s | 0x7f800000u | (m << 13);
-    } else {
-        bits = s | ((e - 15 + 127) << 23) | (m << 13);
-    }
-    float f;
-    memcpy(&f, &bits, 4);
-    return f;
-}
-
-HostT to_host(const rvc_param& p) {
-    HostT t;
-    int64_t n = 1;
-    for (int i = 0; i < p.ndim; ++i) {
-        t.shape.push_back(p.shape[i]);
-        n *= p.shape[i];
-    }
-    t.v.resize(n);
-    if (p.dtype == RVC_DT_F16) {
-        const uint16_t* s = (const uint16_t*)p.data;
-        for (int64_t i = 0; i < n; ++i) t.v[i] = half_to_float(s[i]);
-    } else {
-        memcpy(t.v.data(), p.data, n * 4);
-    }
-    return t;
-}
-
-// torch._weight_norm(v, g, 0): w = v * (g / ||v||) with the norm over every dim but 0 (synth.py:fold_weight_norm)
-HostT fold_wn(const HostT& v, const HostT& g) {
-    HostT w = v;
-    const int64_t n0 = v.dim(0), inner = (int64_t)v.v.size() / n0;
-    for (int64_t i = 0; i < n0; ++i) {
-        double ss = 0;
-        for (int64_t j = 0; j < inner; ++j) ss += (double)v.v[i * inner + j] * v.v[i * inner + j];
-        const float nrm = (float)sqrt(ss);
-        const float f = g.v[i] / nrm;
-        for (int64_t j = 0; j < inner; ++j) w.v[i * inner + j] = v.v[i * inner + j] * f;
-    }
-    return w;
-}
-
-// ------------------------------------------------------------------ packed convs on the device
-struct ConvW {
-    int64_t Co = 0, Ci = 0;
-    int K = 0;       // taps per phase (ConvT: ceil(K/u))
-    int nphase = 1;  // ConvT: u phases
-    int Kfull = 0, u = 1, tpad = 0;
-    float* w = nullptr;  // KM [nphase][Ci*K][Co]
-    float* b = nullptr;
-    void* wx_bf = nullptr;  // split-bf16 image
-    void* wx_hf = nullptr;  // split-fp16 image
-    int nmf = 0;
-};
 
 struct Pair {
     int d;
@@ -138,115 +31,33 @@ struct Flow {
     ConvW ins[3], rs_a[2], rs_b[3];
 };
 
-struct Synth {
-    bool loaded = false;
+}  // namespace synthm
+
+struct Synth : ModelBase {
     rvc_synth_cfg cfg{};
     int emb_dim = 0, upp = 1, kc = 0;
     ConvW emb_phone, proj, cond, conv_pre, conv_post;
     float *emb_pitch = nullptr, *emb_g = nullptr;
     int64_t n_spk = 0;
-    std::vector<Layer> layers;
-    Flow flows[4];
+    std::vector<synthm::Layer> layers;
+    synthm::Flow flows[4];
     float lin_w = 0, lin_b = 0;
     std::vector<ConvW> ups;
     std::vector<ConvW> noise;
     std::vector<int> noise_stride, noise_pad, chans;
-    std::vector<std::vector<std::vector<Pair>>> res;  // [stage][block][pair]
+    std::vector<std::vector<std::vector<synthm::Pair>>> res;  // [stage][block][pair]
 };
 
-}  // namespace
 
-struct rvc_ctx {
-    int device = 0;
-    int prec = RVC_PREC_FP32;
-    bool x6 = true, f16mix = true, fused_rb = true;  // RVC_AMD_X6 / RVC_AMD_F16MIX / RVC_AMD_FUSED_RB as ops.py
-    std::vector<void*> allocs;                        // weights (freed with the model)
-    Synth syn;
-    void* ws = nullptr;  // split-K / split-KV scratch
-    int64_t ws_bytes = 0;
-    float* arena = nullptr;  // activations
-    int64_t arena_floats = 0;
-};
-
-namespace {
-
-int dev_alloc(rvc_ctx* c, size_t bytes, void** out) {
-    MHIP(hipMalloc(out, bytes ? bytes : 4));
-    c->allocs.push_back(*out);
-    return RVC_OK;
+void synth_delete(Synth* s) {
+    if (!s) return;
+    s->release();
+    delete s;
 }
 
-int upload(rvc_ctx* c, const std::vector<float>& h, float** out) {
-    MTRY(dev_alloc(c, h.size() * 4, (void**)out));
-    MHIP(hipMemcpy(*out, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    return RVC_OK;
-}
+namespace synthm {
 
-int make_images(rvc_ctx* c, ConvW& cw) {
-    if (!c->x6) return RVC_OK;
-    const int64_t nb = rvc_conv1d_x6_bytes(cw.nphase, cw.Ci, cw.K, cw.Co);
-    const int64_t nh = rvc_conv1d_f16_bytes(cw.nphase, cw.Ci, cw.K, cw.Co);
-    MCHECK(nb > 0 && nh > 0, "rvc_load_synth: bad conv shape %lld x %lld x %d", (long long)cw.Co, (long long)cw.Ci, cw.K);
-    MTRY(dev_alloc(c, nb, &cw.wx_bf));
-    MTRY(dev_alloc(c, nh, &cw.wx_hf));
-    int nmf = 0;
-    MTRY(rvc_conv1d_pack_x6(cw.w, cw.nphase, cw.Ci, cw.K, cw.Co, cw.wx_bf, &nmf, nullptr));
-    MTRY(rvc_conv1d_pack_f16(cw.w, cw.nphase, cw.Ci, cw.K, cw.Co, cw.wx_hf, &nmf, nullptr));
-    cw.nmf = nmf;
-    return RVC_OK;
-}
-
-// Conv1d weight [Co][Ci][K] (+ bias [Co]) -> KM [Ci*K][Co] (ops.pack_km, groups = 1)
-int make_conv(rvc_ctx* c, const HostT& w, const HostT* b, ConvW& cw) {
-    MCHECK(w.shape.size() >= 2, "rvc_load_synth: conv weight must be 2- or 3-D");
-    cw.Co = w.dim(0);
-    cw.Ci = w.dim(1);
-    cw.K = (int)w.dim(2);
-    cw.Kfull = cw.K;
-    std::vector<float> km((size_t)cw.Co * cw.Ci * cw.K);
-    for (int64_t m = 0; m < cw.Co; ++m)
-        for (int64_t ci = 0; ci < cw.Ci; ++ci)
-            for (int t = 0; t < cw.K; ++t) km[(ci * cw.K + t) * cw.Co + m] = w.v[(m * cw.Ci + ci) * cw.K + t];
-    MTRY(upload(c, km, &cw.w));
-    if (b) {
-        MCHECK((int64_t)b->v.size() == cw.Co, "rvc_load_synth: bias size %zu != %lld", b->v.size(), (long long)cw.Co);
-        MTRY(upload(c, b->v, &cw.b));
-    }
-    return make_images(c, cw);
-}
-
-// ConvTranspose1d weight [Ci][Co][K], stride u -> polyphase KM [u][Ci*T][Co] (ops.pack_convT)
-int make_convT(rvc_ctx* c, const HostT& w, const HostT& b, int u, int pad, ConvW& cw) {
-    cw.Ci = w.dim(0);
-    cw.Co = w.dim(1);
-    cw.Kfull = (int)w.dim(2);
-    cw.u = u;
-    cw.tpad = pad;
-    cw.nphase = u;
-    const int T = (cw.Kfull + u - 1) / u;
-    cw.K = T;
-    std::vector<float> km((size_t)u * cw.Ci * T * cw.Co, 0.f);
-    for (int r = 0; r < u; ++r)
-        for (int tp = 0; tp < T; ++tp) {
-            const int j = r + (T - 1 - tp) * u;
-            if (j >= cw.Kfull) continue;
-            for (int64_t ci = 0; ci < cw.Ci; ++ci)
-                for (int64_t m = 0; m < cw.Co; ++m)
-                    km[(((int64_t)r * cw.Ci + ci) * T + tp) * cw.Co + m] = w.v[(ci * cw.Co + m) * cw.Kfull + j];
-        }
-    MTRY(upload(c, km, &cw.w));
-    MTRY(upload(c, b.v, &cw.b));
-    return make_images(c, cw);
-}
-
-// ------------------------------------------------------------------ pass sets (ops.conv_passes / rb_passes)
-int base_passes(const rvc_ctx* c) { return c->prec == RVC_PREC_FP32 ? 6 : c->prec; }
-
-int conv_passes(const rvc_ctx* c, int K, int64_t Ci, int stride) {
-    if (c->prec == RVC_PREC_FP32 && c->f16mix && stride == 1 && ((K >= 7 && Ci <= 256) || (K >= 3 && Ci >= 64 && Ci <= 128)))
-        return RVC_ARITH_F16X3;
-    return base_passes(c);
-}
+int64_t convT_out_len(const ConvW& cw, int64_t Lin) { return (Lin - 1) * cw.u - 2 * cw.tpad + cw.Kfull; }
 
 int rb_passes(const rvc_ctx* c, int K) {
     if (c->prec == RVC_PREC_FP32 && c->f16mix && K >= 7) return RVC_ARITH_F16X3;
@@ -258,88 +69,6 @@ bool resblock_fusable(const rvc_ctx* c, const ConvW& c1, const ConvW& c2, int d)
            (c1.Co == 32 || c1.Co == 64) && c1.K == c2.K && c1.K % 2 == 1 && c1.K <= 15 && (c1.K - 1) * d <= 64;
 }
 
-int ensure_ws(rvc_ctx* c, int64_t need, hipStream_t s) {
-    if (need <= c->ws_bytes) return RVC_OK;
-    if (c->ws) {
-        MHIP(hipStreamSynchronize(s));
-        MHIP(hipFree(c->ws));
-        c->ws = nullptr;
-        c->ws_bytes = 0;
-    }
-    const int64_t bytes = need + (4 << 20);
-    MHIP(hipMalloc(&c->ws, bytes));
-    c->ws_bytes = bytes;
-    return RVC_OK;
-}
-
-// ------------------------------------------------------------------ launch helpers (ops.conv1d)
-struct CallOpts {
-    const float* bias2 = nullptr;
-    const float* res = nullptr;
-    int stride = 1, pad = 0, dil = 1;
-    int64_t Lout = -1;
-    int in_act = RVC_ACT_NONE, out_act = RVC_ACT_NONE, accumulate = 0;
-    float in_slope = 0.f, in_scale = 1.f, out_scale = 1.f;
-    int64_t B = 1, x_bstride = 0;
-};
-
-int conv(rvc_ctx* c, const ConvW& cw, const float* x, int64_t Lin, float* y, const CallOpts& o, hipStream_t s) {
-    rvc_conv1d_args a;
-    memset(&a, 0, sizeof(a));
-    a.x = x;
-    a.w = cw.w;
-    a.bias = cw.b;
-    a.bias2 = o.bias2;
-    a.res = o.res;
-    a.y = y;
-    a.B = o.B;
-    a.Ci = cw.Ci;
-    a.Co = cw.Co;
-    a.Lin = Lin;
-    a.x_bstride = o.x_bstride;
-    a.groups = 1;
-    a.in_act = o.in_act;
-    a.in_slope = o.in_slope;
-    a.in_scale = o.in_scale;
-    a.out_act = o.out_act;
-    a.out_scale = o.out_scale;
-    a.accumulate = o.accumulate;
-    a.K = cw.K;
-    int stride = o.stride;
-    if (cw.nphase > 1) {  // ConvT as u phase convs (ops.ConvT.__call__)
-        const int64_t Lout = (Lin - 1) * cw.u - 2 * cw.tpad + cw.Kfull;
-        a.Lout = Lout;
-        a.ncols = (Lout - 1 + cw.tpad) / cw.u + 1;
-        a.stride = 1;
-        a.pad = cw.K - 1;
-        a.dil = 1;
-        a.nphase = cw.u;
-        a.ostride = cw.u;
-        a.ooffset = -cw.tpad;
-        stride = 1;
-    } else {
-        a.Lout = o.Lout >= 0 ? o.Lout : (Lin + 2 * o.pad - o.dil * (cw.K - 1) - 1) / o.stride + 1;
-        a.stride = o.stride;
-        a.pad = o.pad;
-        a.dil = o.dil;
-        a.nphase = 1;
-        a.ostride = 1;
-    }
-    if (cw.wx_bf) {
-        const int passes = conv_passes(c, cw.K, cw.Ci, stride);
-        a.wx = passes == RVC_ARITH_F16X3 ? cw.wx_hf : cw.wx_bf;
-        a.wx_nmf = cw.nmf;
-        a.wx_passes = passes;
-    }
-    const int64_t need = rvc_conv1d_workspace_bytes(&a);
-    if (need < 0) return RVC_EINVAL;
-    MTRY(ensure_ws(c, need, s));
-    return rvc_conv1d(&a, need ? c->ws : nullptr, need, s);
-}
-
-int64_t convT_out_len(const ConvW& cw, int64_t Lin) { return (Lin - 1) * cw.u - 2 * cw.tpad + cw.Kfull; }
-
-// ------------------------------------------------------------------ scratch plan for one sequence of T frames
 struct Plan {
     int64_t off = 0;
     int64_t take(int64_t n) {  // 256-B aligned float offsets
@@ -400,9 +129,9 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
 // ------------------------------------------------------------------ one sequence (synth.py infer_cf)
 int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float* nsff0, int64_t T, int64_t sid,
               const float* z_noise, const float* sine_noise, uint64_t seed, float* wav, const Bufs& bf, hipStream_t s) {
-    const Synth& S = c->syn;
+    Synth& S = *c->syn;
     const rvc_synth_cfg& g = S.cfg;
-    float* A = c->arena;
+    float* A = S.arena;
     const int64_t H = g.hidden_channels, I = g.inter_channels, half = I / 2, nh = g.n_heads, kc = S.kc, E = S.emb_dim;
     const int64_t L = T * S.upp;
     MCHECK(sid >= 0 && sid < S.n_spk, "rvc_synth_infer: sid %lld out of range [0, %lld)", (long long)sid, (long long)S.n_spk);
@@ -411,7 +140,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     float* gc = A + bf.gc;
     {
         CallOpts o;
-        MTRY(conv(c, S.cond, S.emb_g + sid * g.gin_channels, 1, gc, o, s));
+        MTRY(conv(c, S, S.cond, S.emb_g + sid * g.gin_channels, 1, gc, o, s));
     }
     // ---- TextEncoder (synthesizers.py:366-371)
     float* phone_cf = A + bf.phone_cf;
@@ -420,19 +149,19 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
           *rk = A + bf.rk, *ffh = A + bf.ffh, *stats = A + bf.stats;
     {
         CallOpts o;
-        MTRY(conv(c, S.emb_phone, phone_cf, T, lin, o, s));
+        MTRY(conv(c, S, S.emb_phone, phone_cf, T, lin, o, s));
     }
     MTRY(rvc_textenc_embed(lin, S.emb_pitch, pitch, x, 1, H, T, (float)sqrt((double)H), 0.1f, s));
     const float scale = (float)(1.0 / sqrt((double)kc));
     for (const Layer& Ly : S.layers) {
         CallOpts o;
-        MTRY(conv(c, Ly.qkv, x, T, qkv, o, s));
+        MTRY(conv(c, S, Ly.qkv, x, T, qkv, o, s));
         CallOpts orl;
         orl.B = nh;
         orl.x_bstride = kc * T;
         orl.Lout = T;
         orl.out_scale = scale;
-        MTRY(conv(c, Ly.relk, qkv, T, rk, orl, s));
+        MTRY(conv(c, S, Ly.relk, qkv, T, rk, orl, s));
         rvc_attn_args at;
         memset(&at, 0, sizeof(at));
         at.q = qkv;
@@ -453,22 +182,22 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         const int64_t need = rvc_attention_workspace_bytes(&at);
         MCHECK(need >= 0, "rvc_synth_infer: attention shape H=%lld D=%lld T=%lld unsupported", (long long)nh,
                (long long)kc, (long long)T);
-        MTRY(ensure_ws(c, need, s));
-        MTRY(rvc_attention(&at, need ? c->ws : nullptr, need, s));
-        MTRY(conv(c, Ly.o, ob, T, tmp, o, s));
+        MTRY(ensure_ws(S, need, s));
+        MTRY(rvc_attention(&at, need ? S.ws : nullptr, need, s));
+        MTRY(conv(c, S, Ly.o, ob, T, tmp, o, s));
         MTRY(rvc_layernorm_cf(x, tmp, Ly.ln1g, Ly.ln1b, x, 1, H, T, 1e-5f, s));
         CallOpts f1;
         f1.pad = (g.kernel_size - 1) / 2;
         f1.out_act = RVC_ACT_RELU;
-        MTRY(conv(c, Ly.ffn1, x, T, ffh, f1, s));
+        MTRY(conv(c, S, Ly.ffn1, x, T, ffh, f1, s));
         CallOpts f2;
         f2.pad = (g.kernel_size - 1) / 2;
-        MTRY(conv(c, Ly.ffn2, ffh, T, tmp, f2, s));
+        MTRY(conv(c, S, Ly.ffn2, ffh, T, tmp, f2, s));
         MTRY(rvc_layernorm_cf(x, tmp, Ly.ln2g, Ly.ln2b, x, 1, H, T, 1e-5f, s));
     }
     {
         CallOpts o;
-        MTRY(conv(c, S.proj, x, T, stats, o, s));
+        MTRY(conv(c, S, S.proj, x, T, stats, o, s));
     }
     // ---- prior sample (synthesizers.py:449)
     float* zp = A + bf.zp;
@@ -489,31 +218,31 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         float *x0 = xf, *x1 = xf + half * T;
         {
             CallOpts o;
-            MTRY(conv(c, F.pre, x0, T, h, o, s));
+            MTRY(conv(c, S, F.pre, x0, T, h, o, s));
         }
         for (int l = 0; l < 3; ++l) {
             CallOpts oi;
             oi.pad = (F.ins[l].K - 1) / 2;
             oi.bias2 = gc + (int64_t)f * 6 * H + (int64_t)l * 2 * H;
-            MTRY(conv(c, F.ins[l], h, T, xin, oi, s));
+            MTRY(conv(c, S, F.ins[l], h, T, xin, oi, s));
             MTRY(rvc_gate(xin, acts, 1, H, T, s));
             if (l < 2) {
                 CallOpts ra;
                 ra.res = h;
-                MTRY(conv(c, F.rs_a[l], acts, T, h, ra, s));
+                MTRY(conv(c, S, F.rs_a[l], acts, T, h, ra, s));
                 CallOpts rb;
                 rb.accumulate = l > 0;
-                MTRY(conv(c, F.rs_b[l], acts, T, outacc, rb, s));
+                MTRY(conv(c, S, F.rs_b[l], acts, T, outacc, rb, s));
             } else {
                 CallOpts rb;
                 rb.accumulate = 1;
-                MTRY(conv(c, F.rs_b[l], acts, T, outacc, rb, s));
+                MTRY(conv(c, S, F.rs_b[l], acts, T, outacc, rb, s));
             }
         }
         CallOpts po;
         po.res = x1;
         po.out_scale = -1.f;
-        MTRY(conv(c, F.post, outacc, T, x1, po, s));
+        MTRY(conv(c, S, F.post, outacc, T, x1, po, s));
         xf_cur = xf;
     }
     const float* z = xf_cur;
@@ -530,7 +259,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         CallOpts o;
         o.pad = 3;
         o.bias2 = gc + 4 * 6 * H;
-        MTRY(conv(c, S.conv_pre, z, T, xcur, o, s));
+        MTRY(conv(c, S, S.conv_pre, z, T, xcur, o, s));
     }
     int64_t Lcur = T;
     float scale_in = 1.f;
@@ -544,13 +273,13 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         ou.in_act = RVC_ACT_LRELU;
         ou.in_slope = kLreluSlope;
         ou.in_scale = scale_in;
-        MTRY(conv(c, S.ups[i], xcur, Lcur, y, ou, s));
+        MTRY(conv(c, S, S.ups[i], xcur, Lcur, y, ou, s));
         CallOpts on;
         on.Lout = Li;
         on.stride = S.noise_stride[i];
         on.pad = S.noise_pad[i];
         on.accumulate = 1;
-        MTRY(conv(c, S.noise[i], har, L, y, on, s));
+        MTRY(conv(c, S, S.noise[i], har, L, y, on, s));
         for (int j = 0; j < nk; ++j) {
             const int kk = g.resblock_kernel_sizes[j];
             const std::vector<Pair>& pairs = S.res[i][j];
@@ -587,7 +316,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
                 o1.dil = P.d;
                 o1.in_act = RVC_ACT_LRELU;
                 o1.in_slope = kLreluSlope;
-                MTRY(conv(c, P.c1, cur, Li, t1, o1, s));
+                MTRY(conv(c, S, P.c1, cur, Li, t1, o1, s));
                 CallOpts o2;
                 o2.pad = (kk - 1) / 2;
                 o2.res = cur;
@@ -600,7 +329,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
                 } else {
                     nxt = cur != xa ? xa : xb;
                 }
-                MTRY(conv(c, P.c2, t1, Li, nxt, o2, s));
+                MTRY(conv(c, S, P.c2, t1, Li, nxt, o2, s));
                 cur = nxt;
             }
         }
@@ -614,21 +343,13 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     op.in_slope = 0.01f;
     op.in_scale = scale_in;
     op.out_act = RVC_ACT_TANH;
-    return conv(c, S.conv_post, xcur, Lcur, wav, op, s);
+    return conv(c, S, S.conv_post, xcur, Lcur, wav, op, s);
 }
 
-void free_model(rvc_ctx* c) {
-    for (void* p : c->allocs) (void)hipFree(p);
-    c->allocs.clear();
-    c->syn = Synth();
-}
+}  // namespace synthm
 
-bool env_on(const char* name) {
-    const char* v = getenv(name);
-    return !(v && strcmp(v, "0") == 0);
-}
+using namespace synthm;
 
-}  // namespace
 
 // ------------------------------------------------------------------ C ABI
 extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
@@ -648,9 +369,9 @@ extern "C" void rvc_ctx_destroy(rvc_ctx* c) {
     if (!c) return;
     if (hipSetDevice(c->device) == hipSuccess) {
         (void)hipDeviceSynchronize();
-        free_model(c);
-        if (c->ws) (void)hipFree(c->ws);
-        if (c->arena) (void)hipFree(c->arena);
+        synth_delete(c->syn);
+        contentvec_delete(c->cv);
+        rmvpe_delete(c->rm);
     }
     delete c;
 }
@@ -665,8 +386,8 @@ extern "C" int rvc_ctx_set_precision(rvc_ctx* c, int prec) {
 }
 
 extern "C" int64_t rvc_synth_out_len(const rvc_ctx* c, int64_t T) {
-    if (!c || !c->syn.loaded || T <= 0) return -1;
-    return T * c->syn.upp;
+    if (!c || !c->syn || !c->syn->loaded || T <= 0) return -1;
+    return T * c->syn->upp;
 }
 
 extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const rvc_synth_cfg* cfg) {
@@ -677,35 +398,12 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
     MCHECK(g.n_upsamples >= 1 && g.n_upsamples <= 8 && g.n_resblocks >= 1 && g.n_resblocks <= 4 && g.n_dilations >= 1 &&
                g.n_dilations <= 4,
            "rvc_load_synth: bad generator config");
-    std::map<std::string, const rvc_param*> by;
-    for (int i = 0; i < n; ++i) {
-        MCHECK(params[i].name && params[i].data && params[i].ndim >= 1 && params[i].ndim <= 4 &&
-                   (params[i].dtype == RVC_DT_F32 || params[i].dtype == RVC_DT_F16),
-               "rvc_load_synth: bad param %d", i);
-        by[params[i].name] = &params[i];
-    }
-    std::string missing;
-    auto has = [&](const std::string& k) { return by.count(k) > 0; };
-    // x.weight (folded from x.weight_g / x.weight_v when those are given), any other key as is
-    auto get = [&](const std::string& k, HostT& out) -> bool {
-        if (has(k)) {
-            out = to_host(*by[k]);
-            return true;
-        }
-        const std::string suf = ".weight";
-        if (k.size() > suf.size() && k.compare(k.size() - suf.size(), suf.size(), suf) == 0) {
-            const std::string base = k.substr(0, k.size() - suf.size());
-            if (has(base + ".weight_g") && has(base + ".weight_v")) {
-                out = fold_wn(to_host(*by[base + ".weight_v"]), to_host(*by[base + ".weight_g"]));
-                return true;
-            }
-        }
-        if (missing.empty()) missing = k;
-        return false;
-    };
+    Params PM;  // x.weight folded from x.weight_g / x.weight_v (dim 0) when those are given
+    MTRY(index_params(params, n, PM, "rvc_load_synth"));
     MHIP(hipSetDevice(c->device));
-    free_model(c);
-    Synth& S = c->syn;
+    synth_delete(c->syn);
+    c->syn = new Synth();
+    Synth& S = *c->syn;
     S.cfg = g;
     const int H = g.hidden_channels;
     S.kc = H / g.n_heads;
@@ -715,16 +413,16 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
                "rvc_load_synth: odd upsample rates (output_padding) are not used by any shipped config");
         S.upp *= g.upsample_rates[i];
     }
-    HostT w, b, w2, b2, w3, b3;
-#define GET(k, t) MCHECK(get(k, t), "rvc_load_synth: missing %s", missing.c_str())
+    HostT w, b, w2, b2;
+#define GET(k, t) MCHECK(PM.get(k, t), "rvc_load_synth: missing %s", PM.missing.c_str())
     // ---- TextEncoder
     GET("enc_p.emb_phone.weight", w);
     GET("enc_p.emb_phone.bias", b);
     S.emb_dim = (int)w.dim(1);
     w.shape.push_back(1);
-    MTRY(make_conv(c, w, &b, S.emb_phone));
+    MTRY(make_conv(c, S, w, &b, S.emb_phone));
     GET("enc_p.emb_pitch.weight", w);
-    MTRY(upload(c, w.v, &S.emb_pitch));
+    MTRY(upload(S, w.v, &S.emb_pitch));
     for (int i = 0; i < g.n_layers; ++i) {
         Layer Ly;
         const std::string p = "enc_p.encoder.attn_layers." + std::to_string(i) + ".";
@@ -741,38 +439,38 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         wqkv.shape[0] = q.dim(0) + k.dim(0) + v.dim(0);
         bqkv.v.insert(bqkv.v.end(), bk.v.begin(), bk.v.end());
         bqkv.v.insert(bqkv.v.end(), bv.v.begin(), bv.v.end());
-        MTRY(make_conv(c, wqkv, &bqkv, Ly.qkv));
+        MTRY(make_conv(c, S, wqkv, &bqkv, Ly.qkv));
         GET(p + "emb_rel_k", w);  // [1][21][kc] -> relk conv weight [21][kc][1]
         MCHECK(w.dim(1) == 21 && w.dim(2) == S.kc, "rvc_load_synth: emb_rel_k must be [1][21][%d]", S.kc);
         HostT ek;
         ek.v = w.v;
         ek.shape = {21, S.kc, 1};
-        MTRY(make_conv(c, ek, nullptr, Ly.relk));
+        MTRY(make_conv(c, S, ek, nullptr, Ly.relk));
         GET(p + "emb_rel_v", w);
-        MTRY(upload(c, w.v, &Ly.ev));
+        MTRY(upload(S, w.v, &Ly.ev));
         GET(p + "conv_o.weight", w);
         GET(p + "conv_o.bias", b);
-        MTRY(make_conv(c, w, &b, Ly.o));
+        MTRY(make_conv(c, S, w, &b, Ly.o));
         const std::string si = std::to_string(i);
         GET("enc_p.encoder.norm_layers_1." + si + ".gamma", w);
-        MTRY(upload(c, w.v, &Ly.ln1g));
+        MTRY(upload(S, w.v, &Ly.ln1g));
         GET("enc_p.encoder.norm_layers_1." + si + ".beta", w);
-        MTRY(upload(c, w.v, &Ly.ln1b));
+        MTRY(upload(S, w.v, &Ly.ln1b));
         GET("enc_p.encoder.ffn_layers." + si + ".conv_1.weight", w);
         GET("enc_p.encoder.ffn_layers." + si + ".conv_1.bias", b);
-        MTRY(make_conv(c, w, &b, Ly.ffn1));
+        MTRY(make_conv(c, S, w, &b, Ly.ffn1));
         GET("enc_p.encoder.ffn_layers." + si + ".conv_2.weight", w);
         GET("enc_p.encoder.ffn_layers." + si + ".conv_2.bias", b);
-        MTRY(make_conv(c, w, &b, Ly.ffn2));
+        MTRY(make_conv(c, S, w, &b, Ly.ffn2));
         GET("enc_p.encoder.norm_layers_2." + si + ".gamma", w);
-        MTRY(upload(c, w.v, &Ly.ln2g));
+        MTRY(upload(S, w.v, &Ly.ln2g));
         GET("enc_p.encoder.norm_layers_2." + si + ".beta", w);
-        MTRY(upload(c, w.v, &Ly.ln2b));
+        MTRY(upload(S, w.v, &Ly.ln2b));
         S.layers.push_back(Ly);
     }
     GET("enc_p.proj.weight", w);
     GET("enc_p.proj.bias", b);
-    MTRY(make_conv(c, w, &b, S.proj));
+    MTRY(make_conv(c, S, w, &b, S.proj));
     // ---- speaker conditioning: 4 flows' cond layers then dec.cond, stacked (synth.py)
     {
         HostT cw, cb;
@@ -789,28 +487,28 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
                 cb.v.insert(cb.v.end(), b.v.begin(), b.v.end());
             }
         }
-        MTRY(make_conv(c, cw, &cb, S.cond));
+        MTRY(make_conv(c, S, cw, &cb, S.cond));
     }
     GET("emb_g.weight", w);
     MCHECK(w.dim(1) == g.gin_channels, "rvc_load_synth: emb_g width %lld != gin_channels %d", (long long)w.dim(1),
            g.gin_channels);
     S.n_spk = w.dim(0);  // convert.py:558 takes the speaker count from emb_g
-    MTRY(upload(c, w.v, &S.emb_g));
+    MTRY(upload(S, w.v, &S.emb_g));
     // ---- flow
     for (int f = 0; f < 4; ++f) {
         Flow& F = S.flows[f];
         const std::string p = "flow.flows." + std::to_string(2 * f) + ".";
         GET(p + "pre.weight", w);
         GET(p + "pre.bias", b);
-        MTRY(make_conv(c, w, &b, F.pre));
+        MTRY(make_conv(c, S, w, &b, F.pre));
         GET(p + "post.weight", w);
         GET(p + "post.bias", b);
-        MTRY(make_conv(c, w, &b, F.post));
+        MTRY(make_conv(c, S, w, &b, F.post));
         for (int l = 0; l < 3; ++l) {
             const std::string sl = std::to_string(l);
             GET(p + "enc.in_layers." + sl + ".weight", w);
             GET(p + "enc.in_layers." + sl + ".bias", b);
-            MTRY(make_conv(c, w, &b, F.ins[l]));
+            MTRY(make_conv(c, S, w, &b, F.ins[l]));
             GET(p + "enc.res_skip_layers." + sl + ".weight", w);
             GET(p + "enc.res_skip_layers." + sl + ".bias", b);
             if (l < 2) {  // res half [:H], skip half [H:]
@@ -822,10 +520,10 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
                 wb.shape[0] = w.dim(0) - H;
                 ba.v.assign(b.v.begin(), b.v.begin() + H);
                 bb.v.assign(b.v.begin() + H, b.v.end());
-                MTRY(make_conv(c, wa, &ba, F.rs_a[l]));
-                MTRY(make_conv(c, wb, &bb, F.rs_b[l]));
+                MTRY(make_conv(c, S, wa, &ba, F.rs_a[l]));
+                MTRY(make_conv(c, S, wb, &bb, F.rs_b[l]));
             } else {
-                MTRY(make_conv(c, w, &b, F.rs_b[l]));
+                MTRY(make_conv(c, S, w, &b, F.rs_b[l]));
             }
         }
     }
@@ -836,7 +534,7 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
     S.lin_b = b.v[0];
     GET("dec.conv_pre.weight", w);
     GET("dec.conv_pre.bias", b);
-    MTRY(make_conv(c, w, &b, S.conv_pre));
+    MTRY(make_conv(c, S, w, &b, S.conv_pre));
     const int nup = g.n_upsamples;
     S.ups.resize(nup);
     S.noise.resize(nup);
@@ -847,7 +545,7 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         const std::string si = std::to_string(i);
         GET("dec.ups." + si + ".weight", w);
         GET("dec.ups." + si + ".bias", b);
-        MTRY(make_convT(c, w, b, u, (k - u) / 2, S.ups[i]));
+        MTRY(make_convT(c, S, w, b, u, (k - u) / 2, S.ups[i]));
         int st = 1;
         for (int j = i + 1; j < nup; ++j) st *= g.upsample_rates[j];
         const int kn = st == 1 ? 1 : st * 2 - st % 2;
@@ -855,7 +553,7 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         S.noise_pad.push_back(st == 1 ? 0 : (kn - st) / 2);
         GET("dec.noise_convs." + si + ".weight", w);
         GET("dec.noise_convs." + si + ".bias", b);
-        MTRY(make_conv(c, w, &b, S.noise[i]));
+        MTRY(make_conv(c, S, w, &b, S.noise[i]));
         S.res[i].resize(g.n_resblocks);
         for (int j = 0; j < g.n_resblocks; ++j) {
             const std::string rb = "dec.resblocks." + std::to_string(i * g.n_resblocks + j) + ".";
@@ -865,16 +563,16 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
                 const std::string sm = std::to_string(m);
                 GET(rb + "convs1." + sm + ".weight", w);
                 GET(rb + "convs1." + sm + ".bias", b);
-                MTRY(make_conv(c, w, &b, P.c1));
+                MTRY(make_conv(c, S, w, &b, P.c1));
                 GET(rb + "convs2." + sm + ".weight", w2);
                 GET(rb + "convs2." + sm + ".bias", b2);
-                MTRY(make_conv(c, w2, &b2, P.c2));
+                MTRY(make_conv(c, S, w2, &b2, P.c2));
                 S.res[i][j].push_back(P);
             }
         }
     }
     GET("dec.conv_post.weight", w);
-    MTRY(make_conv(c, w, nullptr, S.conv_post));
+    MTRY(make_conv(c, S, w, nullptr, S.conv_post));
 #undef GET
     MHIP(hipDeviceSynchronize());
     S.loaded = true;
@@ -884,23 +582,14 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
 extern "C" int rvc_synth_infer(rvc_ctx* c, const float* phone, const int64_t* pitch, const float* pitchf, int64_t B,
                                int64_t T, const int64_t* sid, const float* z_noise, const float* sine_noise,
                                uint64_t seed, float* wav, rvc_stream_t stream) {
-    MCHECK(c && c->syn.loaded, "rvc_synth_infer: no synthesizer loaded");
+    MCHECK(c && c->syn && c->syn->loaded, "rvc_synth_infer: no synthesizer loaded");
     MCHECK(phone && pitch && pitchf && sid && wav, "rvc_synth_infer: null buffer");
     MCHECK(B >= 1 && T >= 1, "rvc_synth_infer: empty input (B=%lld, T=%lld)", (long long)B, (long long)T);
     hipStream_t s = (hipStream_t)stream;
     MHIP(hipSetDevice(c->device));
-    const Bufs bf = plan_bufs(c->syn, T);
-    if (bf.total > c->arena_floats) {
-        if (c->arena) {
-            MHIP(hipStreamSynchronize(s));
-            MHIP(hipFree(c->arena));
-            c->arena = nullptr;
-            c->arena_floats = 0;
-        }
-        MHIP(hipMalloc((void**)&c->arena, bf.total * 4));
-        c->arena_floats = bf.total;
-    }
-    const int64_t I = c->syn.cfg.inter_channels, L = T * c->syn.upp, E = c->syn.emb_dim;
+    const Bufs bf = plan_bufs(*c->syn, T);
+    MTRY(ensure_arena(*c->syn, bf.total, s));
+    const int64_t I = c->syn->cfg.inter_channels, L = T * c->syn->upp, E = c->syn->emb_dim;
     for (int64_t b = 0; b < B; ++b)  // sequences share the scratch in stream order
         MTRY(synth_one(c, phone + b * T * E, pitch + b * T, pitchf + b * T, T, sid[b], z_noise ? z_noise + b * I * T : nullptr,
                        sine_noise ? sine_noise + b * L : nullptr, seed + (uint64_t)b, wav + b * L, bf, s));

@@ -75,6 +75,12 @@ class SynthCfg(ctypes.Structure):
                 ("upsample_initial_channel", c_int), ("spk_embed_dim", c_int), ("gin_channels", c_int), ("sr", c_int)]
 
 
+class ContentVecCfg(ctypes.Structure):
+    """rvc_contentvec_cfg: the fairseq .pt cfg["model"] fields the encoder needs (fairseq.py:30-36)."""
+    _fields_ = [("encoder_embed_dim", c_int), ("encoder_attention_heads", c_int), ("conv_pos_groups", c_int),
+                ("_pad0", c_int)]
+
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "rvc_last_error": [],
@@ -148,6 +154,14 @@ SIGNATURES = {
     "rvc_ctx_set_precision": [c_void_p, c_int],
     "rvc_load_synth": [c_void_p, POINTER(Param), c_int, POINTER(SynthCfg)],
     "rvc_synth_out_len": [c_void_p, c_int64],
+    "rvc_load_contentvec": [c_void_p, POINTER(Param), c_int, POINTER(ContentVecCfg)],
+    "rvc_contentvec_frames": [c_int64],
+    "rvc_contentvec_forward": [c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p, c_void_p],
+    "rvc_load_rmvpe": [c_void_p, POINTER(Param), c_int],
+    "rvc_rmvpe_frames": [c_int64],
+    "rvc_rmvpe_salience_ld": [c_int64],
+    "rvc_rmvpe_forward": [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
+    "rvc_rmvpe_check": [c_void_p],
     "rvc_synth_infer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
                         c_void_p, c_void_p],
 }
@@ -156,7 +170,8 @@ _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint,
-             "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64}
+             "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64,
+             "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64}
 
 _lib = None
 

@@ -1,10 +1,14 @@
-"""The model-level C ABI (include/rvc_amd.h "model-level API", csrc/rvc_model.cpp) from Python.
+"""The model-level C ABI (include/rvc_amd.h "model-level API", csrc/rvc_model.cpp, csrc/rvc_frontend.cpp)
+from Python.
 
 ``NativeSynth`` is a drop-in ``net_g`` for ``VC.pipeline`` (convert.py:381, the ``.infer`` contract of
 Synthesizer.infer, synthesizers.py:446-465) whose loader and launch sequence live in the library: the
 checkpoint's weight dict goes in as named host arrays (``rvc_load_synth``, weight-norm folded natively),
 ``infer`` is one ``rvc_synth_infer`` call.  It is what a non-Python host (cgo / JNI / N-API)
 binds; here it also pins the native sequence against ``SynthesizerAMD`` (tests/test_gpu_native.py).
+``NativeContentVec`` (``model.extract_features``, fairseq.py:1459) and ``NativeRMVPE``
+(``RMVPE.infer_from_audio``, RMVPE.py:223-226) do the same for the front end; each owns its own
+``rvc_ctx``.
 """
 from __future__ import annotations
 
@@ -17,6 +21,48 @@ from . import _lib
 from ._lib import check
 
 PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3, "fp32x6": 6, "f16x3": 16}
+
+
+def _params(W: dict):
+    """Named host arrays (rvc_param) for a weight dict; returns (params, keep-alive list)."""
+    keep, params = [], (_lib.Param * len(W))()
+    for i, (k, v) in enumerate(W.items()):
+        a = torch.as_tensor(v).detach().cpu().contiguous()
+        if a.dtype not in (torch.float16, torch.float32):
+            a = a.float()
+        arr = np.ascontiguousarray(a.numpy())
+        if not 1 <= arr.ndim <= 4:
+            raise ValueError(f"rvc_param: {k} has {arr.ndim} dims")
+        name = k.encode()
+        keep += [arr, name]
+        p = params[i]
+        p.name, p.data = name, ctypes.c_void_p(arr.ctypes.data)
+        p.dtype = 1 if arr.dtype == np.float16 else 0
+        p.ndim = arr.ndim
+        for d, s in enumerate(arr.shape):
+            p.shape[d] = s
+    return params, keep
+
+
+class _Ctx:
+    """One rvc_ctx on a device (destroyed with the object)."""
+
+    def __init__(self, device, precision="fp32"):
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        ctx = ctypes.c_void_p()
+        check(self.lib.rvc_ctx_create(self.device.index or 0, ctypes.byref(ctx)), "rvc_ctx_create")
+        self.ctx = ctx
+        check(self.lib.rvc_ctx_set_precision(ctx, PREC[precision]), "rvc_ctx_set_precision")
+
+    def __del__(self):
+        ctx = getattr(self, "ctx", None)
+        if ctx is not None and ctx.value:
+            self.lib.rvc_ctx_destroy(ctx)
+            self.ctx = None
+
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
 
 def synth_cfg(cpt: dict) -> "_lib.SynthCfg":
@@ -43,48 +89,21 @@ def synth_cfg(cpt: dict) -> "_lib.SynthCfg":
     return c
 
 
-class NativeSynth:
+class NativeSynth(_Ctx):
     """Synthesizer.infer through rvc_ctx / rvc_load_synth / rvc_synth_infer.
 
     ``weights``: the checkpoint's weight dict as stored (fp16 weight_g / weight_v pairs, folded by the
     library) or any dict of already-folded fp32 tensors (synth.fold_weight_norm)."""
 
     def __init__(self, cpt: dict, device: str = "cuda", weights: dict | None = None, precision: str = "fp32"):
-        self.lib = _lib.load()
-        dev = torch.device(device)
-        self.device = dev
+        super().__init__(device, precision)
         self.cfg = synth_cfg(cpt)
         self.upp = int(np.prod(cpt["config"][12]))
         self.inter = self.cfg.inter_channels
-        ctx = ctypes.c_void_p()
-        check(self.lib.rvc_ctx_create(dev.index or 0, ctypes.byref(ctx)), "rvc_ctx_create")
-        self.ctx = ctx
-        check(self.lib.rvc_ctx_set_precision(ctx, PREC[precision]), "rvc_ctx_set_precision")
         W = cpt["weight"] if weights is None else weights
-        keep, params = [], (_lib.Param * len(W))()
-        for i, (k, v) in enumerate(W.items()):
-            a = v.detach().cpu().contiguous()
-            if a.dtype not in (torch.float16, torch.float32):
-                a = a.float()
-            arr = np.ascontiguousarray(a.numpy())
-            name = k.encode()
-            keep += [arr, name]
-            p = params[i]
-            p.name, p.data = name, ctypes.c_void_p(arr.ctypes.data)
-            p.dtype = 1 if arr.dtype == np.float16 else 0
-            p.ndim = arr.ndim
-            if not 1 <= arr.ndim <= 4:
-                raise ValueError(f"NativeSynth: {k} has {arr.ndim} dims")
-            for d, s in enumerate(arr.shape):
-                p.shape[d] = s
-        check(self.lib.rvc_load_synth(ctx, params, len(W), ctypes.byref(self.cfg)), "rvc_load_synth")
+        params, keep = _params(W)
+        check(self.lib.rvc_load_synth(self.ctx, params, len(W), ctypes.byref(self.cfg)), "rvc_load_synth")
         del keep
-
-    def __del__(self):
-        ctx = getattr(self, "ctx", None)
-        if ctx is not None and ctx.value:
-            self.lib.rvc_ctx_destroy(ctx)
-            self.ctx = None
 
     def out_len(self, T: int) -> int:
         return int(self.lib.rvc_synth_out_len(self.ctx, T))
@@ -115,5 +134,94 @@ class NativeSynth:
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         check(self.lib.rvc_synth_infer(self.ctx, p(phone), p(pitch), p(nsff0), B, T,
                                        ctypes.c_void_p(sid_h.ctypes.data), p(zn), p(sn), int(seed), p(o),
-                                       ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "rvc_synth_infer")
+                                       self.stream()), "rvc_synth_infer")
         return o, torch.ones(B, 1, T, device=dev), None
+
+
+class NativeContentVec(_Ctx):
+    """HubertModel.extract_features through rvc_load_contentvec / rvc_contentvec_forward."""
+
+    def __init__(self, ckpt: dict, device: str = "cuda", precision: str = "fp32", weights: dict | None = None):
+        """``weights``: a replacement for ckpt["model"] (e.g. with encoder.pos_conv already folded)."""
+        super().__init__(device, precision)
+        cfg = ckpt["cfg"]["model"]
+        if cfg.get("extractor_mode", "default") != "default" or cfg.get("layer_norm_first", False):
+            raise NotImplementedError("ContentVec/HuBERT-base layout only (extractor 'default', post-LN)")
+        c = _lib.ContentVecCfg()
+        c.encoder_embed_dim = cfg.get("encoder_embed_dim", 768)
+        c.encoder_attention_heads = cfg.get("encoder_attention_heads", 12)
+        c.conv_pos_groups = cfg.get("conv_pos_groups", 16)
+        self.E = c.encoder_embed_dim
+        sd = ckpt["model"] if weights is None else weights
+        W = {k: v for k, v in sd.items() if torch.is_tensor(v) and v.is_floating_point()}
+        params, keep = _params(W)
+        check(self.lib.rvc_load_contentvec(self.ctx, params, len(W), ctypes.byref(c)), "rvc_load_contentvec")
+        self.proj_dim = int(W["final_proj.weight"].shape[0])
+        del keep
+
+    def frames(self, n: int) -> int:
+        return int(self.lib.rvc_contentvec_frames(n))
+
+    def forward(self, wav, output_layer: int = 12, final_proj: bool = False):
+        """wav [B, N] or [N] f32 (device) -> feats [B, T, C] (C = 768, or final_proj's width)."""
+        wav = wav.to(self.device, torch.float32)
+        wav = wav.reshape(1, -1) if wav.dim() == 1 else wav
+        wav = wav.contiguous()
+        B, N = wav.shape
+        T = self.frames(N)
+        out = torch.empty(B, T, self.proj_dim if final_proj else self.E, device=self.device)
+        check(self.lib.rvc_contentvec_forward(self.ctx, ctypes.c_void_p(wav.data_ptr()), B, N, int(output_layer),
+                                              int(bool(final_proj)), ctypes.c_void_p(out.data_ptr()), self.stream()),
+              "rvc_contentvec_forward")
+        return out
+
+    def extract_features(self, source, padding_mask=None, mask=False, ret_conv=False, output_layer=None):
+        """fairseq.py:1459: source [1, N] -> (x [1, T_f, 768], padding_mask [1, T_f])."""
+        if padding_mask is not None and bool(padding_mask.any()):
+            raise NotImplementedError("padded sources are not on the hot path (VC passes an all-False mask)")
+        x = self.forward(source, output_layer or 12)
+        return x, torch.zeros(x.shape[0], x.shape[1], dtype=torch.bool, device=x.device)
+
+
+class NativeRMVPE(_Ctx):
+    """RMVPE salience / f0 through rvc_load_rmvpe / rvc_rmvpe_forward / rvc_rmvpe_decode."""
+
+    def __init__(self, sd: dict, device: str = "cuda", window=None, mel_basis=None):
+        super().__init__(device)
+        W = dict(sd)
+        if window is not None:
+            W["window"] = window
+        if mel_basis is not None:
+            W["mel_basis"] = mel_basis
+        W = {k: v for k, v in W.items() if torch.as_tensor(v).is_floating_point()}
+        params, keep = _params(W)
+        check(self.lib.rvc_load_rmvpe(self.ctx, params, len(W)), "rvc_load_rmvpe")
+        del keep
+
+    def salience(self, wav):
+        """wav [B, N] or [N] f32 (device) -> (salience [B, 360, Tp], F)."""
+        wav = wav.to(self.device, torch.float32)
+        wav = (wav.reshape(1, -1) if wav.dim() == 1 else wav).contiguous()
+        B, N = wav.shape
+        Tp, F = int(self.lib.rvc_rmvpe_salience_ld(N)), int(self.lib.rvc_rmvpe_frames(N))
+        sal = torch.empty(B, 360, Tp, device=self.device)
+        check(self.lib.rvc_rmvpe_forward(self.ctx, ctypes.c_void_p(wav.data_ptr()), B, N,
+                                         ctypes.c_void_p(sal.data_ptr()), self.stream()), "rvc_rmvpe_forward")
+        return sal, F
+
+    def check(self):
+        check(self.lib.rvc_rmvpe_check(self.ctx), "rvc_rmvpe_check")
+
+    def infer_from_audio(self, audio, thred: float = 0.03) -> np.ndarray:
+        """RMVPE.infer_from_audio (RMVPE.py:223-226): f64 numpy [N] -> f64 numpy f0 [1 + N//160]."""
+        from . import ops
+        x = torch.from_numpy(np.asarray(audio)).float().to(self.device)
+        sal, F = self.salience(x)
+        Tp = sal.shape[-1]
+        f0 = torch.empty(F, dtype=torch.float64, device=self.device)
+        coarse = torch.empty(F, dtype=torch.int64, device=self.device)
+        pitchf = torch.empty(F, device=self.device)
+        ops.rmvpe_decode(sal[0], Tp, F, thred, 1.0, f0, coarse, pitchf)
+        out = f0.cpu().numpy()
+        self.check()
+        return out

@@ -52,6 +52,22 @@ def test_model_api_rejects_bad_arguments_without_gpu():
     assert lib.rvc_synth_out_len(None, 10) == -1
     assert lib.rvc_ctx_set_precision(None, 0) == -22
     lib.rvc_ctx_destroy(None)  # no-op
+    assert lib.rvc_load_contentvec(None, None, 0, None) == -22
+    assert lib.rvc_contentvec_forward(None, None, 1, 16000, 12, 0, None, None) == -22
+    assert lib.rvc_load_rmvpe(None, None, 0) == -22
+    assert lib.rvc_rmvpe_forward(None, None, 1, 16000, None, None) == -22
+    assert lib.rvc_rmvpe_check(None) == -22
+
+
+def test_model_api_size_queries():
+    from rvc_amd import contentvec
+    lib = _lib.load()
+    for n in (400, 16000, 160000 + 37, 480000):
+        assert lib.rvc_contentvec_frames(n) == contentvec.frames(n)
+        F = 1 + n // 160
+        assert lib.rvc_rmvpe_frames(n) == F
+        assert lib.rvc_rmvpe_salience_ld(n) == 32 * ((F - 1) // 32 + 1)
+    assert lib.rvc_contentvec_frames(100) == 0
 
 
 def test_synth_cfg_from_checkpoint_config():
@@ -78,7 +94,8 @@ def test_struct_layouts_match_c_compiler(tmp_path):
               "rvc_f0_post": [f[0] for f in _lib.F0Post._fields_],
               "rvc_denoise_args": [f[0] for f in _lib.DenoiseArgs._fields_],
               "rvc_param": [f[0] for f in _lib.Param._fields_],
-              "rvc_synth_cfg": [f[0] for f in _lib.SynthCfg._fields_]}
+              "rvc_synth_cfg": [f[0] for f in _lib.SynthCfg._fields_],
+              "rvc_contentvec_cfg": [f[0] for f in _lib.ContentVecCfg._fields_]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rvc_amd.h"', "int main(void){"]
     for st, fs in fields.items():
         lines.append(f'printf("%zu\\n", sizeof({st}));')
@@ -91,7 +108,7 @@ def test_struct_layouts_match_c_compiler(tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = []
-    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs, _lib.Param, _lib.SynthCfg):
+    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs, _lib.Param, _lib.SynthCfg, _lib.ContentVecCfg):
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f[0]).offset for f in cls._fields_]
     assert got == want

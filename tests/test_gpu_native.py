@@ -95,3 +95,65 @@ def test_native_synth_errors():
     del bad["dec.m_source.l_linear.bias"]
     with pytest.raises(RuntimeError, match="dec.m_source.l_linear.bias"):
         NativeSynth(ck, DEV, weights=bad)
+
+
+# ------------------------------------------------------------------ ContentVec / RMVPE through the model-level ABI
+def test_native_contentvec_matches_golden_and_python(golden):
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.native import NativeContentVec
+    g = golden("contentvec")
+    ck = synthetic.make_contentvec_ckpt(int(g["seed"]))
+    nat, py = NativeContentVec(ck, DEV), ContentVecAMD(ck, DEV)
+    src = torch.from_numpy(g["audio"]).view(1, -1).to(DEV)
+    x2 = nat.forward(src, 12)
+    x1 = nat.forward(src, 9, final_proj=True)
+    torch.cuda.synchronize()
+    assert rms(x2, g["feats_v2"]) < 1e-4  # the reference's own extract_features output
+    assert rms(x1, g["feats_v1"]) < 1e-4
+    # same launches as the Python model: bit-identical on the same folded pos_conv weight (odd T_f, 6.3 s);
+    # the native weight-norm fold (f64 norm) and torch's (f32) differ in the last bits only
+    wav = torch.from_numpy(synthetic.synthetic_audio(6.3, seed=77)).float().to(DEV)
+    ref = py.features_cf(wav, 12).t().unsqueeze(0)
+    assert rms(nat.forward(wav, 12), ref.cpu().numpy()) < 1e-5
+    sd = dict(ck["model"])
+    p = "encoder.pos_conv.0.weight"
+    sd[p] = torch._weight_norm(sd.pop(p + "_v").float(), sd.pop(p + "_g").float(), 2)
+    nat = NativeContentVec(ck, DEV, weights=sd)
+    got = nat.forward(wav, 12)
+    assert got.shape == ref.shape and torch.equal(got, ref)
+    ref1 = py.final_proj(py.extract_features(wav.view(1, -1), output_layer=9)[0])
+    assert torch.equal(nat.forward(wav, 9, final_proj=True), ref1)
+    # B sequences = B single calls
+    wb = torch.stack([wav, wav.flip(0)])
+    both = nat.forward(wb, 12)
+    assert torch.equal(both[0], got[0]) and torch.equal(both[1], nat.forward(wav.flip(0), 12)[0])
+
+
+def test_native_rmvpe_matches_golden_and_python(golden):
+    from rvc_amd import melbasis
+    from rvc_amd.native import NativeRMVPE
+    from rvc_amd.rmvpe import RMVPEAMD
+    g = golden("rmvpe")
+    sd = synthetic.rmvpe_state_dict(int(g["seed"]))
+    py = RMVPEAMD(sd, DEV)
+    nat = NativeRMVPE(sd, DEV, window=torch.hann_window(1024), mel_basis=melbasis.mel_filterbank(16000, 1024, 128, 30, 8000))
+    f0 = nat.infer_from_audio(g["audio"], thred=0.03)
+    assert f0.shape == g["f0"].shape and np.max(np.abs(f0 - g["f0"])) < 1e-2  # test_gpu_rmvpe's output bar
+    # same launches and constants as the Python model: bit-identical salience (5 s)
+    wav = torch.from_numpy(synthetic.synthetic_audio(5.0, seed=31)).float().to(DEV)
+    sal_py, Tp = py.salience(py.mel_spectrogram(wav))
+    sal, F = nat.salience(wav)
+    torch.cuda.synchronize()
+    nat.check()
+    py.check_error()
+    assert sal.shape == (1, 360, Tp) and F == 1 + wav.numel() // 160
+    assert torch.equal(sal[0], sal_py)
+    # natively derived window / DFT / mel constants (the window differs from torch's Sleef cosf in a few last
+    # bits): the salience within test_gpu_rmvpe's bar against the reference (3e-5 RMS)
+    nat2 = NativeRMVPE(sd, DEV)
+    sal2, _ = nat2.salience(wav)
+    assert rms(sal2, sal.cpu().numpy()) < 3e-5
+    # B sequences = B single calls
+    wb = torch.stack([wav, wav.flip(0)])
+    both, _ = nat.salience(wb)
+    assert torch.equal(both[0], sal[0]) and torch.equal(both[1], nat.salience(wav.flip(0))[0][0])
