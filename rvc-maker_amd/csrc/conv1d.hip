@@ -17,6 +17,7 @@
 #include "x6_common.h"
 #include <stdlib.h>
 #include <type_traits>
+#include <algorithm>
 
 namespace {
 
@@ -888,14 +889,27 @@ __global__ __launch_bounds__(256) void pack_x6_kernel(const float* w, int64_t to
 int64_t x6_nmf(int64_t Co) { return (Co + 127) / 128 * 8; }
 
 // Split-fp16 image: per output row m, the power-of-2 scale 2^E_m that maps max |w[.][m]| (over every
-// phase, input channel and tap) below 2^14; rs[m] = 2^-E_m.
-__global__ __launch_bounds__(256) void rowscale_f16_kernel(const float* w, int64_t nrow, int Co, int npad, float* rs) {
-    const int m = blockIdx.x * 256 + threadIdx.x;
-    if (m >= npad) return;
+// phase, input channel and tap) below 2^14; rs[m] = 2^-E_m.  Load time only: blocks of 64 columns x 4 row
+// phases walk one row slice each and merge their |max| with an integer atomic max on the float bits
+// (non-negative floats order as their bit patterns) into rs, zeroed before; rowscale_fin turns it into 2^-E.
+__global__ __launch_bounds__(256) void rowscale_f16_kernel(const float* w, int64_t nrow, int Co, unsigned* amax) {
+    const int m = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t r0 = (int64_t)blockIdx.y * nrow / gridDim.y, r1 = (int64_t)(blockIdx.y + 1) * nrow / gridDim.y;
     float am = 0.f;
     if (m < Co)
-        for (int64_t i = 0; i < nrow; ++i) am = fmaxf(am, fabsf(w[i * Co + m]));
-    rs[m] = ldexpf(1.f, -f16_exp(am));
+        for (int64_t i = r0 + (threadIdx.x >> 6); i < r1; i += 4) am = fmaxf(am, fabsf(w[i * Co + m]));
+    __shared__ float red[256];
+    red[threadIdx.x] = am;
+    __syncthreads();
+    if (threadIdx.x < 64 && m < Co) {
+        am = fmaxf(fmaxf(red[threadIdx.x], red[threadIdx.x + 64]), fmaxf(red[threadIdx.x + 128], red[threadIdx.x + 192]));
+        atomicMax(amax + m, __float_as_uint(am));
+    }
+}
+
+__global__ __launch_bounds__(256) void rowscale_fin_kernel(float* rs, int npad) {
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m < npad) rs[m] = ldexpf(1.f, -f16_exp(__uint_as_float(reinterpret_cast<const unsigned*>(rs)[m])));
 }
 
 // KM weights -> the x6 fragment layout [nphase][K][nch][nmf][3][64] x 16 B with plane 0 = fp16 h and
@@ -960,8 +974,11 @@ extern "C" int rvc_conv1d_pack_f16(const float* w_km, int64_t nphase, int64_t Ci
     const int64_t total = nphase * K * nch * nmf * 3 * 64;
     float* rs = reinterpret_cast<float*>(reinterpret_cast<uint4*>(out) + total);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(rowscale_f16_kernel, dim3(cdiv(nmf * 16, 256)), dim3(256), 0, s, w_km, nphase * Ci * K, (int)Co,
-                       nmf * 16, rs);
+    const int64_t nrow = nphase * Ci * K;
+    RVC_HIP(hipMemsetAsync(rs, 0, (size_t)nmf * 16 * 4, s));
+    hipLaunchKernelGGL(rowscale_f16_kernel, dim3(cdiv(Co, 64), (unsigned)std::min<int64_t>(64, cdiv(nrow, 64))),
+                       dim3(256), 0, s, w_km, nrow, (int)Co, reinterpret_cast<unsigned*>(rs));
+    hipLaunchKernelGGL(rowscale_fin_kernel, dim3(cdiv(nmf * 16, 256)), dim3(256), 0, s, rs, nmf * 16);
     hipLaunchKernelGGL(pack_f16_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, w_km, total, (int)Ci, K, (int)Co, nch,
                        nmf, (const float*)rs, (uint4*)out);
     RVC_HIP(hipGetLastError());

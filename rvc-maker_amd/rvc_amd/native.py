@@ -44,6 +44,16 @@ def _params(W: dict):
     return params, keep
 
 
+def export_synth_safetensors(cpt: dict, path: str) -> None:
+    """The .pth's "weight" dict, unchanged (fp16 weight_g / weight_v pairs), as a safetensors file with
+    __metadata__["rvc_synth_cfg"] = the rvc_synth_cfg ints in field order: what a non-Python host
+    (examples/c_host/synth_demo.c) loads and hands to rvc_load_synth."""
+    from safetensors.torch import save_file
+    ints = np.frombuffer(bytes(synth_cfg(cpt)), dtype=np.int32)
+    save_file({k: v.detach().cpu().contiguous() for k, v in cpt["weight"].items()}, path,
+              metadata={"rvc_synth_cfg": " ".join(str(int(i)) for i in ints)})
+
+
 class _Ctx:
     """One rvc_ctx on a device (destroyed with the object)."""
 

@@ -157,3 +157,29 @@ def test_native_rmvpe_matches_golden_and_python(golden):
     wb = torch.stack([wav, wav.flip(0)])
     both, _ = nat.salience(wb)
     assert torch.equal(both[0], sal[0]) and torch.equal(both[1], nat.salience(wav.flip(0))[0][0])
+
+
+def test_c_host_runs_the_synthesizer_through_the_header_alone(tmp_path):
+    """examples/c_host/synth_demo (gcc, no Python / torch in the process) loads the .pth tensors from a
+    safetensors export and runs rvc_synth_infer: bit-identical to NativeSynth on the same inputs and seed."""
+    import os
+    import subprocess
+    from rvc_amd.native import export_synth_safetensors
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "c_host", "synth_demo")
+    assert os.path.exists(exe), "build it: make -C examples/c_host"
+    ck = synthetic.make_synth_ckpt(40000, "v2", seed=21)
+    export_synth_safetensors(ck, str(tmp_path / "model.safetensors"))
+    T, E, sid, seed = 120, 768, 3, 17
+    phone, pitch, pitchf = inputs(T, seed=4)
+    with open(tmp_path / "inputs.bin", "wb") as f:
+        f.write(np.array([T, E, sid, seed], np.int64).tobytes())
+        f.write(phone[0].cpu().numpy().astype(np.float32).tobytes())
+        f.write(pitch[0].cpu().numpy().astype(np.int64).tobytes())
+        f.write(pitchf[0].cpu().numpy().astype(np.float32).tobytes())
+    r = subprocess.run([exe, str(tmp_path / "model.safetensors"), str(tmp_path / "inputs.bin"), str(tmp_path / "out.f32")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(tmp_path / "out.f32", dtype=np.float32)
+    ref = NativeSynth(ck, DEV).infer(phone, torch.tensor([T]), pitch, pitchf, sid, seed=seed)[0]
+    assert got.shape == (T * 400,)
+    assert np.array_equal(got, ref.reshape(-1).cpu().numpy()), r.stdout
