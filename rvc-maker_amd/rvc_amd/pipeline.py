@@ -272,7 +272,10 @@ class VC:
             raise ValueError("pipeline_device_stream: a batched group needs equal-length clips")
         dev = audios[0].device
         caller = torch.cuda.current_stream(dev)
-        front, back = self._aux_stream(dev, "front"), self._aux_stream(dev, "back")
+        back = self._aux_stream(dev, "back")
+        # front pipelines (front + fside stream pairs) taken in turn by consecutive groups, so that one
+        # group's latency-bound front end (U-Net launches, the BiGRU recurrence) overlaps the next one's
+        fronts = [(self._aux_stream(dev, "front", i), self._aux_stream(dev, "fside", i)) for i in range(self.FRONTS)]
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=dev)
         seed0, tp = self.seed, self.t_pad_tgt
@@ -281,6 +284,7 @@ class VC:
             """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event).
             (The synthesizer's TextEncoder / prior / flow stay on the back stream: moved to the front stream they
             made the front end the critical chain, 705 vs 820 xRT.)"""
+            front, side = fronts[g % len(fronts)]
             with torch.cuda.stream(front):
                 front.wait_stream(caller)  # the caller wrote the inputs on its own stream
                 mark("front_start", g, front)
@@ -290,7 +294,6 @@ class VC:
                 filtered = [self.filt(a.contiguous(), self.t_pad, want_f64=pm) for a in group]
                 xps, x64s = [f for f, _ in filtered], [f for _, f in filtered]
                 xp = xps[0] if len(group) == 1 else torch.stack(xps)
-                side = self._aux_stream(dev, "fside")
                 ready = torch.cuda.Event()
                 ready.record(front)
                 with torch.cuda.stream(side):
@@ -355,14 +358,18 @@ class VC:
     STREAM_PRIORITY = {"front": 0, "fside": 0, "back": -1}
     # pool slot per role: streams of equal priority and slot are one stream object
     STREAM_SLOT = {"front": 1, "fside": 0, "back": 0, "side": 0}
+    # front pipelines of the clip stream (RVC_STREAM_FRONTS); pipeline i > 0 takes pool slots 2i, 2i + 1.
+    # Each needs its own hardware queues: the process's GPU_MAX_HW_QUEUES must cover 2 + 2 * FRONTS streams.
+    FRONTS = max(1, int(os.environ.get("RVC_STREAM_FRONTS", "1")))
 
-    def _aux_stream(self, device, role):
+    def _aux_stream(self, device, role, pipe=0):
         """The clip stream's streams: "front" (filtfilt, ContentVec), "fside" (its f0 branch) and "back" (the
         synthesizer).  The back stream runs at high priority: the synthesizers form the critical chain of
         the stream, and the front end's few-block, latency-bound launches fill the CUs between them
         (RVC_AMD_{FRONT,FSIDE,BACK}_PRIORITY override)."""
         prio = int(os.environ.get(f"RVC_AMD_{role.upper()}_PRIORITY", str(self.STREAM_PRIORITY[role])))
-        return self._pooled_stream(device, prio, self.STREAM_SLOT[role])
+        slot = self.STREAM_SLOT[role] if pipe == 0 else 2 * pipe + (role == "front")
+        return self._pooled_stream(device, prio, slot)
 
     def _pooled_stream(self, device, prio, slot):
         """Streams are pooled by (priority, slot) and shared between roles that never run at once (the

@@ -145,7 +145,8 @@ class RMVPEAMD:
         self.w_hh = torch.stack([sd[g + "weight_hh_l0"], sd[g + "weight_hh_l0_reverse"]], 0).float().contiguous().to(dev)
         self.b_hh = torch.stack([sd[g + "bias_hh_l0"], sd[g + "bias_hh_l0_reverse"]], 0).float().contiguous().to(dev)
         self.fc = ops.Conv(sd["fc.1.weight"].float().unsqueeze(-1), sd["fc.1.bias"].float(), device=dev)
-        self.gran = torch.zeros(1024, dtype=torch.int64, device=dev)
+        self.gran = torch.zeros(1024, dtype=torch.int64, device=dev)  # the default stream's BiGRU hand-off scratch
+        self._grans = {}
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         # The f0 is a per-frame decision (argmax over 360 bins, voicing threshold): RMVPE's convs run at the
         # f32-accurate 6-pass arithmetic whatever ops.precision says (None = follow it).  At 3 passes the
@@ -242,12 +243,25 @@ class RMVPEAMD:
         ops.img_to_seq(img, seq, 3, H, W)
         return seq
 
+    def gran_ws(self, n: int = 1024) -> torch.Tensor:
+        """BiGRU hand-off scratch for the current stream: recurrences running at once on different streams (the
+        clip stream's alternating front pipelines) must not share one."""
+        s = torch.cuda.current_stream(self.device)
+        if s == torch.cuda.default_stream(self.device) and n <= self.gran.numel():
+            return self.gran
+        key = s.stream_id
+        g = self._grans.get(key)
+        if g is None or g.numel() < n:
+            g = torch.zeros(n, dtype=torch.int64, device=self.device)
+            self._grans[key] = g
+        return g
+
     def head(self, seq: torch.Tensor) -> torch.Tensor:
         """BiGRU + Linear + Sigmoid (RMVPE.py:254-260, 141): seq [384][Tp] -> salience [360][Tp]."""
         Tp = seq.shape[-1]
         gi = self.w_ih(seq)  # [1536][Tp]
         y = torch.empty(512, Tp, device=seq.device)
-        ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran, self.err, Tp)
+        ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran_ws(), self.err, Tp)
         return self.fc(y, out_act=ACT_SIGMOID)
 
     def salience(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
@@ -304,7 +318,7 @@ class RMVPEAMD:
             ops.img_to_seq(img[b], seq[b], 3, H, W)
         gi = self.w_ih(seq)  # [B][1536][Tp]
         y = torch.empty(B, 512, Tp, device=dev)
-        gran = self.gran if B == 1 else torch.zeros(1024 * min(B, ops.GRU_B_MAX), dtype=torch.int64, device=dev)
+        gran = self.gran_ws(1024 * min(B, ops.GRU_B_MAX))
         ops.bigru_batched(gi, self.w_hh, self.b_hh, y, gran, self.err, B, Tp)
         return self.fc(y, out_act=ACT_SIGMOID), Tp
 
