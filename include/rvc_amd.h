@@ -366,13 +366,13 @@ int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T,
  *                              (a stream sync when it does); nothing else synchronises. */
 typedef struct rvc_ctx rvc_ctx;
 
-enum { RVC_DT_F32 = 0, RVC_DT_F16 = 1 };
+enum { RVC_DT_F32 = 0, RVC_DT_F16 = 1, RVC_DT_F64 = 2 };
 enum { RVC_PREC_FP32 = 0, RVC_PREC_BF16 = 1, RVC_PREC_BF16X3 = 3, RVC_PREC_FP32X6 = 6, RVC_PREC_F16X3 = 16 };
 
 typedef struct rvc_param {
     const char* name;  /* state-dict key, e.g. "dec.ups.0.weight_v" */
     const void* data;  /* host, dense row-major                     */
-    int dtype;         /* RVC_DT_F32 / RVC_DT_F16                    */
+    int dtype;         /* RVC_DT_F32 / RVC_DT_F16 (RVC_DT_F64: constants) */
     int ndim;
     int64_t shape[4];
 } rvc_param;
@@ -428,6 +428,19 @@ int64_t rvc_rmvpe_frames(int64_t n16k);
 int64_t rvc_rmvpe_salience_ld(int64_t n16k);
 int rvc_rmvpe_forward(rvc_ctx* ctx, const float* wav, int64_t B, int64_t N, float* salience, rvc_stream_t stream);
 int rvc_rmvpe_check(rvc_ctx* ctx);
+
+/* CREPE f0 (VC.get_f0_crepe, convert.py:230-237; CREPE.py, any capacity -- taken from the conv shapes).
+ * params = the CREPE state dict (conv{1..6}, conv{1..6}_BN, classifier); BatchNorm (eps 1e-3) folded at load
+ * in f32 as rvc_amd/crepe.py (or taken from optional "conv{i}_BN.alpha" / ".beta" f32 [C]); optional "log_trans"
+ * f64 [360][360] (default: the 12-bin triangular transition matrix's log, computed natively).
+ *   rvc_crepe_f0: the padded 16 kHz audio f32 [N] (device) -> coarse int64 [T], pitchf f32 [T],
+ *   T = rvc_rmvpe_frames(N): 1024-sample frames at hop 160, the network in 512-frame batches, the librosa
+ *   Viterbi per batch with the dither (device f32 cents [T], or NULL = the triangular law drawn on the device
+ *   from seed), periodicity smoothing, then get_f0's pitch shift (semitones), `post` and the mel quantiser.
+ *   probs (optional, device f32 [360][T]) receives the sigmoid outputs. */
+int rvc_load_crepe(rvc_ctx* ctx, const rvc_param* params, int n);
+int rvc_crepe_f0(rvc_ctx* ctx, const float* audio, int64_t N, const float* dither, uint64_t seed, double pitch_shift,
+                 const rvc_f0_post* post, float* probs, int64_t* coarse, float* pitchf, rvc_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,7 @@ void rvc_set_error(const char* fmt, ...);
 struct Synth;
 struct ContentVec;
 struct Rmvpe;
+struct Crepe;
 
 struct rvc_ctx {
     int device = 0;
@@ -48,11 +49,13 @@ struct rvc_ctx {
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;
+    Crepe* cr = nullptr;
 };
 
 void synth_delete(Synth* s);
 void contentvec_delete(ContentVec* m);
 void rmvpe_delete(Rmvpe* m);
+void crepe_delete(Crepe* m);
 
 namespace rvcm {
 
@@ -99,6 +102,9 @@ inline HostT to_host(const rvc_param& p) {
     if (p.dtype == RVC_DT_F16) {
         const uint16_t* s = (const uint16_t*)p.data;
         for (int64_t i = 0; i < n; ++i) t.v[i] = half_to_float(s[i]);
+    } else if (p.dtype == RVC_DT_F64) {
+        const double* s = (const double*)p.data;
+        for (int64_t i = 0; i < n; ++i) t.v[i] = (float)s[i];
     } else {
         memcpy(t.v.data(), p.data, n * 4);
     }
@@ -153,7 +159,7 @@ struct Params {
 inline int index_params(const rvc_param* params, int n, Params& P, const char* who) {
     for (int i = 0; i < n; ++i) {
         MCHECK(params[i].name && params[i].data && params[i].ndim >= 1 && params[i].ndim <= 4 &&
-                   (params[i].dtype == RVC_DT_F32 || params[i].dtype == RVC_DT_F16),
+                   (params[i].dtype == RVC_DT_F32 || params[i].dtype == RVC_DT_F16 || params[i].dtype == RVC_DT_F64),
                "%s: bad param %d", who, i);
         P.by[params[i].name] = &params[i];
     }

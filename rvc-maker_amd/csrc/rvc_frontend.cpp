@@ -670,3 +670,223 @@ extern "C" int rvc_rmvpe_check(rvc_ctx* c) {
     }
     return RVC_OK;
 }
+
+// ------------------------------------------------------------------ CREPE (rvc_amd/crepe.py)
+struct Crepe : ModelBase {
+    ConvW conv[6], classifier;
+    float *alpha[6] = {nullptr}, *beta[6] = {nullptr};
+    double* log_trans = nullptr;
+    double log_off = 0, log_p_init = 0;
+    int lo = 0, hi = 0;
+    std::map<int64_t, int64_t*> seq_off;  // per length T: batch offsets, resident (uploaded once)
+};
+
+void crepe_delete(Crepe* m) {
+    if (!m) return;
+    m->release();
+    delete m;
+}
+
+namespace fem {
+
+constexpr int kCrepeBatch = 512;  // predict(batch_size=512): the Viterbi runs per batch
+
+// _freq_to_bin (crepe.py, CREPE.py:120-121) in f32 steps: ((1200 log2(f / 10)) - 1997.379...) / 20
+int crepe_bin(float f, bool up) {
+#pragma clang fp contract(off)
+    const float a = f / 10.f;
+    const float l = log2f(a);
+    const float c = 1200.f * l;
+    const float d = c - (float)1997.3794084376191;
+    const float e = d / 20.f;
+    return (int)(up ? ceilf(e) : floorf(e));
+}
+
+// sigmoid outputs of frames [frame0, frame0 + nb) -> out [360][nb] (CrepeAMD.probabilities)
+int crepe_batch(rvc_ctx* c, Crepe& M, Scratch& sc, const float* audio, int64_t N, int64_t frame0, int64_t nb, float* out,
+                hipStream_t s) {
+    float* frames = sc.take(nb * 1024);
+    RUN(rvc_crepe_frames(audio, N, kHop, frame0, nb, frames, s));
+    const float* x = frames;
+    int64_t L = 1024;
+    for (int i = 0; i < 6; ++i) {
+        const ConvW& cw = M.conv[i];
+        CallOpts o;
+        o.B = nb;
+        o.out_act = RVC_ACT_RELU;
+        int64_t Lout;
+        if (i == 0) {
+            Lout = (L + 2 * 254 - 512) / 4 + 1;
+            o.stride = 4;
+            o.pad = 254;
+            o.x_bstride = L;
+        } else {
+            Lout = L;  // pad (31, 32) with k = 64
+            o.pad = 31;
+            o.x_bstride = cw.Ci * L;
+        }
+        o.Lout = Lout;
+        float* y = sc.take(nb * cw.Co * Lout);
+        RUN(conv(c, M, cw, x, L, y, o, s));
+        const int64_t Lp = Lout / 2;
+        float* h = sc.take(nb * cw.Co * Lp);
+        if (i < 5) {
+            RUN(rvc_bn_maxpool(y, nb, cw.Co, Lout, M.alpha[i], M.beta[i], h, cw.Co * Lp, Lp, 1, s));
+        } else {  // classifier input [c * Lp + h][frame]
+            RUN(rvc_bn_maxpool(y, nb, cw.Co, Lout, M.alpha[i], M.beta[i], h, 1, Lp * nb, nb, s));
+        }
+        x = h;
+        L = Lp;
+    }
+    CallOpts o;
+    o.out_act = RVC_ACT_SIGMOID;
+    RUN(conv(c, M, M.classifier, x, nb, out, o, s));
+    return RVC_OK;
+}
+
+int crepe_run(rvc_ctx* c, Crepe& M, Scratch& sc, const float* audio, int64_t N, const float* dither, uint64_t seed,
+              double pitch_shift, const rvc_f0_post* post, float* probs_out, int64_t* coarse, float* pitchf,
+              const int64_t* seq_off, hipStream_t s) {
+    const int64_t T = 1 + N / kHop;
+    float* probs = sc.take(kClass * T);
+    float* pb = sc.take(kClass * (T < kCrepeBatch ? T : kCrepeBatch));
+    int nseq = 0;
+    for (int64_t a = 0; a < T; a += kCrepeBatch, ++nseq) {
+        const int64_t b = a + kCrepeBatch < T ? a + kCrepeBatch : T;
+        MTRY(crepe_batch(c, M, sc, audio, N, a, b - a, pb, s));
+        RUN(hipMemcpy2DAsync(probs + a, T * 4, pb, (b - a) * 4, (b - a) * 4, kClass, hipMemcpyDeviceToDevice, s) ==
+                    hipSuccess
+                ? RVC_OK
+                : RVC_EHIP);
+    }
+    if (!dither) {
+        float* d = sc.take(T);
+        RUN(rvc_rand_triang(d, T, -20.f, 20.f, seed, 0, nullptr, s));
+        dither = d;
+    }
+    const int64_t need = rvc_crepe_decode_ws_bytes(T);
+    float* f0r = sc.take(T);
+    float* pdr = sc.take(T);
+    if (!sc.dry) {
+        // the sigmoid outputs before the decode masks them in place outside [lo, hi)
+        if (probs_out) MHIP(hipMemcpyAsync(probs_out, probs, kClass * T * 4, hipMemcpyDeviceToDevice, s));
+        MTRY(ensure_ws(M, need, s));
+        MTRY(rvc_crepe_decode(probs, T, M.lo, M.hi, seq_off, nseq, M.log_trans, M.log_off, M.log_p_init, dither, M.ws,
+                              need, f0r, pdr, s));
+    }
+    const double mel_min = 1127 * log(1 + 50.0 / 700), mel_max = 1127 * log(1 + 1100.0 / 700);
+    RUN(rvc_crepe_smooth_coarse(f0r, pdr, T, (float)pow(2.0, pitch_shift / 12), mel_min, mel_max, post, coarse, pitchf,
+                                s));
+    return RVC_OK;
+}
+
+}  // namespace fem
+
+extern "C" int rvc_load_crepe(rvc_ctx* c, const rvc_param* params, int n) {
+    MCHECK(c && params && n > 0, "rvc_load_crepe: null argument");
+    Params P;
+    MTRY(index_params(params, n, P, "rvc_load_crepe"));
+    MHIP(hipSetDevice(c->device));
+    crepe_delete(c->cr);
+    c->cr = new Crepe();
+    Crepe& M = *c->cr;
+    HostT w, b;
+#define GET(k, t) MCHECK(P.get(k, t), "rvc_load_crepe: missing %s", P.missing.c_str())
+    const float eps = 0.0010000000474974513f;  // BatchNorm eps 1e-3 as f32 (crepe.py BN_EPS)
+    for (int i = 0; i < 6; ++i) {
+        const std::string si = std::to_string(i + 1);
+        GET("conv" + si + ".weight", w);  // [Co][Ci][k][1]
+        GET("conv" + si + ".bias", b);
+        MCHECK(w.shape.size() == 4 && w.dim(3) == 1, "rvc_load_crepe: conv%s.weight must be [Co][Ci][k][1]", si.c_str());
+        w.shape.pop_back();
+        MTRY(make_conv(c, M, w, &b, M.conv[i]));
+        HostT g, bb, mu, var;
+        const std::string p = "conv" + si + "_BN.";
+        GET(p + "weight", g);
+        GET(p + "bias", bb);
+        GET(p + "running_mean", mu);
+        GET(p + "running_var", var);
+        std::vector<float> al(g.v.size()), be(g.v.size());
+        for (size_t k = 0; k < g.v.size(); ++k) {  // f32 like torch: invstd, alpha = w invstd, beta = b - mean alpha
+#pragma clang fp contract(off)
+            const float inv = 1.0f / sqrtf(var.v[k] + eps);
+            al[k] = g.v[k] * inv;
+            const float ma = mu.v[k] * al[k];
+            be[k] = bb.v[k] - ma;
+        }
+        if (P.has(p + "alpha") && P.has(p + "beta")) {  // a host's own fold (torch's CPU sqrt is not IEEE-exact)
+            HostT a2, b2;
+            GET(p + "alpha", a2);
+            GET(p + "beta", b2);
+            MCHECK(a2.v.size() == al.size() && b2.v.size() == be.size(), "rvc_load_crepe: %salpha/beta size", p.c_str());
+            al = a2.v;
+            be = b2.v;
+        }
+        MTRY(upload(M, al, &M.alpha[i]));
+        MTRY(upload(M, be, &M.beta[i]));
+    }
+    MCHECK(M.conv[0].K == 512 && M.conv[0].Ci == 1, "rvc_load_crepe: conv1 must be Conv2d(1, C, (512, 1), stride 4)");
+    GET("classifier.weight", w);
+    GET("classifier.bias", b);
+    const int64_t nfeat = w.dim(1), c6 = M.conv[5].Co, Hh = nfeat / c6;
+    MCHECK(w.dim(0) == kClass && nfeat == c6 * Hh, "rvc_load_crepe: classifier must be Linear(%lld, 360)", (long long)nfeat);
+    {  // [360][h * c6 + c] -> the flatten order [c * H + h] of the strided bn_maxpool output
+        HostT wp;
+        wp.shape = {kClass, nfeat, 1};
+        wp.v.resize(w.v.size());
+        for (int64_t o = 0; o < kClass; ++o)
+            for (int64_t cc = 0; cc < c6; ++cc)
+                for (int64_t h = 0; h < Hh; ++h) wp.v[(o * c6 + cc) * Hh + h] = w.v[(o * Hh + h) * c6 + cc];
+        MTRY(make_conv(c, M, wp, &b, M.classifier));
+    }
+    std::vector<double> lt((size_t)kClass * kClass);
+    const double tiny = 2.2250738585072014e-308;  // np.finfo(np.float64).tiny
+    if (P.has("log_trans")) {
+        const rvc_param* q = P.by["log_trans"];
+        MCHECK(q->dtype == RVC_DT_F64 && q->ndim == 2 && q->shape[0] == kClass && q->shape[1] == kClass,
+               "rvc_load_crepe: log_trans must be f64 [360][360]");
+        memcpy(lt.data(), q->data, lt.size() * 8);
+    } else {  // tr[i][j] = max(12 - |i - j|, 0) / row sum; log_trans[j][k] = log(tr[k][j] + tiny)
+        std::vector<double> rs(kClass, 0.0);
+        for (int i = 0; i < kClass; ++i)
+            for (int j = 0; j < kClass; ++j) rs[i] += fmax(12.0 - fabs((double)(j - i)), 0.0);
+        for (int j = 0; j < kClass; ++j)
+            for (int k = 0; k < kClass; ++k) lt[(size_t)j * kClass + k] = log(fmax(12.0 - fabs((double)(j - k)), 0.0) / rs[k] + tiny);
+    }
+#undef GET
+    MTRY(dev_alloc(M, lt.size() * 8, (void**)&M.log_trans));
+    MHIP(hipMemcpy(M.log_trans, lt.data(), lt.size() * 8, hipMemcpyHostToDevice));
+    M.log_off = log(0.0 + tiny);
+    M.log_p_init = log(1.0 / 360 + tiny);
+    M.lo = crepe_bin(50.f, false);
+    M.hi = crepe_bin(1100.f, true);
+    MHIP(hipDeviceSynchronize());
+    M.loaded = true;
+    return RVC_OK;
+}
+
+extern "C" int rvc_crepe_f0(rvc_ctx* c, const float* audio, int64_t N, const float* dither, uint64_t seed,
+                            double pitch_shift, const rvc_f0_post* post, float* probs, int64_t* coarse, float* pitchf,
+                            rvc_stream_t stream) {
+    MCHECK(c && c->cr && c->cr->loaded, "rvc_crepe_f0: no CREPE loaded");
+    MCHECK(audio && coarse && pitchf && N >= 1, "rvc_crepe_f0: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    MHIP(hipSetDevice(c->device));
+    Crepe& M = *c->cr;
+    const int64_t T = 1 + N / kHop;
+    int64_t*& so = M.seq_off[T];
+    if (!so) {  // once per length, like crepe.py's resident offsets
+        std::vector<int64_t> off;
+        for (int64_t a = 0; a < T; a += kCrepeBatch) off.push_back(a);
+        off.push_back(T);
+        MTRY(dev_alloc(M, off.size() * 8, (void**)&so));
+        MHIP(hipMemcpy(so, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+    }
+    Scratch sc;
+    MTRY(crepe_run(c, M, sc, audio, N, dither, seed, pitch_shift, post, probs, coarse, pitchf, so, s));
+    MTRY(ensure_arena(M, sc.off, s));
+    Scratch run;
+    run.dry = false;
+    run.base = M.arena;
+    return crepe_run(c, M, run, audio, N, dither, seed, pitch_shift, post, probs, coarse, pitchf, so, s);
+}

@@ -372,6 +372,7 @@ extern "C" void rvc_ctx_destroy(rvc_ctx* c) {
         synth_delete(c->syn);
         contentvec_delete(c->cv);
         rmvpe_delete(c->rm);
+        crepe_delete(c->cr);
     }
     delete c;
 }

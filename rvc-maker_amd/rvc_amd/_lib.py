@@ -162,6 +162,9 @@ SIGNATURES = {
     "rvc_rmvpe_salience_ld": [c_int64],
     "rvc_rmvpe_forward": [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
     "rvc_rmvpe_check": [c_void_p],
+    "rvc_load_crepe": [c_void_p, POINTER(Param), c_int],
+    "rvc_crepe_f0": [c_void_p, c_void_p, c_int64, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p],
     "rvc_synth_infer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
                         c_void_p, c_void_p],
 }

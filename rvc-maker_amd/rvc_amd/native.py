@@ -28,7 +28,7 @@ def _params(W: dict):
     keep, params = [], (_lib.Param * len(W))()
     for i, (k, v) in enumerate(W.items()):
         a = torch.as_tensor(v).detach().cpu().contiguous()
-        if a.dtype not in (torch.float16, torch.float32):
+        if a.dtype not in (torch.float16, torch.float32, torch.float64):
             a = a.float()
         arr = np.ascontiguousarray(a.numpy())
         if not 1 <= arr.ndim <= 4:
@@ -37,7 +37,7 @@ def _params(W: dict):
         keep += [arr, name]
         p = params[i]
         p.name, p.data = name, ctypes.c_void_p(arr.ctypes.data)
-        p.dtype = 1 if arr.dtype == np.float16 else 0
+        p.dtype = {np.dtype(np.float16): 1, np.dtype(np.float64): 2}.get(arr.dtype, 0)
         p.ndim = arr.ndim
         for d, s in enumerate(arr.shape):
             p.shape[d] = s
@@ -235,3 +235,35 @@ class NativeRMVPE(_Ctx):
         out = f0.cpu().numpy()
         self.check()
         return out
+
+
+class NativeCrepe(_Ctx):
+    """VC.get_f0_crepe + get_f0's quantiser through rvc_load_crepe / rvc_crepe_f0."""
+
+    def __init__(self, sd: dict, device: str = "cuda", precision: str = "fp32", log_trans=None, bn=None):
+        """``bn``: optional [(alpha, beta)] x 6 folded BatchNorms (CrepeAMD.bns) instead of the library's fold."""
+        super().__init__(device, precision)
+        W = {k: v for k, v in sd.items() if torch.as_tensor(v).is_floating_point()}
+        for i, (a, b) in enumerate(bn or []):
+            W[f"conv{i + 1}_BN.alpha"], W[f"conv{i + 1}_BN.beta"] = a.cpu(), b.cpu()
+        if log_trans is not None:
+            W["log_trans"] = torch.as_tensor(log_trans, dtype=torch.float64)
+        params, keep = _params(W)
+        check(self.lib.rvc_load_crepe(self.ctx, params, len(W)), "rvc_load_crepe")
+        del keep
+
+    def f0_device(self, audio, pitch_shift: float = 0.0, dither=None, seed: int = 0, want_probs: bool = False):
+        """audio [N] f32 (device) -> (coarse int64 [T], pitchf f32 [T], probs [360][T] | None)."""
+        audio = audio.to(self.device, torch.float32).reshape(-1).contiguous()
+        N = audio.numel()
+        T = 1 + N // 160
+        coarse = torch.empty(T, dtype=torch.int64, device=self.device)
+        pitchf = torch.empty(T, device=self.device)
+        probs = torch.empty(360, T, device=self.device) if want_probs else None
+        d = None
+        if dither is not None:
+            d = torch.as_tensor(np.asarray(dither, dtype=np.float32)).to(self.device).contiguous()
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        check(self.lib.rvc_crepe_f0(self.ctx, p(audio), N, p(d), int(seed), float(pitch_shift), None, p(probs),
+                                    p(coarse), p(pitchf), self.stream()), "rvc_crepe_f0")
+        return coarse, pitchf, probs

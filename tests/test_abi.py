@@ -57,6 +57,8 @@ def test_model_api_rejects_bad_arguments_without_gpu():
     assert lib.rvc_load_rmvpe(None, None, 0) == -22
     assert lib.rvc_rmvpe_forward(None, None, 1, 16000, None, None) == -22
     assert lib.rvc_rmvpe_check(None) == -22
+    assert lib.rvc_load_crepe(None, None, 0) == -22
+    assert lib.rvc_crepe_f0(None, None, 16000, None, 0, 0.0, None, None, None, None, None) == -22
 
 
 def test_model_api_size_queries():

@@ -183,3 +183,30 @@ def test_c_host_runs_the_synthesizer_through_the_header_alone(tmp_path):
     ref = NativeSynth(ck, DEV).infer(phone, torch.tensor([T]), pitch, pitchf, sid, seed=seed)[0]
     assert got.shape == (T * 400,)
     assert np.array_equal(got, ref.reshape(-1).cpu().numpy()), r.stdout
+
+
+@pytest.mark.parametrize("capacity,seconds", [("tiny", 6.0), ("full", 2.5)])
+def test_native_crepe_bit_identical_to_python(capacity, seconds):
+    from rvc_amd.crepe import CrepeAMD
+    from rvc_amd.native import NativeCrepe
+    sd = synthetic.crepe_state_dict(31, capacity)
+    py = CrepeAMD(sd, capacity, DEV)
+    nat = NativeCrepe(sd, DEV, log_trans=py.log_trans.cpu(), bn=py.bns)  # the Python model's own constants
+    wav = torch.from_numpy(synthetic.synthetic_audio(seconds, seed=41)).float().to(DEV)
+    T = 1 + wav.numel() // 160  # 6 s: two 512-frame Viterbi batches
+    dither = np.random.default_rng(3).triangular(-20.0, 0.0, 20.0, size=T)
+    py.dither_fn = lambda n: dither
+    trace = {}
+    c_py, f_py = py.f0_device(wav, 2.0, trace=trace)
+    c_n, f_n, probs = nat.f0_device(wav, 2.0, dither=dither, want_probs=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(probs.t().cpu().numpy(), trace["probs"])
+    assert torch.equal(c_n, c_py) and torch.equal(f_n, f_py)
+    # natively derived BatchNorm fold (IEEE sqrt; torch's CPU sqrt is off by an ulp on a few channels) and
+    # transition matrix: the same probabilities to f32 rounding, the same coarse track
+    c2, f2, p2 = NativeCrepe(sd, DEV).f0_device(wav, 2.0, dither=dither, want_probs=True)
+    assert float((p2 - probs).abs().max()) < 1e-5
+    assert float((c2 == c_py).float().mean()) > 0.99
+    # device dither (NULL): finite, in the quantiser's range
+    c3, f3, _ = nat.f0_device(wav, 0.0, seed=5)
+    assert int(c3.min()) >= 1 and int(c3.max()) <= 255 and torch.isfinite(f3).all()
