@@ -1,5 +1,6 @@
 // Normalisations over the channels-first activations ([B][C][T], t contiguous).
 #include "rvc_common.h"
+#include <stdlib.h>
 
 // ---------------------------------------------------------------- LayerNorm over channels
 // out[c][t] = (v - mean_t) * rstd_t * gamma[c] + beta[c],  v = x[c][t] (+ res[c][t])
@@ -66,10 +67,84 @@ __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const
     for (int c = grp; c < C; c += 16) ob[(int64_t)c * T + t] = (tile[c * 17 + col] - mean) * rstd * gamma[c] + beta[c];
 }
 
+// Register-resident form for the path's small column counts (ContentVec: 1599 columns, TextEncoder: 3198):
+// a block of 16 waves owns 16 columns, 64 channel groups of CPT channels each; every thread loads its CPT
+// values (x + res) at once, keeps them in registers through the two-pass mean / variance (sums reduced over the
+// wave's 4 groups by shuffles, then over the 16 waves through LDS) and writes the normalised values from
+// them.  4x the waves of the LDS-tile form per column block, no tile round trip.
+template <int CPT>
+__global__ __launch_bounds__(1024) void layernorm_cf_reg_kernel(const float* x, const float* res, const float* gamma,
+                                                                const float* beta, float* out, int C, int64_t T,
+                                                                float eps) {
+    const int tid = threadIdx.x;
+    const int col = tid & 15, grp = tid >> 4, wv = tid >> 6;  // 16 columns x 64 channel groups
+    const int b = blockIdx.y;
+    const int64_t t = (int64_t)blockIdx.x * 16 + col;
+    const bool ok = t < T;
+    const int64_t tc = ok ? t : T - 1;
+    const float* xb = x + (int64_t)b * C * T + tc;
+    const float* rb = res ? res + (int64_t)b * C * T + tc : nullptr;
+    float v[CPT], r[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = grp + 64 * u;
+        const int cc = c < C ? c : C - 1;
+        v[u] = xb[(int64_t)cc * T];
+        r[u] = rb ? rb[(int64_t)cc * T] : 0.f;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        v[u] = rb ? v[u] + r[u] : v[u];
+        if (grp + 64 * u < C) s += v[u];
+    }
+    __shared__ float red[2][16][16];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if ((tid & 63) < 16) red[0][wv][col] = s;
+    __syncthreads();
+    float mean = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) mean += red[0][w][col];
+    mean /= (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const float d = v[u] - mean;
+        if (grp + 64 * u < C) q += d * d;
+    }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    if ((tid & 63) < 16) red[1][wv][col] = q;
+    __syncthreads();
+    float var = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) var += red[1][w][col];
+    const float rstd = 1.0f / sqrtf(var / (float)C + eps);
+    if (!ok) return;
+    float* ob = out + (int64_t)b * C * T + t;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = grp + 64 * u;
+        if (c < C) ob[(int64_t)c * T] = (v[u] - mean) * rstd * gamma[c] + beta[c];
+    }
+}
+
 extern "C" int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out,
                                 int64_t B, int64_t C, int64_t T, float eps, rvc_stream_t stream) {
     RVC_CHECK_ARG(x && gamma && beta && out && B > 0 && C > 0 && T > 0, "layernorm_cf: bad args");
     RVC_CHECK_ARG(C <= 2048, "layernorm_cf: C=%lld > 2048", (long long)C);
+    static const int reg = getenv("RVC_LN_REG") ? atoi(getenv("RVC_LN_REG")) : 1;
+    // measured (scripts/micro.py norms): C=768 T=1599 19.6 -> 12.0 us, C=512 12.0 -> 9.0; C=192 T=3198 8.7 -> 9.2
+    // (the LDS-tile form keeps C <= 256)
+    if (reg && C > 256 && C <= 768) {
+        const dim3 grid(cdiv(T, 16), (unsigned)B);
+        hipStream_t s = (hipStream_t)stream;
+        if (C <= 512) hipLaunchKernelGGL(layernorm_cf_reg_kernel<8>, grid, dim3(1024), 0, s, x, res, gamma, beta, out, (int)C, T, eps);
+        else hipLaunchKernelGGL(layernorm_cf_reg_kernel<12>, grid, dim3(1024), 0, s, x, res, gamma, beta, out, (int)C, T, eps);
+        RVC_HIP(hipGetLastError());
+        return RVC_OK;
+    }
     size_t lds = (size_t)(C + 16) * 17 * 4;
     hipLaunchKernelGGL(layernorm_cf_kernel, dim3(cdiv(T, 16), (unsigned)B), dim3(256), lds, (hipStream_t)stream, x,
                        res, gamma, beta, out, (int)C, T, eps);
