@@ -439,6 +439,26 @@ int rvc_rmvpe_check(rvc_ctx* ctx);
  *   from seed), periodicity smoothing, then get_f0's pitch shift (semitones), `post` and the mel quantiser.
  *   probs (optional, device f32 [360][T]) receives the sigmoid outputs. */
 int rvc_load_crepe(rvc_ctx* ctx, const rvc_param* params, int n);
+
+/* One VC.pipeline segment (convert.py:388-458 for N + 160 <= x_max s, f0_method "rmvpe", no index, volume
+ * envelope 1): filtfilt + reflect padding by x_pad s, RMVPE f0 (thred 0.03, pitch shift), ContentVec (v2: layer 12;
+ * v1: layer 9 + final_proj), phone upsample + protect, Synthesizer.infer with device noise at `seed`, the
+ * x_pad trim at tgt_sr and the peak normalisation.  Needs ContentVec, RMVPE and the synthesizer loaded on the
+ * context; audio f32 [N] 16 kHz (device) -> out f32 [rvc_vc_out_len(ctx, N, args)] (device).  Equal to
+ * rvc_amd.pipeline.VC.pipeline_device on the same models and seed (tests/test_gpu_native.py). */
+typedef struct rvc_vc_args {
+    int64_t sid;
+    double pitch_shift; /* semitones */
+    float protect;
+    int version;        /* 1 or 2 */
+    int x_pad, x_max;   /* Config: 1 and 41 at full precision */
+    int tgt_sr, _pad0;
+    uint64_t seed;
+} rvc_vc_args;
+
+int64_t rvc_vc_out_len(const rvc_ctx* ctx, int64_t N, const rvc_vc_args* args);
+int rvc_vc_convert(rvc_ctx* ctx, const float* audio, int64_t N, const rvc_vc_args* args, float* out,
+                   rvc_stream_t stream);
 int rvc_crepe_f0(rvc_ctx* ctx, const float* audio, int64_t N, const float* dither, uint64_t seed, double pitch_shift,
                  const rvc_f0_post* post, float* probs, int64_t* coarse, float* pitchf, rvc_stream_t stream);
 

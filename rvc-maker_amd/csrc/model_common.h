@@ -41,6 +41,7 @@ struct Synth;
 struct ContentVec;
 struct Rmvpe;
 struct Crepe;
+struct VcState;
 
 struct rvc_ctx {
     int device = 0;
@@ -50,12 +51,21 @@ struct rvc_ctx {
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;
     Crepe* cr = nullptr;
+    VcState* vc = nullptr;  // rvc_vc_convert's own scratch
 };
 
 void synth_delete(Synth* s);
 void contentvec_delete(ContentVec* m);
 void rmvpe_delete(Rmvpe* m);
 void crepe_delete(Crepe* m);
+void vc_delete(VcState* v);
+
+// internal entry points shared by the model files (rvc_vc_convert drives them)
+int synth_run_cf(rvc_ctx* c, const float* phone_cf, const int64_t* pitch, const float* pitchf, int64_t T, int64_t sid,
+                 uint64_t seed, float* wav, hipStream_t s);  // phone channels-first [E][T]
+bool synth_info(const rvc_ctx* c, int* emb_dim, int* upp);  // loaded? + its phone width and upsampling
+int contentvec_cf(rvc_ctx* c, const float* wav, int64_t N, int out_layer, int final_proj, float* feats_cf,
+                  hipStream_t s);  // -> [C][T_f]
 
 namespace rvcm {
 
@@ -400,6 +410,16 @@ struct Scratch {
     do {                       \
         if (!sc.dry) MTRY(call); \
     } while (0)
+
+// fixed layouts: 256-B aligned float offsets
+struct Plan {
+    int64_t off = 0;
+    int64_t take(int64_t n) {  // 256-B aligned float offsets
+        const int64_t o = off;
+        off += (n + 63) & ~int64_t(63);
+        return o;
+    }
+};
 
 inline bool env_on(const char* name) {
     const char* v = getenv(name);

@@ -72,7 +72,7 @@ int64_t cv_frames(int64_t n) {
 
 // ------------------------------------------------------------------ ContentVec forward, one sequence
 int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, int out_layer, int final_proj,
-           float* feats, hipStream_t s) {
+           float* feats, hipStream_t s, bool cf_out = false) {
     const int64_t E = M.E;
     // feature extractor (fairseq.py:1165-1195): conv(k10 s5) + GroupNorm + GELU, then conv + GELU
     int64_t L = N;
@@ -151,11 +151,16 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
         RUN(conv(c, M, Ly.fc2, hb, T, yb, o, s));
         RUN(rvc_layernorm_cf(xe, yb, Ly.ln2g, Ly.ln2b, xe, 1, E, T, 1e-5f, s));
     }
-    if (final_proj) {
+    if (final_proj && cf_out) {  // VC.features_device: final_proj on the channels-first features
+        CallOpts o;
+        RUN(conv(c, M, M.final_proj, xe, T, feats, o, s));
+    } else if (final_proj) {
         float* fp = sc.take(M.final_proj.Co * T);
         CallOpts o;
         RUN(conv(c, M, M.final_proj, xe, T, fp, o, s));
         RUN(rvc_transpose(fp, feats, 1, M.final_proj.Co, T, s));
+    } else if (cf_out) {
+        RUN(hipMemcpyAsync(feats, xe, E * T * 4, hipMemcpyDeviceToDevice, s) == hipSuccess ? RVC_OK : RVC_EHIP);
     } else {
         RUN(rvc_transpose(xe, feats, 1, E, T, s));
     }
@@ -889,4 +894,115 @@ extern "C" int rvc_crepe_f0(rvc_ctx* c, const float* audio, int64_t N, const flo
     run.dry = false;
     run.base = M.arena;
     return crepe_run(c, M, run, audio, N, dither, seed, pitch_shift, post, probs, coarse, pitchf, so, s);
+}
+
+int contentvec_cf(rvc_ctx* c, const float* wav, int64_t N, int out_layer, int final_proj, float* feats_cf,
+                  hipStream_t s) {
+    MCHECK(c && c->cv && c->cv->loaded, "rvc_vc_convert: no ContentVec loaded");
+    ContentVec& M = *c->cv;
+    Scratch sc;
+    MTRY(cv_one(c, M, sc, wav, N, out_layer, final_proj, feats_cf, s, true));
+    MTRY(ensure_arena(M, sc.off, s));
+    Scratch run;
+    run.dry = false;
+    run.base = M.arena;
+    return cv_one(c, M, run, wav, N, out_layer, final_proj, feats_cf, s, true);
+}
+
+// ------------------------------------------------------------------ one VC.pipeline segment (rvc_amd/pipeline.py)
+struct VcState : ModelBase {};
+
+void vc_delete(VcState* v) {
+    if (!v) return;
+    v->release();
+    delete v;
+}
+
+namespace {
+
+// signal.butter(N=5, Wn=48, btype="high", fs=16000) (convert.py:30) and lfilter_zi of it, as scipy gives them
+const double kBH[6] = {0.96996064518384473, -4.8498032259192234, 9.6996064518384468,
+                       -9.6996064518384468, 4.8498032259192234, -0.96996064518384473};
+const double kAH[6] = {1, -4.9390018191683636, 9.757863526739543, -9.6395448494134577, 4.7615067973562093,
+                       -0.94082365320546057};
+const double kZI[5] = {-0.96996047969958465, 3.8798419288925783, -5.8197629081730433, 3.879841948472456,
+                       -0.96996048949233871};
+
+struct VcPlan {
+    int64_t tpad, Np, F, ld, Tf, T, L, tp, out_len, C;
+};
+
+int vc_plan(const rvc_ctx* c, int64_t N, const rvc_vc_args* a, VcPlan& p) {
+    int emb_dim = 0, upp = 0;
+    MCHECK(c->cv && c->cv->loaded && c->rm && c->rm->loaded && synth_info(c, &emb_dim, &upp),
+           "rvc_vc_convert: load ContentVec, RMVPE and the synthesizer first");
+    MCHECK(a && (a->version == 1 || a->version == 2) && a->x_pad >= 0 && a->x_max > 0 && a->tgt_sr > 0,
+           "rvc_vc_convert: bad args");
+    p.tpad = 16000LL * a->x_pad;
+    MCHECK(N >= 1 && N + 160 <= 16000LL * a->x_max,
+           "rvc_vc_convert: %lld samples: one segment only (N + 160 <= x_max s; longer inputs need the quiet-point "
+           "search, VC.pipeline)", (long long)N);
+    p.Np = N + 2 * p.tpad;
+    p.F = 1 + p.Np / kHop;
+    p.ld = rvc_rmvpe_salience_ld(p.Np);
+    p.Tf = rvc_contentvec_frames(p.Np);
+    const int64_t p_len = p.Np / kHop;
+    MCHECK(p.Tf >= 1 && 2 * p.Tf <= p_len, "rvc_vc_convert: input too short");
+    p.T = 2 * p.Tf;  // min(2 T_f, p_len), convert.py:364-370
+    p.C = a->version == 1 ? c->cv->final_proj.Co : c->cv->E;
+    MCHECK(p.C == emb_dim, "rvc_vc_convert: features of %lld channels, the synthesizer takes %d", (long long)p.C,
+           emb_dim);
+    p.L = p.T * upp;
+    p.tp = (int64_t)a->tgt_sr * a->x_pad;
+    p.out_len = p.L - 2 * p.tp;
+    MCHECK(p.out_len > 0, "rvc_vc_convert: input too short");
+    return RVC_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t rvc_vc_out_len(const rvc_ctx* c, int64_t N, const rvc_vc_args* a) {
+    VcPlan p;
+    if (!c || vc_plan(c, N, a, p) != RVC_OK) return -1;
+    return p.out_len;
+}
+
+extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const rvc_vc_args* a, float* out,
+                              rvc_stream_t stream) {
+    MCHECK(c && audio && out, "rvc_vc_convert: null argument");
+    VcPlan p;
+    MTRY(vc_plan(c, N, a, p));
+    hipStream_t s = (hipStream_t)stream;
+    MHIP(hipSetDevice(c->device));
+    if (!c->vc) c->vc = new VcState();
+    VcState& V = *c->vc;
+    const int64_t fw = (rvc_filtfilt_work_bytes(N) + 7) / 8;
+    MCHECK(fw > 0, "rvc_vc_convert: filtfilt work size");
+    Plan pl;  // f32 slots; the int64 / f64 buffers take two each
+    const int64_t o_work = pl.take(2 * fw), o_xp = pl.take(p.Np), o_sal = pl.take(kClass * p.ld),
+                  o_coarse = pl.take(2 * p.F), o_pitchf = pl.take(p.F), o_feats = pl.take(p.C * p.Tf),
+                  o_phone = pl.take(p.C * p.T), o_wav = pl.take(p.L), o_ws = pl.take(16);
+    MTRY(ensure_arena(V, pl.off, s));
+    float* A = V.arena;
+    float* xp = A + o_xp;
+    // filtfilt + reflect padding (convert.py:403, 416), f64 on the device
+    MTRY(rvc_filtfilt_pad(audio, N, kBH, kAH, kZI, p.tpad, (double*)(A + o_work), xp, nullptr, s));
+    // f0: RMVPE over the padded signal, thred 0.03, pitch shift (VC.get_f0, convert.py:248-255, 304-323)
+    float* sal = A + o_sal;
+    int64_t* coarse = (int64_t*)(A + o_coarse);
+    float* pitchf = A + o_pitchf;
+    MTRY(rvc_rmvpe_forward(c, xp, 1, p.Np, sal, (rvc_stream_t)s));
+    MTRY(rvc_rmvpe_decode(sal, p.ld, p.F, 0.03, pow(2.0, a->pitch_shift / 12.0), nullptr, nullptr, coarse, pitchf,
+                          (rvc_stream_t)s));
+    // features (convert.py:337-340), phone upsample + protect (:361-378)
+    float* feats = A + o_feats;
+    MTRY(contentvec_cf(c, xp, p.Np, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
+    float* phone = A + o_phone;
+    MTRY(rvc_phone_upsample(feats, feats, a->protect < 0.5f ? pitchf : nullptr, phone, p.C, p.Tf, p.T, a->protect,
+                            (rvc_stream_t)s));
+    // Synthesizer.infer (convert.py:381) with device noise at seed, then the trim and peak normalisation
+    float* wav = A + o_wav;
+    MTRY(synth_run_cf(c, phone, coarse, pitchf, p.T, a->sid, a->seed, wav, s));
+    MHIP(hipMemcpyAsync(out, wav + p.tp, p.out_len * 4, hipMemcpyDeviceToDevice, s));
+    return rvc_peak_normalize(out, p.out_len, A + o_ws, nullptr, (rvc_stream_t)s);
 }

@@ -69,14 +69,7 @@ bool resblock_fusable(const rvc_ctx* c, const ConvW& c1, const ConvW& c2, int d)
            (c1.Co == 32 || c1.Co == 64) && c1.K == c2.K && c1.K % 2 == 1 && c1.K <= 15 && (c1.K - 1) * d <= 64;
 }
 
-struct Plan {
-    int64_t off = 0;
-    int64_t take(int64_t n) {  // 256-B aligned float offsets
-        const int64_t o = off;
-        off += (n + 63) & ~int64_t(63);
-        return o;
-    }
-};
+
 
 struct Bufs {
     int64_t phone_cf, lin, x, tmp, o, ml, qkv, rk, ffh, stats, znoise, zp, fb0, fb1, h, acts, outacc, xin, gc, har, work,
@@ -128,7 +121,8 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
 
 // ------------------------------------------------------------------ one sequence (synth.py infer_cf)
 int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float* nsff0, int64_t T, int64_t sid,
-              const float* z_noise, const float* sine_noise, uint64_t seed, float* wav, const Bufs& bf, hipStream_t s) {
+              const float* z_noise, const float* sine_noise, uint64_t seed, float* wav, const Bufs& bf, hipStream_t s,
+              bool phone_is_cf = false) {
     Synth& S = *c->syn;
     const rvc_synth_cfg& g = S.cfg;
     float* A = S.arena;
@@ -143,8 +137,11 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         MTRY(conv(c, S, S.cond, S.emb_g + sid * g.gin_channels, 1, gc, o, s));
     }
     // ---- TextEncoder (synthesizers.py:366-371)
-    float* phone_cf = A + bf.phone_cf;
-    MTRY(rvc_transpose(phone, phone_cf, 1, T, E, s));
+    const float* phone_cf = phone;  // [E][T]
+    if (!phone_is_cf) {             // [T][E] as Synthesizer.infer takes it
+        MTRY(rvc_transpose(phone, A + bf.phone_cf, 1, T, E, s));
+        phone_cf = A + bf.phone_cf;
+    }
     float *lin = A + bf.lin, *x = A + bf.x, *tmp = A + bf.tmp, *ob = A + bf.o, *ml = A + bf.ml, *qkv = A + bf.qkv,
           *rk = A + bf.rk, *ffh = A + bf.ffh, *stats = A + bf.stats;
     {
@@ -370,6 +367,7 @@ extern "C" void rvc_ctx_destroy(rvc_ctx* c) {
     if (hipSetDevice(c->device) == hipSuccess) {
         (void)hipDeviceSynchronize();
         synth_delete(c->syn);
+        vc_delete(c->vc);
         contentvec_delete(c->cv);
         rmvpe_delete(c->rm);
         crepe_delete(c->cr);
@@ -595,4 +593,19 @@ extern "C" int rvc_synth_infer(rvc_ctx* c, const float* phone, const int64_t* pi
         MTRY(synth_one(c, phone + b * T * E, pitch + b * T, pitchf + b * T, T, sid[b], z_noise ? z_noise + b * I * T : nullptr,
                        sine_noise ? sine_noise + b * L : nullptr, seed + (uint64_t)b, wav + b * L, bf, s));
     return RVC_OK;
+}
+
+int synth_run_cf(rvc_ctx* c, const float* phone_cf, const int64_t* pitch, const float* pitchf, int64_t T, int64_t sid,
+                 uint64_t seed, float* wav, hipStream_t s) {
+    MCHECK(c && c->syn && c->syn->loaded, "rvc_vc_convert: no synthesizer loaded");
+    const Bufs bf = plan_bufs(*c->syn, T);
+    MTRY(ensure_arena(*c->syn, bf.total, s));
+    return synth_one(c, phone_cf, pitch, pitchf, T, sid, nullptr, nullptr, seed, wav, bf, s, true);
+}
+
+bool synth_info(const rvc_ctx* c, int* emb_dim, int* upp) {
+    if (!c || !c->syn || !c->syn->loaded) return false;
+    *emb_dim = c->syn->emb_dim;
+    *upp = c->syn->upp;
+    return true;
 }

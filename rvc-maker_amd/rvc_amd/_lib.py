@@ -81,6 +81,12 @@ class ContentVecCfg(ctypes.Structure):
                 ("_pad0", c_int)]
 
 
+class VcArgs(ctypes.Structure):
+    """rvc_vc_args: one VC.pipeline segment (convert.py:388-458)."""
+    _fields_ = [("sid", c_int64), ("pitch_shift", c_double), ("protect", c_float), ("version", c_int),
+                ("x_pad", c_int), ("x_max", c_int), ("tgt_sr", c_int), ("_pad0", c_int), ("seed", c_uint64)]
+
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "rvc_last_error": [],
@@ -163,6 +169,8 @@ SIGNATURES = {
     "rvc_rmvpe_forward": [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p],
     "rvc_rmvpe_check": [c_void_p],
     "rvc_load_crepe": [c_void_p, POINTER(Param), c_int],
+    "rvc_vc_out_len": [c_void_p, c_int64, POINTER(VcArgs)],
+    "rvc_vc_convert": [c_void_p, c_void_p, c_int64, POINTER(VcArgs), c_void_p, c_void_p],
     "rvc_crepe_f0": [c_void_p, c_void_p, c_int64, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p],
     "rvc_synth_infer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
@@ -174,7 +182,8 @@ _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint,
              "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64,
-             "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64}
+             "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64,
+             "rvc_vc_out_len": c_int64}
 
 _lib = None
 

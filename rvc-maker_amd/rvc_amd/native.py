@@ -267,3 +267,54 @@ class NativeCrepe(_Ctx):
         check(self.lib.rvc_crepe_f0(self.ctx, p(audio), N, p(d), int(seed), float(pitch_shift), None, p(probs),
                                     p(coarse), p(pitchf), self.stream()), "rvc_crepe_f0")
         return coarse, pitchf, probs
+
+
+class NativeVC(_Ctx):
+    """One ``VC.pipeline`` segment through the model-level ABI: ContentVec, RMVPE and the synthesizer loaded on
+    one context, ``convert`` = rvc_vc_convert (filtfilt, f0, features, upsample + protect, synthesizer, trim,
+    peak normalisation).  ``synth_weights`` / ``hub_weights`` / ``rmvpe_consts`` as the single-model classes."""
+
+    def __init__(self, hub_ckpt: dict, rmvpe_sd: dict, synth_cpt: dict, device: str = "cuda", precision="fp32",
+                 synth_weights=None, hub_weights=None, window=None, mel_basis=None):
+        super().__init__(device, precision)
+        cfg = hub_ckpt["cfg"]["model"]
+        c = _lib.ContentVecCfg()
+        c.encoder_embed_dim = cfg.get("encoder_embed_dim", 768)
+        c.encoder_attention_heads = cfg.get("encoder_attention_heads", 12)
+        c.conv_pos_groups = cfg.get("conv_pos_groups", 16)
+        sd = hub_ckpt["model"] if hub_weights is None else hub_weights
+        W = {k: v for k, v in sd.items() if torch.is_tensor(v) and v.is_floating_point()}
+        params, keep = _params(W)
+        check(self.lib.rvc_load_contentvec(self.ctx, params, len(W), ctypes.byref(c)), "rvc_load_contentvec")
+        W = dict(rmvpe_sd)
+        if window is not None:
+            W["window"] = window
+        if mel_basis is not None:
+            W["mel_basis"] = mel_basis
+        W = {k: v for k, v in W.items() if torch.as_tensor(v).is_floating_point()}
+        params, keep = _params(W)
+        check(self.lib.rvc_load_rmvpe(self.ctx, params, len(W)), "rvc_load_rmvpe")
+        self.cfg = synth_cfg(synth_cpt)
+        W = synth_cpt["weight"] if synth_weights is None else synth_weights
+        params, keep = _params(W)
+        check(self.lib.rvc_load_synth(self.ctx, params, len(W), ctypes.byref(self.cfg)), "rvc_load_synth")
+        del keep
+        self.tgt_sr = int(synth_cpt["config"][-1])
+
+    def args(self, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0, x_pad=1, x_max=41):
+        a = _lib.VcArgs()
+        a.sid, a.pitch_shift, a.protect, a.version = int(sid), float(pitch), float(protect), 1 if version == "v1" else 2
+        a.x_pad, a.x_max, a.tgt_sr, a.seed = x_pad, x_max, self.tgt_sr, int(seed)
+        return a
+
+    def convert(self, audio, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0):
+        """audio f32 [N] 16 kHz (device) -> waveform f32 at tgt_sr (device)."""
+        audio = audio.to(self.device, torch.float32).reshape(-1).contiguous()
+        a = self.args(sid, pitch, protect, version, seed)
+        n = int(self.lib.rvc_vc_out_len(self.ctx, audio.numel(), ctypes.byref(a)))
+        if n <= 0:
+            raise RuntimeError(f"rvc_vc_out_len: {self.lib.rvc_last_error().decode()}")
+        out = torch.empty(n, device=self.device)
+        check(self.lib.rvc_vc_convert(self.ctx, ctypes.c_void_p(audio.data_ptr()), audio.numel(), ctypes.byref(a),
+                                      ctypes.c_void_p(out.data_ptr()), self.stream()), "rvc_vc_convert")
+        return out

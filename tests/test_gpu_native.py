@@ -210,3 +210,32 @@ def test_native_crepe_bit_identical_to_python(capacity, seconds):
     # device dither (NULL): finite, in the quantiser's range
     c3, f3, _ = nat.f0_device(wav, 0.0, seed=5)
     assert int(c3.min()) >= 1 and int(c3.max()) <= 255 and torch.isfinite(f3).all()
+
+
+@pytest.mark.parametrize("sr,version,protect,pitch", [(48000, "v2", 0.33, 0.0), (32000, "v1", 0.5, 3.0)])
+def test_native_vc_convert_equals_pipeline_device(sr, version, protect, pitch):
+    """rvc_vc_convert (one segment through the C ABI) vs VC.pipeline_device on the same models, constants and
+    seed: bit-identical waveform."""
+    from rvc_amd import melbasis
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.native import NativeVC
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD, fold_weight_norm
+    hub_ck = synthetic.make_contentvec_ckpt(51)
+    rm_sd = synthetic.rmvpe_state_dict(52)
+    cpt = synthetic.make_synth_ckpt(sr, version, seed=53)
+    hub, net_g = ContentVecAMD(hub_ck, DEV), SynthesizerAMD(cpt, DEV)
+    vc = VC(sr, Config(DEV), rmvpe=RMVPEAMD(rm_sd, DEV))
+    hw = dict(hub_ck["model"])
+    p = "encoder.pos_conv.0.weight"
+    hw[p] = torch._weight_norm(hw.pop(p + "_v").float(), hw.pop(p + "_g").float(), 2)
+    nat = NativeVC(hub_ck, rm_sd, cpt, DEV, synth_weights=fold_weight_norm(cpt["weight"]), hub_weights=hw,
+                   window=torch.hann_window(1024), mel_basis=melbasis.mel_filterbank(16000, 1024, 128, 30, 8000))
+    audio = torch.from_numpy(synthetic.synthetic_audio(4.3, seed=54)).float().to(DEV)
+    ref = vc.pipeline_device(hub, net_g, 0, audio, pitch, version, protect)
+    got = nat.convert(audio, 0, pitch, protect, version, seed=0)
+    torch.cuda.synchronize()
+    vc.check_errors()
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref), rms(got, ref)
