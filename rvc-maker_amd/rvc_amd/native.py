@@ -54,6 +54,14 @@ def export_synth_safetensors(cpt: dict, path: str) -> None:
               metadata={"rvc_synth_cfg": " ".join(str(int(i)) for i in ints)})
 
 
+def export_safetensors(tensors: dict, path: str, **meta_ints) -> None:
+    """Floating tensors of a checkpoint dict as safetensors, with each keyword as a __metadata__ string of
+    ints: e.g. the ContentVec ``model`` dict with rvc_contentvec_cfg=[768, 12, 16, 0] (examples/c_host)."""
+    from safetensors.torch import save_file
+    W = {k: v.detach().cpu().contiguous() for k, v in tensors.items() if torch.is_tensor(v) and v.is_floating_point()}
+    save_file(W, path, metadata={k: " ".join(str(int(i)) for i in v) for k, v in meta_ints.items()})
+
+
 class _Ctx:
     """One rvc_ctx on a device (destroyed with the object)."""
 

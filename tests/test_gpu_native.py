@@ -239,3 +239,28 @@ def test_native_vc_convert_equals_pipeline_device(sr, version, protect, pitch):
     vc.check_errors()
     assert got.shape == ref.shape
     assert torch.equal(got, ref), rms(got, ref)
+
+
+def test_c_host_runs_a_whole_segment(tmp_path):
+    """examples/c_host/vc_demo: ContentVec, RMVPE and the voice model from safetensors exports, one
+    rvc_vc_convert call, from plain C; bit-identical to NativeVC on the same clip and seed."""
+    import os
+    import subprocess
+    from rvc_amd.native import NativeVC, export_safetensors, export_synth_safetensors
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "c_host", "vc_demo")
+    assert os.path.exists(exe), "build it: make -C examples/c_host"
+    hub_ck = synthetic.make_contentvec_ckpt(61)
+    rm_sd = synthetic.rmvpe_state_dict(62)
+    cpt = synthetic.make_synth_ckpt(40000, "v2", seed=63)
+    export_safetensors(hub_ck["model"], str(tmp_path / "hub.safetensors"), rvc_contentvec_cfg=[768, 12, 16, 0])
+    export_safetensors(rm_sd, str(tmp_path / "rmvpe.safetensors"))
+    export_synth_safetensors(cpt, str(tmp_path / "model.safetensors"))
+    audio = synthetic.synthetic_audio(3.7, seed=64).astype(np.float32)
+    audio.tofile(tmp_path / "audio.f32")
+    r = subprocess.run([exe, str(tmp_path / "hub.safetensors"), str(tmp_path / "rmvpe.safetensors"),
+                        str(tmp_path / "model.safetensors"), str(tmp_path / "audio.f32"), str(tmp_path / "out.f32"),
+                        "2", "0.33", "7"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(tmp_path / "out.f32", dtype=np.float32)
+    ref = NativeVC(hub_ck, rm_sd, cpt, DEV).convert(torch.from_numpy(audio).to(DEV), 0, 2.0, 0.33, "v2", seed=7)
+    assert got.shape == tuple(ref.shape) and np.array_equal(got, ref.cpu().numpy()), r.stdout
