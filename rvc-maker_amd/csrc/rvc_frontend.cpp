@@ -910,10 +910,18 @@ int contentvec_cf(rvc_ctx* c, const float* wav, int64_t N, int out_layer, int fi
 }
 
 // ------------------------------------------------------------------ one VC.pipeline segment (rvc_amd/pipeline.py)
-struct VcState : ModelBase {};
+// rvc_vc_convert's scratch plus its f0 side stream: RMVPE runs there, concurrently with ContentVec on the
+// caller's stream (as VC._pipeline_on_device does), joined by an event before the phone upsample
+struct VcState : ModelBase {
+    hipStream_t side = nullptr;
+    hipEvent_t ev_in = nullptr, ev_f0 = nullptr;
+};
 
 void vc_delete(VcState* v) {
     if (!v) return;
+    if (v->side) (void)hipStreamDestroy(v->side);
+    if (v->ev_in) (void)hipEventDestroy(v->ev_in);
+    if (v->ev_f0) (void)hipEventDestroy(v->ev_f0);
     v->release();
     delete v;
 }
@@ -976,6 +984,13 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     MHIP(hipSetDevice(c->device));
     if (!c->vc) c->vc = new VcState();
     VcState& V = *c->vc;
+    if (!V.side) {  // high priority: the f0 branch is the longer one (RMVPE with the BiGRU recurrence)
+        int least = 0, greatest = 0;
+        MHIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        MHIP(hipStreamCreateWithPriority(&V.side, hipStreamNonBlocking, greatest));
+        MHIP(hipEventCreateWithFlags(&V.ev_in, hipEventDisableTiming));
+        MHIP(hipEventCreateWithFlags(&V.ev_f0, hipEventDisableTiming));
+    }
     const int64_t fw = (rvc_filtfilt_work_bytes(N) + 7) / 8;
     MCHECK(fw > 0, "rvc_vc_convert: filtfilt work size");
     Plan pl;  // f32 slots; the int64 / f64 buffers take two each
@@ -991,12 +1006,16 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     float* sal = A + o_sal;
     int64_t* coarse = (int64_t*)(A + o_coarse);
     float* pitchf = A + o_pitchf;
-    MTRY(rvc_rmvpe_forward(c, xp, 1, p.Np, sal, (rvc_stream_t)s));
+    MHIP(hipEventRecord(V.ev_in, s));
+    MHIP(hipStreamWaitEvent(V.side, V.ev_in, 0));
+    MTRY(rvc_rmvpe_forward(c, xp, 1, p.Np, sal, (rvc_stream_t)V.side));
     MTRY(rvc_rmvpe_decode(sal, p.ld, p.F, 0.03, pow(2.0, a->pitch_shift / 12.0), nullptr, nullptr, coarse, pitchf,
-                          (rvc_stream_t)s));
+                          (rvc_stream_t)V.side));
+    MHIP(hipEventRecord(V.ev_f0, V.side));
     // features (convert.py:337-340), phone upsample + protect (:361-378)
     float* feats = A + o_feats;
     MTRY(contentvec_cf(c, xp, p.Np, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
+    MHIP(hipStreamWaitEvent(s, V.ev_f0, 0));  // join: the upsample reads pitchf
     float* phone = A + o_phone;
     MTRY(rvc_phone_upsample(feats, feats, a->protect < 0.5f ? pitchf : nullptr, phone, p.C, p.Tf, p.T, a->protect,
                             (rvc_stream_t)s));
