@@ -440,8 +440,7 @@ int rvc_rmvpe_check(rvc_ctx* ctx);
  *   probs (optional, device f32 [360][T]) receives the sigmoid outputs. */
 int rvc_load_crepe(rvc_ctx* ctx, const rvc_param* params, int n);
 
-/* One VC.pipeline segment (convert.py:388-458 for N + 160 <= x_max s, f0_method "rmvpe", no index, volume
- * envelope 1): filtfilt + reflect padding by x_pad s, RMVPE f0 (thred 0.03, pitch shift), ContentVec (v2: layer 12;
+/* One VC.pipeline segment (convert.py:388-458 for N + 160 <= x_max s, f0_method "rmvpe", volume envelope 1): filtfilt + reflect padding by x_pad s, RMVPE f0 (thred 0.03, pitch shift), ContentVec (v2: layer 12;
  * v1: layer 9 + final_proj), phone upsample + protect, Synthesizer.infer with device noise at `seed`, the
  * x_pad trim at tgt_sr and the peak normalisation.  Needs ContentVec, RMVPE and the synthesizer loaded on the
  * context; audio f32 [N] 16 kHz (device) -> out f32 [rvc_vc_out_len(ctx, N, args)] (device).  Equal to
@@ -452,9 +451,26 @@ typedef struct rvc_vc_args {
     float protect;
     int version;        /* 1 or 2 */
     int x_pad, x_max;   /* Config: 1 and 41 at full precision */
-    int tgt_sr, _pad0;
+    int tgt_sr;
+    float index_rate;   /* != 0: FAISS IVF-Flat retrieval + blend (convert.py:349-359), index from rvc_load_index */
     uint64_t seed;
 } rvc_vc_args;
+
+/* The retrieval index rvc_vc_convert blends with (a faiss IndexIVFFlat(L2) as create_index.py writes it; read
+ * without faiss by rvc_amd.faiss_index): HOST arrays, copied to the device.  centroids [nlist][d]; inverted lists
+ * in CSR form: list_off [nlist + 1], codes [ntotal][d] (list-major), ids [ntotal]; big = reconstruct_n(0, ntotal)
+ * [ntotal][d]; nprobe as the index stores it. */
+typedef struct rvc_ivf_index {
+    int64_t d, nlist, ntotal;
+    int nprobe, _pad0;
+    const float* centroids;
+    const int64_t* list_off;
+    const float* codes;
+    const int64_t* ids;
+    const float* big;
+} rvc_ivf_index;
+
+int rvc_load_index(rvc_ctx* ctx, const rvc_ivf_index* index);
 
 int64_t rvc_vc_out_len(const rvc_ctx* ctx, int64_t N, const rvc_vc_args* args);
 int rvc_vc_convert(rvc_ctx* ctx, const float* audio, int64_t N, const rvc_vc_args* args, float* out,

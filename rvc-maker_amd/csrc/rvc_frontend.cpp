@@ -915,10 +915,19 @@ int contentvec_cf(rvc_ctx* c, const float* wav, int64_t N, int out_layer, int fi
 struct VcState : ModelBase {
     hipStream_t side = nullptr;
     hipEvent_t ev_in = nullptr, ev_f0 = nullptr;
+    // retrieval index (rvc_load_index): device copies, owned in allocs
+    bool has_index = false;
+    int64_t d = 0, nlist = 0, ntotal = 0;
+    int nprobe = 1;
+    float *centT = nullptr, *codes = nullptr, *big = nullptr;
+    int64_t *list_off = nullptr, *ids = nullptr;
+    void* ivf_ws = nullptr;
+    int64_t ivf_ws_bytes = 0;
 };
 
 void vc_delete(VcState* v) {
     if (!v) return;
+    if (v->ivf_ws) (void)hipFree(v->ivf_ws);
     if (v->side) (void)hipStreamDestroy(v->side);
     if (v->ev_in) (void)hipEventDestroy(v->ev_in);
     if (v->ev_f0) (void)hipEventDestroy(v->ev_f0);
@@ -960,6 +969,8 @@ int vc_plan(const rvc_ctx* c, int64_t N, const rvc_vc_args* a, VcPlan& p) {
     p.C = a->version == 1 ? c->cv->final_proj.Co : c->cv->E;
     MCHECK(p.C == emb_dim, "rvc_vc_convert: features of %lld channels, the synthesizer takes %d", (long long)p.C,
            emb_dim);
+    MCHECK(a->index_rate == 0.f || (c->vc && c->vc->has_index && c->vc->d == p.C),
+           "rvc_vc_convert: index_rate %g needs an index of the features' width (rvc_load_index)", (double)a->index_rate);
     p.L = p.T * upp;
     p.tp = (int64_t)a->tgt_sr * a->x_pad;
     p.out_len = p.L - 2 * p.tp;
@@ -996,7 +1007,9 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     Plan pl;  // f32 slots; the int64 / f64 buffers take two each
     const int64_t o_work = pl.take(2 * fw), o_xp = pl.take(p.Np), o_sal = pl.take(kClass * p.ld),
                   o_coarse = pl.take(2 * p.F), o_pitchf = pl.take(p.F), o_feats = pl.take(p.C * p.Tf),
-                  o_phone = pl.take(p.C * p.T), o_wav = pl.take(p.L), o_ws = pl.take(16);
+                  o_phone = pl.take(p.C * p.T), o_wav = pl.take(p.L), o_ws = pl.take(16),
+                  o_blend = pl.take(p.C * p.Tf), o_D = pl.take(8 * p.Tf), o_I = pl.take(2 * 8 * p.Tf),
+                  o_probes = pl.take(2 * (int64_t)V.nprobe * p.Tf);
     MTRY(ensure_arena(V, pl.off, s));
     float* A = V.arena;
     float* xp = A + o_xp;
@@ -1015,13 +1028,68 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     // features (convert.py:337-340), phone upsample + protect (:361-378)
     float* feats = A + o_feats;
     MTRY(contentvec_cf(c, xp, p.Np, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
+    const float* fb = feats;  // convert.py:347: the protect blend keeps the pre-retrieval features
+    if (a->index_rate != 0.f) {  // search(k = 8) + blend (convert.py:349-359) on the channels-first features
+        const int64_t need = rvc_ivf_coarse_ws_bytes(p.Tf, V.nlist);
+        if (need > V.ivf_ws_bytes) {
+            if (V.ivf_ws) {
+                MHIP(hipStreamSynchronize(s));
+                MHIP(hipFree(V.ivf_ws));
+                V.ivf_ws = nullptr;
+            }
+            MHIP(hipMalloc(&V.ivf_ws, need));
+            V.ivf_ws_bytes = need;
+        }
+        float* D = A + o_D;
+        int64_t* I = (int64_t*)(A + o_I);
+        MTRY(rvc_ivf_search(feats, p.Tf, p.C, p.Tf, 1, V.centT, V.nlist, V.nprobe, V.list_off, V.codes, V.ids, 8,
+                            V.ivf_ws, need, (int64_t*)(A + o_probes), D, I, (rvc_stream_t)s));
+        MTRY(rvc_ivf_blend(feats, p.Tf, p.C, p.Tf, 1, D, I, 8, V.big, V.ntotal, (double)a->index_rate, A + o_blend, p.Tf,
+                           1, (rvc_stream_t)s));
+        fb = A + o_blend;
+    }
     MHIP(hipStreamWaitEvent(s, V.ev_f0, 0));  // join: the upsample reads pitchf
     float* phone = A + o_phone;
-    MTRY(rvc_phone_upsample(feats, feats, a->protect < 0.5f ? pitchf : nullptr, phone, p.C, p.Tf, p.T, a->protect,
+    MTRY(rvc_phone_upsample(fb, feats, a->protect < 0.5f ? pitchf : nullptr, phone, p.C, p.Tf, p.T, a->protect,
                             (rvc_stream_t)s));
     // Synthesizer.infer (convert.py:381) with device noise at seed, then the trim and peak normalisation
     float* wav = A + o_wav;
     MTRY(synth_run_cf(c, phone, coarse, pitchf, p.T, a->sid, a->seed, wav, s));
     MHIP(hipMemcpyAsync(out, wav + p.tp, p.out_len * 4, hipMemcpyDeviceToDevice, s));
     return rvc_peak_normalize(out, p.out_len, A + o_ws, nullptr, (rvc_stream_t)s);
+}
+
+extern "C" int rvc_load_index(rvc_ctx* c, const rvc_ivf_index* x) {
+    MCHECK(c && x && x->centroids && x->list_off && x->big && x->d > 0 && x->nlist > 0 && x->ntotal >= 0 &&
+               x->nprobe >= 1,
+           "rvc_load_index: bad index");
+    MCHECK(x->list_off[0] == 0 && x->list_off[x->nlist] == x->ntotal, "rvc_load_index: list_off must span [0, ntotal]");
+    MCHECK(x->ntotal == 0 || (x->codes && x->ids), "rvc_load_index: codes / ids missing");
+    MHIP(hipSetDevice(c->device));
+    if (!c->vc) c->vc = new VcState();
+    VcState& V = *c->vc;
+    if (V.has_index) {  // replace: the old arrays stay owned until the context goes (allocs)
+        V.has_index = false;
+    }
+    V.d = x->d;
+    V.nlist = x->nlist;
+    V.ntotal = x->ntotal;
+    V.nprobe = x->nprobe < x->nlist ? x->nprobe : (int)x->nlist;
+    std::vector<float> ct((size_t)x->d * x->nlist);  // centroids transposed [d][nlist] (retrieval.py)
+    for (int64_t l = 0; l < x->nlist; ++l)
+        for (int64_t k = 0; k < x->d; ++k) ct[(size_t)k * x->nlist + l] = x->centroids[l * x->d + k];
+    MTRY(upload(V, ct, &V.centT));
+    const int64_t nt = x->ntotal > 0 ? x->ntotal : 1;
+    auto up = [&](const void* src, size_t bytes, void** dst) -> int {
+        MTRY(dev_alloc(V, bytes, dst));
+        if (src) MHIP(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+        else MHIP(hipMemset(*dst, 0, bytes));
+        return RVC_OK;
+    };
+    MTRY(up(x->list_off, (x->nlist + 1) * 8, (void**)&V.list_off));
+    MTRY(up(x->ntotal ? x->codes : nullptr, nt * x->d * 4, (void**)&V.codes));
+    MTRY(up(x->ntotal ? x->ids : nullptr, nt * 8, (void**)&V.ids));
+    MTRY(up(x->ntotal ? x->big : nullptr, nt * x->d * 4, (void**)&V.big));
+    V.has_index = true;
+    return RVC_OK;
 }

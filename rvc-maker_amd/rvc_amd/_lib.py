@@ -84,7 +84,14 @@ class ContentVecCfg(ctypes.Structure):
 class VcArgs(ctypes.Structure):
     """rvc_vc_args: one VC.pipeline segment (convert.py:388-458)."""
     _fields_ = [("sid", c_int64), ("pitch_shift", c_double), ("protect", c_float), ("version", c_int),
-                ("x_pad", c_int), ("x_max", c_int), ("tgt_sr", c_int), ("_pad0", c_int), ("seed", c_uint64)]
+                ("x_pad", c_int), ("x_max", c_int), ("tgt_sr", c_int), ("index_rate", c_float), ("seed", c_uint64)]
+
+
+class IvfIndex(ctypes.Structure):
+    """rvc_ivf_index: a faiss IndexIVFFlat's arrays on the host (rvc_load_index)."""
+    _fields_ = [("d", c_int64), ("nlist", c_int64), ("ntotal", c_int64), ("nprobe", c_int), ("_pad0", c_int),
+                ("centroids", c_void_p), ("list_off", c_void_p), ("codes", c_void_p), ("ids", c_void_p),
+                ("big", c_void_p)]
 
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
@@ -170,6 +177,7 @@ SIGNATURES = {
     "rvc_rmvpe_check": [c_void_p],
     "rvc_load_crepe": [c_void_p, POINTER(Param), c_int],
     "rvc_vc_out_len": [c_void_p, c_int64, POINTER(VcArgs)],
+    "rvc_load_index": [c_void_p, POINTER(IvfIndex)],
     "rvc_vc_convert": [c_void_p, c_void_p, c_int64, POINTER(VcArgs), c_void_p, c_void_p],
     "rvc_crepe_f0": [c_void_p, c_void_p, c_int64, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p],

@@ -309,16 +309,31 @@ class NativeVC(_Ctx):
         del keep
         self.tgt_sr = int(synth_cpt["config"][-1])
 
-    def args(self, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0, x_pad=1, x_max=41):
+    def load_index(self, index) -> None:
+        """A faiss_index.IVFFlatIndex (as read_index gives it) -> rvc_load_index."""
+        sizes = np.array([len(i) for i in index.ids], dtype=np.int64)
+        off = np.zeros(index.nlist + 1, dtype=np.int64)
+        np.cumsum(sizes, out=off[1:])
+        keep = [np.ascontiguousarray(index.centroids, dtype=np.float32), off,
+                np.ascontiguousarray(np.concatenate(index.codes) if off[-1] else np.zeros((1, index.d)), np.float32),
+                np.ascontiguousarray(np.concatenate(index.ids) if off[-1] else np.zeros(1), np.int64),
+                np.ascontiguousarray(index.reconstruct_n(0, index.ntotal), np.float32)]
+        x = _lib.IvfIndex()
+        x.d, x.nlist, x.ntotal, x.nprobe = index.d, index.nlist, int(off[-1]), index.nprobe
+        x.centroids, x.list_off, x.codes, x.ids, x.big = (ctypes.c_void_p(a.ctypes.data) for a in keep)
+        check(self.lib.rvc_load_index(self.ctx, ctypes.byref(x)), "rvc_load_index")
+
+    def args(self, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0, x_pad=1, x_max=41, index_rate=0.0):
         a = _lib.VcArgs()
+        a.index_rate = float(index_rate)
         a.sid, a.pitch_shift, a.protect, a.version = int(sid), float(pitch), float(protect), 1 if version == "v1" else 2
         a.x_pad, a.x_max, a.tgt_sr, a.seed = x_pad, x_max, self.tgt_sr, int(seed)
         return a
 
-    def convert(self, audio, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0):
+    def convert(self, audio, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0, index_rate=0.0):
         """audio f32 [N] 16 kHz (device) -> waveform f32 at tgt_sr (device)."""
         audio = audio.to(self.device, torch.float32).reshape(-1).contiguous()
-        a = self.args(sid, pitch, protect, version, seed)
+        a = self.args(sid, pitch, protect, version, seed, index_rate=index_rate)
         n = int(self.lib.rvc_vc_out_len(self.ctx, audio.numel(), ctypes.byref(a)))
         if n <= 0:
             raise RuntimeError(f"rvc_vc_out_len: {self.lib.rvc_last_error().decode()}")

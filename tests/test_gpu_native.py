@@ -264,3 +264,36 @@ def test_c_host_runs_a_whole_segment(tmp_path):
     got = np.fromfile(tmp_path / "out.f32", dtype=np.float32)
     ref = NativeVC(hub_ck, rm_sd, cpt, DEV).convert(torch.from_numpy(audio).to(DEV), 0, 2.0, 0.33, "v2", seed=7)
     assert got.shape == tuple(ref.shape) and np.array_equal(got, ref.cpu().numpy()), r.stdout
+
+
+def test_native_vc_convert_with_index_equals_pipeline_device():
+    """BASELINE configs[2]'s retrieval (IVF-Flat, index_rate 0.75) inside rvc_vc_convert: bit-identical to
+    VC.pipeline_device with the same index."""
+    from rvc_amd import melbasis
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.faiss_index import IVFFlatIndex
+    from rvc_amd.native import NativeVC
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.retrieval import IVFFlatDevice
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD, fold_weight_norm
+    hub_ck, rm_sd, cpt = synthetic.make_contentvec_ckpt(71), synthetic.rmvpe_state_dict(72), \
+        synthetic.make_synth_ckpt(48000, "v2", seed=73)
+    hub, net_g = ContentVecAMD(hub_ck, DEV), SynthesizerAMD(cpt, DEV)
+    vc = VC(48000, Config(DEV), rmvpe=RMVPEAMD(rm_sd, DEV))
+    feats = hub.features_cf(torch.from_numpy(synthetic.synthetic_audio(8.0, seed=74)).to(DEV)).t().cpu().numpy()
+    rng = np.random.default_rng(2)
+    idx = IVFFlatIndex.build(feats[rng.choice(len(feats), 24, replace=False)], feats, nprobe=3)
+    hw = dict(hub_ck["model"])
+    p = "encoder.pos_conv.0.weight"
+    hw[p] = torch._weight_norm(hw.pop(p + "_v").float(), hw.pop(p + "_g").float(), 2)
+    nat = NativeVC(hub_ck, rm_sd, cpt, DEV, synth_weights=fold_weight_norm(cpt["weight"]), hub_weights=hw,
+                   window=torch.hann_window(1024), mel_basis=melbasis.mel_filterbank(16000, 1024, 128, 30, 8000))
+    nat.load_index(idx)
+    audio = torch.from_numpy(synthetic.synthetic_audio(5.1, seed=75)).float().to(DEV)
+    ref = vc.pipeline_device(hub, net_g, 0, audio, 0, "v2", 0.33, IVFFlatDevice(idx, DEV), 0.75)
+    got = nat.convert(audio, 0, 0.0, 0.33, "v2", seed=0, index_rate=0.75)
+    plain = nat.convert(audio, 0, 0.0, 0.33, "v2", seed=0)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), rms(got, ref)
+    assert not torch.equal(got, plain)
