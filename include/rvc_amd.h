@@ -451,8 +451,8 @@ typedef struct rvc_vc_args {
     float protect;
     int version;        /* 1 or 2 */
     int x_pad, x_max;   /* Config: 1 and 41 at full precision */
-    int tgt_sr;
-    float index_rate;   /* != 0: FAISS IVF-Flat retrieval + blend (convert.py:349-359), index from rvc_load_index */
+    int tgt_sr, _pad0;
+    double index_rate;  /* != 0: FAISS IVF-Flat retrieval + blend (convert.py:349-359), index from rvc_load_index */
     uint64_t seed;
 } rvc_vc_args;
 

@@ -969,8 +969,8 @@ int vc_plan(const rvc_ctx* c, int64_t N, const rvc_vc_args* a, VcPlan& p) {
     p.C = a->version == 1 ? c->cv->final_proj.Co : c->cv->E;
     MCHECK(p.C == emb_dim, "rvc_vc_convert: features of %lld channels, the synthesizer takes %d", (long long)p.C,
            emb_dim);
-    MCHECK(a->index_rate == 0.f || (c->vc && c->vc->has_index && c->vc->d == p.C),
-           "rvc_vc_convert: index_rate %g needs an index of the features' width (rvc_load_index)", (double)a->index_rate);
+    MCHECK(a->index_rate == 0.0 || (c->vc && c->vc->has_index && c->vc->d == p.C),
+           "rvc_vc_convert: index_rate %g needs an index of the features' width (rvc_load_index)", a->index_rate);
     p.L = p.T * upp;
     p.tp = (int64_t)a->tgt_sr * a->x_pad;
     p.out_len = p.L - 2 * p.tp;
@@ -1029,7 +1029,7 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     float* feats = A + o_feats;
     MTRY(contentvec_cf(c, xp, p.Np, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
     const float* fb = feats;  // convert.py:347: the protect blend keeps the pre-retrieval features
-    if (a->index_rate != 0.f) {  // search(k = 8) + blend (convert.py:349-359) on the channels-first features
+    if (a->index_rate != 0.0) {  // search(k = 8) + blend (convert.py:349-359) on the channels-first features
         const int64_t need = rvc_ivf_coarse_ws_bytes(p.Tf, V.nlist);
         if (need > V.ivf_ws_bytes) {
             if (V.ivf_ws) {
@@ -1044,7 +1044,7 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
         int64_t* I = (int64_t*)(A + o_I);
         MTRY(rvc_ivf_search(feats, p.Tf, p.C, p.Tf, 1, V.centT, V.nlist, V.nprobe, V.list_off, V.codes, V.ids, 8,
                             V.ivf_ws, need, (int64_t*)(A + o_probes), D, I, (rvc_stream_t)s));
-        MTRY(rvc_ivf_blend(feats, p.Tf, p.C, p.Tf, 1, D, I, 8, V.big, V.ntotal, (double)a->index_rate, A + o_blend, p.Tf,
+        MTRY(rvc_ivf_blend(feats, p.Tf, p.C, p.Tf, 1, D, I, 8, V.big, V.ntotal, a->index_rate, A + o_blend, p.Tf,
                            1, (rvc_stream_t)s));
         fb = A + o_blend;
     }

@@ -84,7 +84,7 @@ class ContentVecCfg(ctypes.Structure):
 class VcArgs(ctypes.Structure):
     """rvc_vc_args: one VC.pipeline segment (convert.py:388-458)."""
     _fields_ = [("sid", c_int64), ("pitch_shift", c_double), ("protect", c_float), ("version", c_int),
-                ("x_pad", c_int), ("x_max", c_int), ("tgt_sr", c_int), ("index_rate", c_float), ("seed", c_uint64)]
+                ("x_pad", c_int), ("x_max", c_int), ("tgt_sr", c_int), ("_pad0", c_int), ("index_rate", c_double), ("seed", c_uint64)]
 
 
 class IvfIndex(ctypes.Structure):
