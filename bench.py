@@ -34,7 +34,14 @@ import torch  # noqa: E402
 
 METRIC = "audio-seconds/sec/GPU (xRT) end-to-end VC, 48k v2; 1/2/4/8 GPU scaling"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
-PEAK_X6_TFLOPS = 2500.0 / 6  # bf16 dense MFMA peak (~2.5 PF) over the six split-bf16 passes per f32 product
+PEAK_MFMA16_TFLOPS = 2500.0  # bf16 / fp16 dense MFMA peak (MI355X_MICROARCH.md)
+
+
+def pass_peak(passes):
+    """The f32-equivalent ceiling of one split-operand launch: the 16-bit dense MFMA peak over the MFMA passes
+    each product takes (6 / 8 split-bf16, 3 split-fp16 or bf16x3, 1 bf16)."""
+    n = {16: 3, 7: 6}.get(passes, passes)  # RVC_ARITH_F16X3: 3 fp16 passes; RVC_ARITH_FP32_SA: 6 passes
+    return PEAK_MFMA16_TFLOPS / n
 DTYPES = {"fp32": "f32-equivalent (split-bf16 6-pass MFMA; split-fp16 3-pass MFMA for k >= 7 convs and ResBlock "
                   "pairs; f32 accumulate)",
           "fp32x6": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
@@ -74,7 +81,8 @@ class ConvProbe:
             e0.record(s)
             out = self.orig(*a, **k)
             e1.record(s)
-            self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE, self._bytes(a, k, out)))
+            self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE, self._bytes(a, k, out),
+                             self.ops.LAST_CONV_PASSES))
             return out
         def wrapped_rb(x, y, c1, c2, dil, slope, accumulate=False):
             s = torch.cuda.current_stream()
@@ -85,7 +93,7 @@ class ConvProbe:
             C, L = x.shape
             flops = 2 * 2.0 * C * C * c1.K * L
             nbytes = 4.0 * (C * L * (2 + bool(accumulate)) + 2 * C * C * c1.K)  # x, y (+ y read), both weights
-            self.rec.append((e0, e1, flops, 1, nbytes))
+            self.rec.append((e0, e1, flops, 1, nbytes, self.ops.rb_passes(c1.K)))
             return out
         self.ops.conv1d = wrapped
         self.ops.resblock_pair = wrapped_rb
@@ -112,9 +120,25 @@ class ConvProbe:
         """(launches, kernel ms, algorithmic FLOPs) over the launches of one engine (None = all)."""
         torch.cuda.synchronize()
         rec = [r for r in self.rec if engine is None or r[3] == engine]
-        ms = [e0.elapsed_time(e1) for e0, e1, _, _, _ in rec]
-        fl = [f for _, _, f, _, _ in rec]
+        ms = [r[0].elapsed_time(r[1]) for r in rec]
+        fl = [r[2] for r in rec]
         return len(ms), float(sum(ms)), float(sum(fl))
+
+    def by_passes(self):
+        """Split-operand launches grouped by pass set: {passes: (launches, kernel ms, FLOPs)}, and the
+        FLOP-weighted ceiling of the family: sum FLOPs / sum (FLOPs / the launch's own pass-set peak)."""
+        torch.cuda.synchronize()
+        groups = {}
+        for r in self.rec:
+            if r[3] != 1:
+                continue
+            g = groups.setdefault(r[5], [0, 0.0, 0.0])
+            g[0] += 1
+            g[1] += r[0].elapsed_time(r[1])
+            g[2] += r[2]
+        tot = sum(g[2] for g in groups.values())
+        weighted = tot / sum(g[2] / pass_peak(p) for p, g in groups.items()) if tot else None
+        return groups, weighted
 
     def algorithmic_bytes(self, engine=None):
         rec = [r for r in self.rec if engine is None or r[3] == engine]
@@ -125,12 +149,13 @@ def pmc_traffic(kernel_family="x6"):
     """Per-launch HBM bytes of a conv family from the committed PMC summary of this same bench step
     (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled
     per MI355X_MICROARCH.md), or None when absent."""
-    path = os.path.join(REPO, "profiles", "r2_pmc_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f)[kernel_family]["traffic_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        return None
+    for name in ("r3_pmc_traffic.json", "r2_pmc_traffic.json"):  # the newest committed summary
+        try:
+            with open(os.path.join(REPO, "profiles", name)) as f:
+                return json.load(f)[kernel_family]["traffic_bytes_per_launch"], name
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
@@ -251,8 +276,6 @@ def main():
     from rvc_amd import ops, synthetic
     from rvc_amd.shard import gather_waveforms
     ops.set_precision(args.precision)
-    npass = 3 if ops.PASSES[args.precision] == ops.F16X3 else ops.PASSES[args.precision]
-    peak = 2500.0 / npass  # bf16 / fp16 dense MFMA peak over the passes per product
     vc, hub, net_g = build_models(dev, sr=args.sr)
     index = None
     if args.index_rate > 0:
@@ -356,20 +379,31 @@ def main():
     if rank == 0 and not args.no_roofline:
         with ConvProbe() as probe:  # one eager pass (a graph replay launches no host-side conv calls)
             vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
-        n, ms, flops = probe.summary(engine=1)  # dominant family: the split-bf16 conv engine
+        n, ms, flops = probe.summary(engine=1)  # dominant family: the split-operand conv engine
         n32, ms32, fl32 = probe.summary(engine=0)
+        groups, peak = probe.by_passes()
         achieved = flops / (ms * 1e-3) / 1e12
+        traffic, tsrc = (pmc_traffic("x6") if (args.sr, args.f0, args.precision, args.index_rate, args.seconds)
+                         == (48000, "rmvpe", "fp32", 0.0, 30.0) else (None, None))
+        alg_bytes = probe.algorithmic_bytes(engine=1)
+        names = {1: "bf16 x1", 3: "split-bf16 x3", 6: "split-bf16 x6", 7: "split-bf16 x6 split-acc", 16: "split-fp16 x3"}
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
-                # HBM bytes per x6 launch from PMC (default 48k / rmvpe / fp32 step only), beside the
+                # HBM bytes per launch of the family from PMC (default 48k / rmvpe / fp32 step only), beside the
                 # algorithmic bytes per launch measured here
-                "traffic": (pmc_traffic("x6") if (args.sr, args.f0, args.precision, args.index_rate, args.seconds)
-                            == (48000, "rmvpe", "fp32", 0.0, 30.0) else None),
-                "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/r2_pmc_traffic.json)",
-                "algorithmic_bytes_per_launch": round(probe.algorithmic_bytes(engine=1)),
-                "kernel": f"conv_x6_kernel<*> + resblock_x6_kernel<*> (implicit-GEMM convs / fused ResBlock conv "
-                          f"pairs, {npass} split-bf16 MFMA pass(es) per product); "
-                          f"achieved = algorithmic FLOPs / kernel time; peak = bf16 dense MFMA peak / {npass}",
+                "traffic": traffic,
+                "traffic_unit": f"bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/{tsrc})",
+                "algorithmic_bytes_per_launch": round(alg_bytes),
+                "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
+                "kernel": "conv_x6_kernel<*> + resblock_x6_kernel<*> (implicit-GEMM convs / fused ResBlock conv "
+                          "pairs on the split-operand MFMA engine); achieved = algorithmic FLOPs / kernel time; peak = "
+                          "the FLOP-weighted ceiling of the pass sets that ran: sum FLOPs / sum (FLOPs / (2.5 PF dense "
+                          "16-bit MFMA / passes per product))",
+                "by_pass_set": {names.get(p, str(p)): {"launches": g[0], "kernel_ms": round(g[1], 3),
+                                                       "gflop": round(g[2] / 1e9, 1),
+                                                       "tflops": round(g[2] / max(g[1], 1e-9) / 1e9, 2),
+                                                       "peak": round(pass_peak(p), 1)}
+                                for p, g in sorted(groups.items())},
                 "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "algorithmic_gflop_per_step": round(flops / 1e9, 1), "kernel_ms_per_step": round(ms, 3),
                 "f32_engine": {"launches": n32, "kernel_ms": round(ms32, 3), "gflop": round(fl32 / 1e9, 1),

@@ -76,7 +76,10 @@ typedef struct {
     int ncfg;
 } Model;
 
-static void parse_tensor(const char* obj, const char* data, rvc_param* prm) {
+static size_t dtype_size(int dt) { return dt == RVC_DT_F16 ? 2 : dt == RVC_DT_F32 ? 4 : 8; }
+
+/* data_size: bytes after the header; every tensor's [a, b) must lie inside it and hold numel * dtype bytes */
+static void parse_tensor(const char* obj, const char* data, size_t data_size, rvc_param* prm) {
     const char* d = strstr(obj, "\"dtype\"");
     const char* s = strstr(obj, "\"shape\"");
     const char* o = strstr(obj, "\"data_offsets\"");
@@ -99,8 +102,22 @@ static void parse_tensor(const char* obj, const char* data, rvc_param* prm) {
         prm->ndim = 1;
         prm->shape[0] = 1;
     }
-    p = strchr(o, '[') + 1;
+    long long numel = 1;
+    for (int i = 0; i < prm->ndim; ++i) {
+        if (prm->shape[i] < 0 || (prm->shape[i] > 0 && numel > (1LL << 40) / prm->shape[i])) DIE("bad shape");
+        numel *= prm->shape[i];
+    }
+    p = strchr(o, '[');
+    if (!p) DIE("bad data_offsets");
+    ++p;
     const long long a = strtoll(p, (char**)&p, 10);
+    p = skip_ws(p);
+    if (*p != ',') DIE("bad data_offsets");
+    const long long b = strtoll(p + 1, (char**)&p, 10);
+    if (a < 0 || a > b || (unsigned long long)b > (unsigned long long)data_size)
+        DIE("data_offsets [%lld, %lld) outside the %zu data bytes", a, b, data_size);
+    if ((unsigned long long)(b - a) != (unsigned long long)numel * dtype_size(prm->dtype))
+        DIE("data_offsets span %lld bytes, shape x dtype needs %lld", b - a, numel * (long long)dtype_size(prm->dtype));
     prm->data = data + a;
 }
 
@@ -109,7 +126,9 @@ static Model load_safetensors(const char* path, const char* meta_key, char** kee
     char* buf = slurp(path, &n);
     *keep = buf;
     unsigned long long hlen;
+    if (n < 8) DIE("%s: truncated safetensors file", path);
     memcpy(&hlen, buf, 8);
+    if (hlen > n - 8) DIE("%s: header length %llu exceeds the file", path, hlen);
     char* hdr = buf + 8;
     const char* data = hdr + hlen;
     char save = hdr[hlen];
@@ -150,7 +169,7 @@ static Model load_safetensors(const char* path, const char* meta_key, char** kee
             if (m.n == 4096) DIE("too many tensors");
             m.names[m.n] = strdup(key);
             m.params[m.n].name = m.names[m.n];
-            parse_tensor(obj, data, &m.params[m.n]);
+            parse_tensor(obj, data, n - 8 - hlen, &m.params[m.n]);
             ++m.n;
         }
         free(obj);

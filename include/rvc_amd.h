@@ -62,6 +62,8 @@ int rvc_version(void);
  *   pre(v) = in_act(v * in_scale)
  */
 #define RVC_ARITH_F16X3 16 /* rvc_conv1d_args.wx_passes / rvc_resblock_args.passes: split-fp16, 3 passes */
+#define RVC_ARITH_FP32_SA 7 /* rvc_conv1d_args.wx_passes: 6-pass split-bf16 with the correction passes in their
+                               own f32 accumulators (fewer roundings of the large sum; RMVPE) */
 
 typedef struct rvc_conv1d_args {
     const float* x;    /* [B][Ci][Lin] with batch stride x_bstride           */
@@ -86,8 +88,10 @@ typedef struct rvc_conv1d_args {
     /* Split-bf16 engine: wx = the same weights pre-split into bf16 h/m/l planes by
        rvc_conv1d_pack_x6 (NULL = f32 MFMA engine).  Used for stride-1, ungrouped, 1-D convs;
        other shapes ignore it.  wx_nmf = its padded 16-row fragment count.
-       wx_passes: bf16 MFMA passes per product -- 0 or 6 = f32-accurate (hH+hM+mH+hL+mM+lH),
-       3 = hH+hM+mH (16-bit operand mantissas), 1 = hH (bf16 operands); f32 accumulation always.
+       wx_passes: bf16 MFMA passes per product -- 0 or 6 = f32-accurate (hH+hM+mH+hL+mM+lH, products to
+       2^-24), RVC_ARITH_FP32_SA = the same 6 passes with hH and the 5 corrections accumulated apart (RMVPE,
+       whose f0 is a per-frame decision), 3 = hH+hM+mH (16-bit operand mantissas), 1 = hH (bf16 operands);
+       f32 accumulation always.
        RVC_ARITH_F16X3: wx is an rvc_conv1d_pack_f16 image instead -- split-fp16 operands (per-row
        weight and per-tile activation power-of-2 scales, 11 + 11 significant bits each), hH + hL + lH
        on the fp16 MFMA: ~2^-20 relative per product, f32 accumulation. */
@@ -96,7 +100,10 @@ typedef struct rvc_conv1d_args {
 } rvc_conv1d_args;
 
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned
- * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args). */
+ * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args).  Its first
+ * 64 KB hold the split blocks' arrival counters: the workspace must be ZERO when first used, and every
+ * completed launch leaves them zero again (the partial tiles are reduced inside the launch).  Launches that
+ * may run concurrently need separate workspaces. */
 int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a);
 /* Which engine a call would run on: 0 = f32 MFMA, 1 = split-bf16 (x6); -1 on bad args. */
 int rvc_conv1d_engine(const rvc_conv1d_args* a);
@@ -221,6 +228,11 @@ int rvc_sine_source(const float* f0, const float* noise, float* har, float* work
 int rvc_stft_frames(const float* x, const float* win, float* framesT, int64_t N, int64_t F, int nfft, int hop,
                     rvc_stream_t stream);
 int rvc_spec_mag(const float* spec, float* mag, int64_t K, int64_t F, rvc_stream_t stream);
+/* stft_mag: B signals x [b * x_bstride + n] (n < N) -> mag [b * mag_bstride + k * F + f] = |STFT| (k <= nfft/2),
+ *        reflect-centred frames x win (torch.stft center=True + sqrt(re^2 + im^2), RMVPE.py:168-169), an f64 FFT
+ *        rounded to f32 once; nfft a power of 2 <= 1024.  Replaces stft_frames + the DFT GEMM + spec_mag. */
+int rvc_stft_mag(const float* x, const float* win, float* mag, int64_t B, int64_t N, int64_t F, int nfft, int hop,
+                 int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream);
 int rvc_mel_image(const float* mel, float* img, int64_t M, int64_t F, int64_t Tp, float scale, float shift,
                   rvc_stream_t stream);
 int rvc_avgpool2(const float* in, float* out, int64_t C, int64_t H, int64_t W, rvc_stream_t stream);
@@ -313,13 +325,21 @@ int rvc_denoise(const float* y, int64_t n, const rvc_denoise_args* a, void* work
  * Replaces faiss IndexIVFFlat(L2).search(feats, k=8) + the blend of convert.py:349-359.
  * Queries (query i, dim c) live at q[c*cs + i*qs] (channels-first [d][nq]: cs = nq, qs = 1).
  * centT: centroids transposed [d][nlist]; inverted lists in CSR form: list_off [nlist+1],
- * codes [ntotal][d] (list-major), ids [ntotal].  Distances are computed in f64; results are
- * D f32 [nq][k] (squared L2), I int64 [nq][k], missing results (FLT_MAX, -1) as in faiss.
+ * codes [ntotal][d] (list-major), ids [ntotal].  Results are D f32 [nq][k] (squared L2), I int64 [nq][k],
+ * ascending by (distance, id), missing results (FLT_MAX, -1) as in faiss.
+ * Arithmetic (rvc_ivf_search = RVC_IVF_FAISS): faiss's own f32 evaluation -- coarse ||x||^2 + ||c||^2 - 2<x,c>
+ * clamped at 0 for nq >= 20 (knn_L2sqr's BLAS path), fvec_L2sqr below 20 and in the list scan, each f32 sum in
+ * the structure of faiss's AVX2 kernels (d % 8 == 0); RVC_IVF_EXACT: f64 distances (a diagnostic).
  * ws: rvc_ivf_coarse_ws_bytes(nq, nlist) bytes; probes: int64 [nq][nprobe] scratch/out. */
+enum { RVC_IVF_FAISS = 0, RVC_IVF_EXACT = 1 };
 int64_t rvc_ivf_coarse_ws_bytes(int64_t nq, int64_t nlist);
 int rvc_ivf_search(const float* q, int64_t nq, int64_t d, int64_t cs, int64_t qs, const float* centT, int64_t nlist,
                    int nprobe, const int64_t* list_off, const float* codes, const int64_t* ids, int k, void* ws,
                    int64_t ws_bytes, int64_t* probes, float* D, int64_t* I, rvc_stream_t stream);
+int rvc_ivf_search_ex(const float* q, int64_t nq, int64_t d, int64_t cs, int64_t qs, const float* centT,
+                      int64_t nlist, int nprobe, const int64_t* list_off, const float* codes, const int64_t* ids,
+                      int k, void* ws, int64_t ws_bytes, int64_t* probes, float* D, int64_t* I, int arithmetic,
+                      rvc_stream_t stream);
 /* out = (sum_j big[I_j] * w_j / sum w) * index_rate + (1 - index_rate) * feats, w = (1/D)^2, in the
  * f32 operation order of the reference's numpy/torch code; big = reconstruct_n(0, ntotal) [ntotal][d]. */
 int rvc_ivf_blend(const float* feats, int64_t nq, int64_t d, int64_t fcs, int64_t fqs, const float* D, const int64_t* I,
@@ -354,7 +374,8 @@ int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T,
  * on the same fp32 weights.
  *   rvc_ctx_create / destroy   one context per HIP device (not re-entrant; calls are stream-ordered).
  *   rvc_ctx_set_precision      the conv engine's arithmetic: RVC_PREC_FP32 (default: 6-pass split-bf16
- *                              mixed with split-fp16 where measured faster), _FP32X6, _F16X3, _BF16X3, _BF16.
+ *                              mixed with split-fp16 where measured faster), _FP32X6, _FP32SA, _F16X3,
+ *                              _BF16X3, _BF16.  RMVPE always runs at _FP32SA (rvc_rmvpe_forward).
  *   rvc_load_synth             params = the .pth "weight" dict (train.py:729-742) as named HOST arrays,
  *                              f32 or f16; weight-norm pairs (x.weight_g / x.weight_v) are folded at load
  *                              (torch._weight_norm, dim 0), already-folded x.weight is taken as is.
@@ -367,7 +388,8 @@ int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T,
 typedef struct rvc_ctx rvc_ctx;
 
 enum { RVC_DT_F32 = 0, RVC_DT_F16 = 1, RVC_DT_F64 = 2 };
-enum { RVC_PREC_FP32 = 0, RVC_PREC_BF16 = 1, RVC_PREC_BF16X3 = 3, RVC_PREC_FP32X6 = 6, RVC_PREC_F16X3 = 16 };
+enum { RVC_PREC_FP32 = 0, RVC_PREC_BF16 = 1, RVC_PREC_BF16X3 = 3, RVC_PREC_FP32X6 = 6, RVC_PREC_FP32SA = 7,
+       RVC_PREC_F16X3 = 16 };
 
 typedef struct rvc_param {
     const char* name;  /* state-dict key, e.g. "dec.ups.0.weight_v" */
@@ -459,7 +481,9 @@ typedef struct rvc_vc_args {
 /* The retrieval index rvc_vc_convert blends with (a faiss IndexIVFFlat(L2) as create_index.py writes it; read
  * without faiss by rvc_amd.faiss_index): HOST arrays, copied to the device.  centroids [nlist][d]; inverted lists
  * in CSR form: list_off [nlist + 1], codes [ntotal][d] (list-major), ids [ntotal]; big = reconstruct_n(0, ntotal)
- * [ntotal][d]; nprobe as the index stores it. */
+ * [ntotal][d]; nprobe as the index stores it.  Validated on the host (d a multiple of 8 up to 1024, ntotal > 0,
+ * list_off non-decreasing from 0 to ntotal, every id in [0, ntotal)): a malformed index is a load error.
+ * Loading again replaces the index and frees the previous one's device arrays (after a device sync). */
 typedef struct rvc_ivf_index {
     int64_t d, nlist, ntotal;
     int nprobe, _pad0;
@@ -471,6 +495,8 @@ typedef struct rvc_ivf_index {
 } rvc_ivf_index;
 
 int rvc_load_index(rvc_ctx* ctx, const rvc_ivf_index* index);
+/* device memory in use on the current device (hipMemGetInfo total - free), for load / reload accounting */
+int64_t rvc_device_bytes_in_use(void);
 
 int64_t rvc_vc_out_len(const rvc_ctx* ctx, int64_t N, const rvc_vc_args* args);
 int rvc_vc_convert(rvc_ctx* ctx, const float* audio, int64_t N, const rvc_vc_args* args, float* out,

@@ -15,17 +15,19 @@ import torch.nn.functional as F
 N_MELS, N_CLASS = 128, 360
 
 
-def load_weights(sd: dict) -> dict:
-    return {k: v.float() for k, v in sd.items() if v.is_floating_point()}
+def load_weights(sd: dict, dtype=torch.float32) -> dict:
+    """Float tensors of the state dict in ``dtype`` (f32 = the reference's arithmetic; f64 is the
+    diagnostic "exact" run the parity tests measure both the reference's and the device's f32 noise against)."""
+    return {k: v.to(dtype) for k, v in sd.items() if v.is_floating_point()}
 
 
 def mel_spectrogram(audio, mel_basis, n_fft=1024, hop=160, clamp=1e-5):
     """MelSpectrogram.forward, keyshift 0, center=True (RMVPE.py:162-181)."""
-    win = torch.hann_window(n_fft)
+    win = torch.hann_window(n_fft).to(audio.dtype)  # the f32 window (RMVPE.py:166), upcast in an f64 run
     fft = torch.stft(audio, n_fft=n_fft, hop_length=hop, win_length=n_fft, window=win, center=True,
                      return_complex=True)
     mag = torch.sqrt(fft.real.pow(2) + fft.imag.pow(2))
-    mel = torch.matmul(mel_basis, mag)
+    mel = torch.matmul(mel_basis.to(mag.dtype), mag)
     return torch.log(torch.clamp(mel, min=clamp))
 
 
@@ -72,8 +74,8 @@ def _gru_dir(x, w_ih, w_hh, b_ih, b_hh, reverse):
     T = x.shape[0]
     H = w_hh.shape[1]
     gi = F.linear(x, w_ih, b_ih)
-    h = torch.zeros(H)
-    out = torch.empty(T, H)
+    h = torch.zeros(H, dtype=x.dtype)
+    out = torch.empty(T, H, dtype=x.dtype)
     steps = range(T - 1, -1, -1) if reverse else range(T)
     for t in steps:
         gh = F.linear(h, w_hh, b_hh)
@@ -96,7 +98,7 @@ def bigru(W, x):
 
 def bigru_torch(W, x):
     """Same as ``bigru`` through torch's own GRU kernel (what the reference executes)."""
-    gru = torch.nn.GRU(384, 256, num_layers=1, batch_first=True, bidirectional=True)
+    gru = torch.nn.GRU(384, 256, num_layers=1, batch_first=True, bidirectional=True).to(x.dtype)
     gru.load_state_dict({k[len("fc.0.gru."):]: W[k] for k in W if k.startswith("fc.0.gru.")})
     with torch.no_grad():
         return gru(x)[0]

@@ -9,8 +9,8 @@
 // Block = 256 threads = 4 wave64s (WM x WN); a wave owns a (16*FM) x (16*FN) tile in FM*FN
 // accumulators.  Chunks are software-pipelined through registers: chunk i+1's global loads are
 // issued before chunk i's MFMAs and written to LDS after them (one LDS buffer, two barriers).
-// Small grids split the k range over blockIdx.z (split-K); partial tiles go to a workspace and
-// conv_splitk_reduce applies the epilogue.  The epilogue fuses bias, a second bias (speaker
+// Small grids split the k range over blockIdx.z (split-K); partial tiles go to a workspace and the
+// last of a tile's split blocks to finish sums them (in split order) and applies the epilogue.  The epilogue fuses bias, a second bias (speaker
 // conditioning), activation, residual add, accumulate, polyphase/strided stores (ConvTranspose)
 // and border masking (2-D mode).
 #include "rvc_common.h"
@@ -22,6 +22,10 @@
 namespace {
 
 constexpr int KCH = 32;     // flattened k per chunk
+// Split-K arrival counters, one per (output tile, compute wave), at the head of the workspace; zero when
+// the workspace is first used, and left zero by every launch (the last arriver resets its counter).
+constexpr int SPLITK_CNT = 16384;
+constexpr int64_t SPLITK_CNT_BYTES = SPLITK_CNT * 4;
 constexpr int NB_MAX = 16;  // staged B elements per thread (rows * span <= 256 * NB_MAX)
 
 struct ConvParams {
@@ -32,6 +36,8 @@ struct ConvParams {
     const float* res;
     float* y;
     float* ws;  // split-K partials [ksplit][B*nphase][Co][ncols]
+    unsigned* cnt;  // split-K arrival counters [tile]
+    int splitk_fused;  // 1: the last-arriving split block reduces; 0: conv_splitk_reduce after the launch
     int64_t B, Ci, Co, Lin, Lout, ncols;
     int64_t x_bstride, y_bstride, res_bstride, w_bstride;
     int K, stride, dil, pad, groups;
@@ -92,16 +98,24 @@ __device__ __forceinline__ void apply_act(floatx4 (&acc)[FM][FN], float slope, f
 }
 
 // Shared epilogue of the conv engines (both produce the MFMA 16x16 C layout: lane l holds column
-// l&15, rows (l>>4)*4 + r of each fragment).  Split-K partial tiles go to the workspace; otherwise
-// bias, 2nd bias, activation, scale, residual, accumulate and the (strided / polyphase / masked)
-// store are fused here.
+// l&15, rows (l>>4)*4 + r of each fragment).  Split-K: each split block stores its partial tile to the
+// workspace and counts in on the tile's arrival counter; the block that arrives last sums the ksplit
+// partials in split order -- the order of the separate reduce pass this replaced, so results are
+// unchanged -- and stores through epilogue_store (cdna_hip_programming.md, in-launch split-K: plain
+// stores, vmcnt drain, barrier, one agent release + relaxed ticket; the last arriver one agent acquire).
+// `lflag` is an LDS word of the kernel's own array, free by the time the epilogue runs.  Otherwise
+// bias, 2nd bias, activation, scale, residual, accumulate and the (strided / polyphase / masked) store
+// are fused here.
 template <int FM, int FN, int WM, int WN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc)[FM][FN], int lane, int wm, int wn,
-                                              int split, int phase, int b, int g, int Cog, int m0g, int64_t n0) {
+                                              int split, int phase, int b, int g, int Cog, int m0g, int64_t n0,
+                                              unsigned* lflag) {
     const int ln = lane & 15;
     const int lr = (lane >> 4) * 4;
     if (p.ksplit > 1) {
-        float* wsb = p.ws + (((int64_t)split * p.B * p.nphase + (int64_t)b * p.nphase + phase) * p.Co) * p.ncols;
+        const int64_t bp = (int64_t)b * p.nphase + phase;
+        const int64_t sstride = p.B * p.nphase * p.Co * p.ncols;
+        float* wsb = p.ws + split * sstride + bp * p.Co * p.ncols;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -112,6 +126,58 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
                 for (int j = 0; j < FN; ++j) {
                     const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
                     if (mg < Cog && n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
+                }
+            }
+        if (!p.splitk_fused) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every compute wave's partial stores done (loader waves have exited)
+        if (threadIdx.x == 0) {
+            const int64_t tile = ((int64_t)(blockIdx.z / p.ksplit) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned prev = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = prev == (unsigned)p.ksplit - 1;
+            if (last) {
+                __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            *lflag = last ? 1u : 0u;
+        }
+        __syncthreads();
+        if (!*lflag) return;
+        // the k loop outermost (one independent load per element per step), each element summed from 0 in
+        // split order, then stored element by element through epilogue_store as the reduce pass did
+        const float* src0 = p.ws + bp * p.Co * p.ncols;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < p.ksplit; ++k) {
+            const float* srck = src0 + k * sstride;
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
+                    const int64_t m = (int64_t)g * Cog + (mg < Cog ? mg : 0);
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
+                        acc[i][j][r] += srck[m * p.ncols + (n < p.ncols ? n : 0)];
+                    }
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
+                    if (mg < Cog && n < p.ncols)
+                        epilogue_store(p, acc[i][j][r], b, (int64_t)g * Cog + mg, out_pos(p, n, phase));
                 }
             }
         return;
@@ -358,7 +424,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
         __syncthreads();
     }
 
-    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, g, Cog, m0g, n0);
+    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, g, Cog, m0g, n0, (unsigned*)koff);
 }
 
 // ------------------------------------------------------------------ split-bf16 ("x6") engine
@@ -401,12 +467,17 @@ constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2
 // take the tile's |max| over every chunk of the block's k range (the chunks beyond the first two are
 // loaded for it alone; they stay in L2 for the staging pass), agree on a power-of-2 scale through LDS, and
 // stage the scaled activations as h / l planes; the epilogue multiplies by both reciprocal scales (exact).
-template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16>
+// SA (with NP = 6): the five correction passes (hM mH hL mM lH, each <= 2^-8 of hH) accumulate apart from
+// hH and the two sums are added once at the end: the f32 accumulator of the large terms is rounded once per
+// 32 products instead of six times, the corrections' roundings are 2^-8 smaller (RMVPE, whose f0 is a
+// per-frame decision: scripts/conv_prec.py).
+template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
     constexpr int NCW = WM * WN;  // compute waves; 4 loader waves follow them
     static_assert(NP == 6 || NP == 3 || NP == 1, "6, 3 or 1 passes");
     static_assert(!F16 || NP == 3, "split-fp16: 3 passes");
+    static_assert(!SA || (NP == 6 && !F16), "split accumulators: 6-pass split-bf16");
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
@@ -562,10 +633,17 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             for (int q = 0; q < NPL; ++q) a[q][i] = src[(i * 3 + q) * 64 + lane];
     };
     floatx4 acc[FM][FN];
+    floatx4 acc_lo[SA ? FM : 1][SA ? FN : 1];  // SA: the correction passes
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (SA) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc_lo[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
     const int ln = lane & 15, lg = lane >> 4;
     const int pb = wn * 16 * FN + ln;
     // B operands are read from LDS one column fragment j at a time (NPL ds_read_b128 each), the next
@@ -589,16 +667,25 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 for (int i = 0; i < FM; ++i) acc[i][j][0] += __builtin_bit_cast(float, (a[0][i].x ^ bq[NPL - 1].y) & 0x3fffffu);
                 continue;
             }
-            // NP passes over the FM accumulators of this column fragment
+            // NP passes over the FM accumulators of this column fragment: hH hM mH hL mM lH
             constexpr int PA[6] = {0, 0, 1, 0, 1, 2};
             constexpr int PB[6] = {0, 1, 0, 2, 1, 0};
+            if constexpr (SA) {
 #pragma unroll
-            for (int ps = 0; ps < NP; ++ps)
+                for (int i = 0; i < FM; ++i) acc[i][j] = mfma_bf16(a[0][i], bq[0], acc[i][j]);
 #pragma unroll
-                for (int i = 0; i < FM; ++i) {
-                    if constexpr (F16) acc[i][j] = mfma_f16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
-                    else acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
-                }
+                for (int ps = 1; ps < 6; ++ps)
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) acc_lo[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc_lo[i][j]);
+            } else {
+#pragma unroll
+                for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) {
+                        if constexpr (F16) acc[i][j] = mfma_f16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                        else acc[i][j] = mfma_bf16(a[PA[ps]][i], bq[PB[ps]], acc[i][j]);
+                    }
+            }
         }
     };
     // Weight fragments are prefetched PD k-steps ahead through a ring of NB = PD + 1 register buffers
@@ -608,7 +695,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     // depth: as many k-steps as fit a 24-uint4 (96-VGPR) ring, at most 4
     // (8 compute waves = 3 waves per SIMD: an 18-uint4 ring, at most 2 deep)
     // (a 256-column tile, FN = 8, keeps its 64 accumulators by giving the ring 12 uint4)
-    constexpr int PD_FIT = (FN == 8 ? 12 : (NCW == 8 ? 18 : 24)) / (NPL * FM) - 1;
+    constexpr int PD_FIT = ((FN == 8 ? 12 : (NCW == 8 ? 18 : 24)) - (SA ? FM * FN : 0)) / (NPL * FM) - 1;
     constexpr int PD_MAX = x6_min_blocks<FM, FN, NCW, NP>() == 2 ? 1 : (NCW == 8 ? 2 : 4);
     constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > PD_MAX ? PD_MAX : PD_FIT);
     constexpr int NB = PD + 1;
@@ -636,6 +723,14 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             }
         }
     }
+    if constexpr (SA) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] += acc_lo[i][j][r];
+    }
     if (kAblations && (p.dbg & 1)) {
         if (acc[0][0][0] == 1234.5f) p.y[lane] = acc[FM - 1][FN - 1][3];  // keep the loop live
         return;
@@ -653,9 +748,10 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 for (int j = 0; j < FN; ++j) acc[i][j][r] *= f;
             }
     }
-    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
+    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0, reinterpret_cast<unsigned*>(tmax));
 }
 
+// The separate split-K reduce (RVC_SPLITK_FUSED=0): sums the ksplit partials in split order, then the epilogue
 __global__ void conv_splitk_reduce(ConvParams p) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = blockIdx.y;
@@ -679,12 +775,12 @@ hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int FM, int FN, int WM, int WN, int NP, bool F16 = false>
+template <int FM, int FN, int WM, int WN, int NP, bool F16 = false, bool SA = false>
 void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     // loader items per thread sized to the staged span (unused items would still issue loads)
     const dim3 blk(64 * (WM * WN + 4));
-    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16>), grid, blk, lds, s, p);
+    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -692,12 +788,25 @@ hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) 
     if (p.wx_passes == RVC_ARITH_F16X3) launch_x6_np<FM, FN, WM, WN, 3, true>(p, grid, lds, s);
     else if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
     else if (p.wx_passes == 3) launch_x6_np<FM, FN, WM, WN, 3>(p, grid, lds, s);
+    else if (p.wx_passes == RVC_ARITH_FP32_SA) {
+        // split accumulators: only the tiles RMVPE's convs take (<= 64 rows on 4 / 8 waves, 128 x 128 on 8)
+        if constexpr ((WM * WN == 8 && FN == 4) || (WM * WN == 4 && FM <= 2 && FN == 2) || (WM == 2 && WN == 4))
+            launch_x6_np<FM, FN, WM, WN, 6, false, true>(p, grid, lds, s);
+        else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);
+    }
     else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);
     return hipGetLastError();
 }
 
 void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y; p.ws = nullptr;
+    p.cnt = nullptr;
+    // in-launch split-K reduce (RVC_SPLITK_FUSED=1): measured 11 % slower end to end than the separate
+    // reduce pass (780 vs 880 xRT, same box): each split block's agent release writes back its 64 KB+ partial
+    // tile and the last arriver sums up to 16 of them alone -- the guide's bound for in-launch combines is a
+    // few tens of KB per tile.  Off by default.
+    static const int fused = getenv("RVC_SPLITK_FUSED") ? atoi(getenv("RVC_SPLITK_FUSED")) : 0;
+    p.splitk_fused = fused;
     p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout;
     p.ncols = a->ncols > 0 ? a->ncols : a->Lout;
     p.x_bstride = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
@@ -727,7 +836,7 @@ void split_k(ConvParams& p, int64_t tiles, int nch) {
     // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU
     static const int target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
     int ks = 1;
-    if (tiles < target && nch >= 4) {
+    if (tiles < target && nch >= 4 && tiles * 8 <= SPLITK_CNT) {
         ks = (int)((target + tiles - 1) / tiles);
         if (ks > 16) ks = 16;
         if (ks > nch / 2) ks = nch / 2;
@@ -757,7 +866,8 @@ bool x6_eligible(const rvc_conv1d_args* a) {
     return a->wx && (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
            a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= X6_K_MAX &&
            (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
-           (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 || a->wx_passes == 3 ||
+           (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 ||
+                                                a->wx_passes == RVC_ARITH_FP32_SA || a->wx_passes == 3 ||
                                                 a->wx_passes == 1 || a->wx_passes == RVC_ARITH_F16X3);
 }
 
@@ -784,7 +894,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         // 8 compute waves (2 per SIMD beside 1 loader wave: one's MFMAs cover the other's waits) beat
         // 4 waves of twice the tile on every 128/256-channel shape, and on 64 channels at >= 3 passes
         static const int w8 = getenv("RVC_X6_W8") ? atoi(getenv("RVC_X6_W8")) : 1;
-        const int np = a->wx_passes == 0 ? 6 : a->wx_passes;
+        const int np = a->wx_passes == 0 || a->wx_passes == RVC_ARITH_FP32_SA ? 6 : a->wx_passes;
         // 128 x 256 on 8 compute waves for the split-fp16 convs (RVC_X6_BN256: 1 = split-fp16 only, the
         // default; 2 = every pass set; 0 = off): half the blocks, so half the per-block prologue / epilogue
         // (~15-25 us each), and each weight fragment feeds twice the MFMAs; stride-1, short tap spans.
@@ -813,7 +923,8 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
         const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
         split_k(p, tiles, p.wx_nch);
-        lds = (size_t)2 * (p.wx_passes == 6 ? 3 : (p.wx_passes == 1 ? 1 : 2)) * p.span * 64 + 16;  // + F16 tile max
+        lds = (size_t)2 * (p.wx_passes == 6 || p.wx_passes == RVC_ARITH_FP32_SA ? 3 : (p.wx_passes == 1 ? 1 : 2)) *
+              p.span * 64 + 16;  // + F16 tile max / split-K flag
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         return RVC_OK;
@@ -1002,7 +1113,7 @@ extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {
     size_t lds;
     if (plan(a, p, cfg, grid, lds) != RVC_OK) return -1;
     if (p.ksplit <= 1) return 0;
-    return (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+    return SPLITK_CNT_BYTES + (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
 }
 
 extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
@@ -1013,10 +1124,11 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     int rc = plan(a, p, cfg, grid, lds);
     if (rc != RVC_OK) return rc;
     if (p.ksplit > 1) {
-        const int64_t need = (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+        const int64_t need = SPLITK_CNT_BYTES + (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
         RVC_CHECK_ARG(ws && ws_bytes >= need, "conv1d: split-K needs %lld B of workspace (got %lld)",
                       (long long)need, (long long)ws_bytes);
-        p.ws = (float*)ws;
+        p.cnt = (unsigned*)ws;
+        p.ws = (float*)((char*)ws + SPLITK_CNT_BYTES);
     }
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
@@ -1038,7 +1150,7 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     else if (cfg.FN == 4) e = launch<2, 4, 2, 2>(p, grid, lds, s);
     else e = launch<2, 2, 2, 2>(p, grid, lds, s);
     RVC_HIP(e);
-    if (p.ksplit > 1) {
+    if (p.ksplit > 1 && !p.splitk_fused) {
         hipLaunchKernelGGL(conv_splitk_reduce, dim3(cdiv(p.ncols, 256), (unsigned)p.Co, (unsigned)(p.B * p.nphase)),
                            dim3(256), 0, s, p);
         RVC_HIP(hipGetLastError());

@@ -303,6 +303,8 @@ inline int ensure_ws(ModelBase& m, int64_t need, hipStream_t s) {
     }
     const int64_t bytes = need + (4 << 20);
     MHIP(hipMalloc(&m.ws, bytes));
+    // the conv engine's split-K arrival counters start at zero -- ordered on s, before the launch that uses it
+    MHIP(hipMemsetAsync(m.ws, 0, bytes, s));
     m.ws_bytes = bytes;
     return RVC_OK;
 }

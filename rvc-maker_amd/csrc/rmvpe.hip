@@ -47,6 +47,84 @@ extern "C" int rvc_spec_mag(const float* spec, float* mag, int64_t K, int64_t F,
     return RVC_OK;
 }
 
+// ---------------------------------------------------------------- STFT magnitude in f64
+// mag[b][k][f] = |sum_n xr[f*hop + n - nfft/2] win[n] e^{-2 pi i k n / nfft}| for k <= nfft/2, with centred
+// reflect padding (torch.stft center=True, RMVPE.py:168-169), computed as an f64 radix-2 FFT in LDS and
+// rounded to f32 once.  The reference evaluates this in f32 (torch.stft + sqrt(re^2 + im^2)); a bin far
+// below the frame's energy then carries a relative error that log(clamp(mel, 1e-5)) turns into an absolute
+// one (1e-3 on the synthetic weights with the f32 DFT GEMM this replaced, 2e-4 for torch's f32 FFT, ~1e-7
+// here: scripts/rmvpe_prec.py).  STFT_FPB frames per block share the twiddle table; the bins of a block are
+// stored STFT_FPB consecutive frames at a time.
+constexpr int STFT_NMAX = 1024, STFT_FPB = 8;
+
+__global__ __launch_bounds__(256) void stft_mag_kernel(const float* x, const float* win, float* mag, int64_t N,
+                                                       int64_t F, int nfft, int logn, int hop, int64_t x_bs,
+                                                       int64_t m_bs) {
+    __shared__ double2 a[STFT_FPB][STFT_NMAX];
+    __shared__ double2 tw[STFT_NMAX / 2];
+    const int b = blockIdx.y;
+    const int64_t f0 = (int64_t)blockIdx.x * STFT_FPB;
+    const float* xb = x + b * x_bs;
+    for (int j = threadIdx.x; j < nfft / 2; j += blockDim.x) {
+        double s, c;
+        sincospi(-2.0 * (double)j / (double)nfft, &s, &c);
+        tw[j] = make_double2(c, s);
+    }
+    for (int i = threadIdx.x; i < STFT_FPB * nfft; i += blockDim.x) {
+        const int q = i / nfft, n = i - q * nfft;
+        const int64_t f = f0 + q;
+        double v = 0.0;
+        if (f < F) {
+            int64_t j = f * hop + n - nfft / 2;
+            if (j < 0) j = -j;
+            if (j >= N) j = 2 * (N - 1) - j;
+            v = (double)xb[j] * (double)win[n];
+        }
+        a[q][__brev((unsigned)n) >> (32 - logn)] = make_double2(v, 0.0);
+    }
+    __syncthreads();
+    for (int s = 1; s <= logn; ++s) {
+        const int half = 1 << (s - 1);
+        for (int j = threadIdx.x; j < nfft / 2; j += blockDim.x) {
+            const int pos = j & (half - 1);
+            const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + half;
+            const double2 w = tw[pos << (logn - s)];
+#pragma unroll
+            for (int q = 0; q < STFT_FPB; ++q) {
+                const double2 u = a[q][i0], v = a[q][i1];
+                const double2 t = make_double2(w.x * v.x - w.y * v.y, w.x * v.y + w.y * v.x);
+                a[q][i0] = make_double2(u.x + t.x, u.y + t.y);
+                a[q][i1] = make_double2(u.x - t.x, u.y - t.y);
+            }
+        }
+        __syncthreads();
+    }
+    const int K = nfft / 2 + 1;
+    float* mb = mag + b * m_bs;
+    for (int i = threadIdx.x; i < K * STFT_FPB; i += blockDim.x) {
+        const int k = i / STFT_FPB, q = i - k * STFT_FPB;
+        const int64_t f = f0 + q;
+        if (f < F) {
+            const double2 v = a[q][k];
+            mb[(int64_t)k * F + f] = (float)sqrt(v.x * v.x + v.y * v.y);
+        }
+    }
+}
+
+extern "C" int rvc_stft_mag(const float* x, const float* win, float* mag, int64_t B, int64_t N, int64_t F,
+                            int nfft, int hop, int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream) {
+    int logn = 0;
+    while ((1 << logn) < nfft) ++logn;
+    RVC_CHECK_ARG(x && win && mag && B > 0 && N > nfft / 2 && F > 0 && hop > 0, "stft_mag: bad args");
+    RVC_CHECK_ARG((1 << logn) == nfft && nfft >= 2 && nfft <= STFT_NMAX, "stft_mag: nfft must be a power of 2 <= 1024");
+    RVC_CHECK_ARG((F - 1) * hop <= 2 * (N - 1), "stft_mag: F too large for reflect padding");
+    RVC_CHECK_ARG(B == 1 || (x_bstride >= N && mag_bstride >= (int64_t)(nfft / 2 + 1) * F), "stft_mag: bad batch strides");
+    hipLaunchKernelGGL(stft_mag_kernel, dim3(cdiv(F, STFT_FPB), (unsigned)B), dim3(256), 0, (hipStream_t)stream, x,
+                       win, mag, N, F, nfft, logn, hop, x_bstride, mag_bstride);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
 // ---------------------------------------------------------------- U-Net input image
 // img[(t+1)*(W+2) + m+1] = mel[m][src(t)] * scale + shift for t < Tp (reflect-padded frames,
 // RMVPE.py:213) with the encoder's input BatchNorm2d(1) folded to (scale, shift) (RMVPE.py:64).

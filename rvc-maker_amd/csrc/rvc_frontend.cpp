@@ -39,7 +39,7 @@ struct ContentVec : ModelBase {
 };
 
 struct Rmvpe : ModelBase {
-    ConvW dft, mel, cnn, w_ih, fc;
+    ConvW mel, cnn, w_ih, fc;
     float in_scale = 1.f, in_shift = 0.f;
     float *window = nullptr, *w_hh = nullptr, *b_hh = nullptr;
     std::vector<std::vector<fem::Cbr>> enc, inter;  // [level][block]
@@ -294,16 +294,9 @@ int cbr_run(rvc_ctx* c, Rmvpe& M, Scratch& sc, const Cbr& blk, const float* x, i
 // mel -> U-Net -> BiGRU -> fc for one sequence (rmvpe.py f0_device up to the decode)
 int rm_one(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, float* sal, hipStream_t s) {
     const int64_t F = 1 + N / kHop, Tp = 32 * ((F - 1) / 32 + 1);
-    // MelSpectrogram.forward (RMVPE.py:162-181)
-    float* frames = sc.take((int64_t)kNfft * F);
-    RUN(rvc_stft_frames(wav, M.window, frames, N, F, kNfft, kHop, s));
-    float* spec = sc.take((int64_t)(kNfft + 2) * F);
-    {
-        CallOpts o;
-        RUN(conv(c, M, M.dft, frames, F, spec, o, s));
-    }
+    // MelSpectrogram.forward (RMVPE.py:162-181): |STFT| in f64 (rvc_stft_mag), then the mel GEMM + log
     float* mag = sc.take((int64_t)(kNfft / 2 + 1) * F);
-    RUN(rvc_spec_mag(spec, mag, kNfft / 2 + 1, F, s));
+    RUN(rvc_stft_mag(wav, M.window, mag, 1, N, F, kNfft, kHop, 0, 0, s));
     float* mel = sc.take((int64_t)kMels * F);
     {
         CallOpts o;
@@ -521,7 +514,7 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
     Rmvpe& M = *c->rm;
     HostT w, b;
 #define GET(k, t) MCHECK(P.get(k, t), "rvc_load_rmvpe: missing %s", P.missing.c_str())
-    // constants: Hann window, DFT basis, mel basis (rmvpe.py __init__, melbasis.py)
+    // constants: Hann window, mel basis (rmvpe.py __init__, melbasis.py)
     if (P.has("window")) {
         GET("window", w);
         MCHECK((int64_t)w.v.size() == kNfft, "rvc_load_rmvpe: window must have %d entries", kNfft);
@@ -536,18 +529,6 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
         }
     }
     MTRY(upload(M, w.v, &M.window));
-    {
-        HostT d;
-        d.shape = {kNfft + 2, kNfft, 1};
-        d.v.resize((size_t)(kNfft + 2) * kNfft);
-        for (int k = 0; k <= kNfft / 2; ++k)
-            for (int i = 0; i < kNfft; ++i) {
-                const double ang = 2.0 * M_PI * (double)((int64_t)k * i) / kNfft;
-                d.v[(size_t)k * kNfft + i] = (float)cos(ang);
-                d.v[(size_t)(k + kNfft / 2 + 1) * kNfft + i] = (float)-sin(ang);
-            }
-        MTRY(make_conv(c, M, d, nullptr, M.dft));
-    }
     HostT mb;
     if (P.has("mel_basis")) {
         GET("mel_basis", mb);
@@ -648,7 +629,7 @@ extern "C" int rvc_rmvpe_forward(rvc_ctx* c, const float* wav, int64_t B, int64_
     MHIP(hipSetDevice(c->device));
     Rmvpe& M = *c->rm;
     const int prev = c->prec;
-    c->prec = RVC_PREC_FP32;  // f32-accurate whatever the context's precision (rmvpe.py: self.precision)
+    c->prec = RVC_PREC_FP32SA;  // exact products whatever the context's precision (rmvpe.py: self.precision)
     Scratch sc;
     int rc = rm_one(c, M, sc, wav, N, salience, s);
     if (rc == RVC_OK) rc = ensure_arena(M, sc.off, s);
@@ -912,21 +893,28 @@ int contentvec_cf(rvc_ctx* c, const float* wav, int64_t N, int out_layer, int fi
 // ------------------------------------------------------------------ one VC.pipeline segment (rvc_amd/pipeline.py)
 // rvc_vc_convert's scratch plus its f0 side stream: RMVPE runs there, concurrently with ContentVec on the
 // caller's stream (as VC._pipeline_on_device does), joined by an event before the phone upsample
-struct VcState : ModelBase {
-    hipStream_t side = nullptr;
-    hipEvent_t ev_in = nullptr, ev_f0 = nullptr;
-    // retrieval index (rvc_load_index): device copies, owned in allocs
-    bool has_index = false;
+// the retrieval index (rvc_load_index): device copies, owned here and freed as a whole when replaced
+struct IvfIndex : ModelBase {
     int64_t d = 0, nlist = 0, ntotal = 0;
     int nprobe = 1;
     float *centT = nullptr, *codes = nullptr, *big = nullptr;
     int64_t *list_off = nullptr, *ids = nullptr;
+};
+
+struct VcState : ModelBase {
+    hipStream_t side = nullptr;
+    hipEvent_t ev_in = nullptr, ev_f0 = nullptr;
+    IvfIndex* ix = nullptr;
     void* ivf_ws = nullptr;
     int64_t ivf_ws_bytes = 0;
 };
 
 void vc_delete(VcState* v) {
     if (!v) return;
+    if (v->ix) {
+        v->ix->release();
+        delete v->ix;
+    }
     if (v->ivf_ws) (void)hipFree(v->ivf_ws);
     if (v->side) (void)hipStreamDestroy(v->side);
     if (v->ev_in) (void)hipEventDestroy(v->ev_in);
@@ -969,7 +957,7 @@ int vc_plan(const rvc_ctx* c, int64_t N, const rvc_vc_args* a, VcPlan& p) {
     p.C = a->version == 1 ? c->cv->final_proj.Co : c->cv->E;
     MCHECK(p.C == emb_dim, "rvc_vc_convert: features of %lld channels, the synthesizer takes %d", (long long)p.C,
            emb_dim);
-    MCHECK(a->index_rate == 0.0 || (c->vc && c->vc->has_index && c->vc->d == p.C),
+    MCHECK(a->index_rate == 0.0 || (c->vc && c->vc->ix && c->vc->ix->d == p.C),
            "rvc_vc_convert: index_rate %g needs an index of the features' width (rvc_load_index)", a->index_rate);
     p.L = p.T * upp;
     p.tp = (int64_t)a->tgt_sr * a->x_pad;
@@ -1009,7 +997,8 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
                   o_coarse = pl.take(2 * p.F), o_pitchf = pl.take(p.F), o_feats = pl.take(p.C * p.Tf),
                   o_phone = pl.take(p.C * p.T), o_wav = pl.take(p.L), o_ws = pl.take(16),
                   o_blend = pl.take(p.C * p.Tf), o_D = pl.take(8 * p.Tf), o_I = pl.take(2 * 8 * p.Tf),
-                  o_probes = pl.take(2 * (int64_t)V.nprobe * p.Tf);
+                  o_probes = pl.take(2 * (int64_t)(V.ix ? V.ix->nprobe : 1) * p.Tf);
+    if (pl.off > V.arena_floats && V.side) MHIP(hipStreamSynchronize(V.side));  // the old arena may be in use there
     MTRY(ensure_arena(V, pl.off, s));
     float* A = V.arena;
     float* xp = A + o_xp;
@@ -1021,6 +1010,16 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     float* pitchf = A + o_pitchf;
     MHIP(hipEventRecord(V.ev_in, s));
     MHIP(hipStreamWaitEvent(V.side, V.ev_in, 0));
+    // from the fork on, every return joins the side stream back into s (its writes to V.arena must be
+    // ordered before the next call's arena use on s)
+    struct Join {
+        hipStream_t s, side;
+        hipEvent_t ev;
+        bool armed = true;
+        ~Join() {
+            if (armed && hipEventRecord(ev, side) == hipSuccess) (void)hipStreamWaitEvent(s, ev, 0);
+        }
+    } join{s, V.side, V.ev_f0};
     MTRY(rvc_rmvpe_forward(c, xp, 1, p.Np, sal, (rvc_stream_t)V.side));
     MTRY(rvc_rmvpe_decode(sal, p.ld, p.F, 0.03, pow(2.0, a->pitch_shift / 12.0), nullptr, nullptr, coarse, pitchf,
                           (rvc_stream_t)V.side));
@@ -1030,7 +1029,8 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
     MTRY(contentvec_cf(c, xp, p.Np, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
     const float* fb = feats;  // convert.py:347: the protect blend keeps the pre-retrieval features
     if (a->index_rate != 0.0) {  // search(k = 8) + blend (convert.py:349-359) on the channels-first features
-        const int64_t need = rvc_ivf_coarse_ws_bytes(p.Tf, V.nlist);
+        const IvfIndex& X = *V.ix;
+        const int64_t need = rvc_ivf_coarse_ws_bytes(p.Tf, X.nlist);
         if (need > V.ivf_ws_bytes) {
             if (V.ivf_ws) {
                 MHIP(hipStreamSynchronize(s));
@@ -1042,12 +1042,13 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
         }
         float* D = A + o_D;
         int64_t* I = (int64_t*)(A + o_I);
-        MTRY(rvc_ivf_search(feats, p.Tf, p.C, p.Tf, 1, V.centT, V.nlist, V.nprobe, V.list_off, V.codes, V.ids, 8,
+        MTRY(rvc_ivf_search(feats, p.Tf, p.C, p.Tf, 1, X.centT, X.nlist, X.nprobe, X.list_off, X.codes, X.ids, 8,
                             V.ivf_ws, need, (int64_t*)(A + o_probes), D, I, (rvc_stream_t)s));
-        MTRY(rvc_ivf_blend(feats, p.Tf, p.C, p.Tf, 1, D, I, 8, V.big, V.ntotal, a->index_rate, A + o_blend, p.Tf,
+        MTRY(rvc_ivf_blend(feats, p.Tf, p.C, p.Tf, 1, D, I, 8, X.big, X.ntotal, a->index_rate, A + o_blend, p.Tf,
                            1, (rvc_stream_t)s));
         fb = A + o_blend;
     }
+    join.armed = false;
     MHIP(hipStreamWaitEvent(s, V.ev_f0, 0));  // join: the upsample reads pitchf
     float* phone = A + o_phone;
     MTRY(rvc_phone_upsample(fb, feats, a->protect < 0.5f ? pitchf : nullptr, phone, p.C, p.Tf, p.T, a->protect,
@@ -1060,36 +1061,58 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
 }
 
 extern "C" int rvc_load_index(rvc_ctx* c, const rvc_ivf_index* x) {
-    MCHECK(c && x && x->centroids && x->list_off && x->big && x->d > 0 && x->nlist > 0 && x->ntotal >= 0 &&
-               x->nprobe >= 1,
-           "rvc_load_index: bad index");
+    MCHECK(c && x && x->centroids && x->list_off && x->big && x->codes && x->ids, "rvc_load_index: null array");
+    // everything rvc_ivf_search / rvc_ivf_blend read on the device is validated here, on the host, so that a
+    // malformed or foreign index is a load error instead of an out-of-bounds device read later
+    MCHECK(x->d > 0 && x->d <= 1024 && x->d % 8 == 0, "rvc_load_index: d = %lld (1..1024, a multiple of 8)",
+           (long long)x->d);
+    MCHECK(x->nlist > 0 && x->ntotal > 0 && x->nprobe >= 1, "rvc_load_index: nlist %lld, ntotal %lld, nprobe %d",
+           (long long)x->nlist, (long long)x->ntotal, x->nprobe);
     MCHECK(x->list_off[0] == 0 && x->list_off[x->nlist] == x->ntotal, "rvc_load_index: list_off must span [0, ntotal]");
-    MCHECK(x->ntotal == 0 || (x->codes && x->ids), "rvc_load_index: codes / ids missing");
+    for (int64_t l = 0; l < x->nlist; ++l)
+        MCHECK(x->list_off[l] <= x->list_off[l + 1], "rvc_load_index: list_off decreases at list %lld", (long long)l);
+    for (int64_t i = 0; i < x->ntotal; ++i)
+        MCHECK(x->ids[i] >= 0 && x->ids[i] < x->ntotal, "rvc_load_index: id %lld of entry %lld outside [0, ntotal)",
+               (long long)x->ids[i], (long long)i);
     MHIP(hipSetDevice(c->device));
     if (!c->vc) c->vc = new VcState();
     VcState& V = *c->vc;
-    if (V.has_index) {  // replace: the old arrays stay owned until the context goes (allocs)
-        V.has_index = false;
+    if (V.ix) {  // replace: no call may still read the old arrays
+        MHIP(hipDeviceSynchronize());
+        V.ix->release();
+        delete V.ix;
+        V.ix = nullptr;
     }
-    V.d = x->d;
-    V.nlist = x->nlist;
-    V.ntotal = x->ntotal;
-    V.nprobe = x->nprobe < x->nlist ? x->nprobe : (int)x->nlist;
+    IvfIndex* X = new IvfIndex();
+    X->d = x->d;
+    X->nlist = x->nlist;
+    X->ntotal = x->ntotal;
+    X->nprobe = x->nprobe < x->nlist ? x->nprobe : (int)x->nlist;
+    auto fail = [&](int rc) {
+        X->release();
+        delete X;
+        return rc;
+    };
     std::vector<float> ct((size_t)x->d * x->nlist);  // centroids transposed [d][nlist] (retrieval.py)
     for (int64_t l = 0; l < x->nlist; ++l)
         for (int64_t k = 0; k < x->d; ++k) ct[(size_t)k * x->nlist + l] = x->centroids[l * x->d + k];
-    MTRY(upload(V, ct, &V.centT));
-    const int64_t nt = x->ntotal > 0 ? x->ntotal : 1;
+    int rc = upload(*X, ct, &X->centT);
     auto up = [&](const void* src, size_t bytes, void** dst) -> int {
-        MTRY(dev_alloc(V, bytes, dst));
-        if (src) MHIP(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
-        else MHIP(hipMemset(*dst, 0, bytes));
+        MTRY(dev_alloc(*X, bytes, dst));
+        MHIP(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
         return RVC_OK;
     };
-    MTRY(up(x->list_off, (x->nlist + 1) * 8, (void**)&V.list_off));
-    MTRY(up(x->ntotal ? x->codes : nullptr, nt * x->d * 4, (void**)&V.codes));
-    MTRY(up(x->ntotal ? x->ids : nullptr, nt * 8, (void**)&V.ids));
-    MTRY(up(x->ntotal ? x->big : nullptr, nt * x->d * 4, (void**)&V.big));
-    V.has_index = true;
+    if (rc == RVC_OK) rc = up(x->list_off, (x->nlist + 1) * 8, (void**)&X->list_off);
+    if (rc == RVC_OK) rc = up(x->codes, x->ntotal * x->d * 4, (void**)&X->codes);
+    if (rc == RVC_OK) rc = up(x->ids, x->ntotal * 8, (void**)&X->ids);
+    if (rc == RVC_OK) rc = up(x->big, x->ntotal * x->d * 4, (void**)&X->big);
+    if (rc != RVC_OK) return fail(rc);
+    V.ix = X;
     return RVC_OK;
+}
+
+extern "C" int64_t rvc_device_bytes_in_use(void) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return -1;
+    return (int64_t)(total_b - free_b);
 }

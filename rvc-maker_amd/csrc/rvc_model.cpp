@@ -378,7 +378,7 @@ extern "C" void rvc_ctx_destroy(rvc_ctx* c) {
 extern "C" int rvc_ctx_set_precision(rvc_ctx* c, int prec) {
     MCHECK(c, "rvc_ctx_set_precision: null ctx");
     MCHECK(prec == RVC_PREC_FP32 || prec == RVC_PREC_BF16 || prec == RVC_PREC_BF16X3 || prec == RVC_PREC_FP32X6 ||
-               prec == RVC_PREC_F16X3,
+               prec == RVC_PREC_FP32SA || prec == RVC_PREC_F16X3,
            "rvc_ctx_set_precision: unknown precision %d", prec);
     c->prec = prec;
     return RVC_OK;
@@ -389,6 +389,21 @@ extern "C" int64_t rvc_synth_out_len(const rvc_ctx* c, int64_t T) {
     return T * c->syn->upp;
 }
 
+namespace {
+// shape check of a loaded tensor: dims d0..d2 (-1 = any); a mismatch is a load error, not a device fault later
+int expect(const HostT& t, const std::string& name, int64_t d0, int64_t d1 = -1, int64_t d2 = -1, int ndim = -1) {
+    const int64_t want[3] = {d0, d1, d2};
+    int64_t numel = 1;
+    for (int64_t x : t.shape) numel *= x;
+    MCHECK(numel == (int64_t)t.v.size(), "rvc_load_synth: %s: %zu values for its shape", name.c_str(), t.v.size());
+    MCHECK(ndim < 0 || (int)t.shape.size() == ndim, "rvc_load_synth: %s must be %d-D", name.c_str(), ndim);
+    for (int i = 0; i < 3; ++i)
+        MCHECK(want[i] < 0 || t.dim(i) == want[i], "rvc_load_synth: %s dim %d is %lld, expected %lld", name.c_str(), i,
+               (long long)t.dim(i), (long long)want[i]);
+    return RVC_OK;
+}
+}  // namespace
+
 extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const rvc_synth_cfg* cfg) {
     MCHECK(c && params && n > 0 && cfg, "rvc_load_synth: null argument");
     const rvc_synth_cfg& g = *cfg;
@@ -397,6 +412,9 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
     MCHECK(g.n_upsamples >= 1 && g.n_upsamples <= 8 && g.n_resblocks >= 1 && g.n_resblocks <= 4 && g.n_dilations >= 1 &&
                g.n_dilations <= 4,
            "rvc_load_synth: bad generator config");
+    MCHECK(g.hidden_channels > 0 && g.filter_channels > 0 && g.kernel_size > 0 && g.inter_channels > 0 &&
+               g.gin_channels > 0 && g.upsample_initial_channel >> g.n_upsamples > 0,
+           "rvc_load_synth: bad channel config");
     Params PM;  // x.weight folded from x.weight_g / x.weight_v (dim 0) when those are given
     MTRY(index_params(params, n, PM, "rvc_load_synth"));
     MHIP(hipSetDevice(c->device));
@@ -417,10 +435,12 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
     // ---- TextEncoder
     GET("enc_p.emb_phone.weight", w);
     GET("enc_p.emb_phone.bias", b);
+    MTRY(expect(w, "enc_p.emb_phone.weight", H, -1, -1, 2));
     S.emb_dim = (int)w.dim(1);
     w.shape.push_back(1);
     MTRY(make_conv(c, S, w, &b, S.emb_phone));
     GET("enc_p.emb_pitch.weight", w);
+    MTRY(expect(w, "enc_p.emb_pitch.weight", 256, H, -1, 2));
     MTRY(upload(S, w.v, &S.emb_pitch));
     for (int i = 0; i < g.n_layers; ++i) {
         Layer Ly;
@@ -432,6 +452,9 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         GET(p + "conv_q.bias", bq);
         GET(p + "conv_k.bias", bk);
         GET(p + "conv_v.bias", bv);
+        MTRY(expect(q, p + "conv_q.weight", H, H, 1));
+        MTRY(expect(k, p + "conv_k.weight", H, H, 1));
+        MTRY(expect(v, p + "conv_v.weight", H, H, 1));
         HostT wqkv = q, bqkv = bq;
         wqkv.v.insert(wqkv.v.end(), k.v.begin(), k.v.end());
         wqkv.v.insert(wqkv.v.end(), v.v.begin(), v.v.end());
@@ -446,29 +469,38 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         ek.shape = {21, S.kc, 1};
         MTRY(make_conv(c, S, ek, nullptr, Ly.relk));
         GET(p + "emb_rel_v", w);
+        MTRY(expect(w, p + "emb_rel_v", 1, 21, S.kc));
         MTRY(upload(S, w.v, &Ly.ev));
         GET(p + "conv_o.weight", w);
         GET(p + "conv_o.bias", b);
+        MTRY(expect(w, p + "conv_o.weight", H, H, 1));
         MTRY(make_conv(c, S, w, &b, Ly.o));
         const std::string si = std::to_string(i);
         GET("enc_p.encoder.norm_layers_1." + si + ".gamma", w);
+        MTRY(expect(w, "norm_layers_1." + si + ".gamma", H, -1, -1, 1));
         MTRY(upload(S, w.v, &Ly.ln1g));
         GET("enc_p.encoder.norm_layers_1." + si + ".beta", w);
+        MTRY(expect(w, "norm_layers_1." + si + ".beta", H, -1, -1, 1));
         MTRY(upload(S, w.v, &Ly.ln1b));
         GET("enc_p.encoder.ffn_layers." + si + ".conv_1.weight", w);
         GET("enc_p.encoder.ffn_layers." + si + ".conv_1.bias", b);
+        MTRY(expect(w, "ffn_layers." + si + ".conv_1.weight", g.filter_channels, H, g.kernel_size));
         MTRY(make_conv(c, S, w, &b, Ly.ffn1));
         GET("enc_p.encoder.ffn_layers." + si + ".conv_2.weight", w);
         GET("enc_p.encoder.ffn_layers." + si + ".conv_2.bias", b);
+        MTRY(expect(w, "ffn_layers." + si + ".conv_2.weight", H, g.filter_channels, g.kernel_size));
         MTRY(make_conv(c, S, w, &b, Ly.ffn2));
         GET("enc_p.encoder.norm_layers_2." + si + ".gamma", w);
+        MTRY(expect(w, "norm_layers_2." + si + ".gamma", H, -1, -1, 1));
         MTRY(upload(S, w.v, &Ly.ln2g));
         GET("enc_p.encoder.norm_layers_2." + si + ".beta", w);
+        MTRY(expect(w, "norm_layers_2." + si + ".beta", H, -1, -1, 1));
         MTRY(upload(S, w.v, &Ly.ln2b));
         S.layers.push_back(Ly);
     }
     GET("enc_p.proj.weight", w);
     GET("enc_p.proj.bias", b);
+    MTRY(expect(w, "enc_p.proj.weight", 2 * g.inter_channels, H, 1));
     MTRY(make_conv(c, S, w, &b, S.proj));
     // ---- speaker conditioning: 4 flows' cond layers then dec.cond, stacked (synth.py)
     {
@@ -477,6 +509,7 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
             const std::string p = f < 4 ? "flow.flows." + std::to_string(2 * f) + ".enc.cond_layer." : "dec.cond.";
             GET(p + "weight", w);
             GET(p + "bias", b);
+            MTRY(expect(w, p + "weight", f < 4 ? 2 * H * 3 : g.upsample_initial_channel, g.gin_channels, 1));
             if (f == 0) {
                 cw = w;
                 cb = b;
@@ -499,17 +532,21 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         const std::string p = "flow.flows." + std::to_string(2 * f) + ".";
         GET(p + "pre.weight", w);
         GET(p + "pre.bias", b);
+        MTRY(expect(w, p + "pre.weight", H, g.inter_channels / 2, 1));
         MTRY(make_conv(c, S, w, &b, F.pre));
         GET(p + "post.weight", w);
         GET(p + "post.bias", b);
+        MTRY(expect(w, p + "post.weight", g.inter_channels / 2, H, 1));
         MTRY(make_conv(c, S, w, &b, F.post));
         for (int l = 0; l < 3; ++l) {
             const std::string sl = std::to_string(l);
             GET(p + "enc.in_layers." + sl + ".weight", w);
             GET(p + "enc.in_layers." + sl + ".bias", b);
+            MTRY(expect(w, p + "enc.in_layers." + sl + ".weight", 2 * H, H, 5));
             MTRY(make_conv(c, S, w, &b, F.ins[l]));
             GET(p + "enc.res_skip_layers." + sl + ".weight", w);
             GET(p + "enc.res_skip_layers." + sl + ".bias", b);
+            MTRY(expect(w, p + "enc.res_skip_layers." + sl + ".weight", l < 2 ? 2 * H : H, H, 1));
             if (l < 2) {  // res half [:H], skip half [H:]
                 const int64_t inner = (int64_t)w.v.size() / w.dim(0);
                 HostT wa = w, wb = w, ba = b, bb = b;
@@ -529,10 +566,13 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
     // ---- generator
     GET("dec.m_source.l_linear.weight", w);
     GET("dec.m_source.l_linear.bias", b);
+    MTRY(expect(w, "dec.m_source.l_linear.weight", 1, 1, -1, 2));
+    MTRY(expect(b, "dec.m_source.l_linear.bias", 1, -1, -1, 1));
     S.lin_w = w.v[0];
     S.lin_b = b.v[0];
     GET("dec.conv_pre.weight", w);
     GET("dec.conv_pre.bias", b);
+    MTRY(expect(w, "dec.conv_pre.weight", g.upsample_initial_channel, g.inter_channels, 7));
     MTRY(make_conv(c, S, w, &b, S.conv_pre));
     const int nup = g.n_upsamples;
     S.ups.resize(nup);
@@ -544,6 +584,9 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         const std::string si = std::to_string(i);
         GET("dec.ups." + si + ".weight", w);
         GET("dec.ups." + si + ".bias", b);
+        const int ch = g.upsample_initial_channel >> (i + 1);
+        MTRY(expect(w, "dec.ups." + si + ".weight", 2 * ch, ch, k));
+        MTRY(expect(b, "dec.ups." + si + ".bias", ch, -1, -1, 1));
         MTRY(make_convT(c, S, w, b, u, (k - u) / 2, S.ups[i]));
         int st = 1;
         for (int j = i + 1; j < nup; ++j) st *= g.upsample_rates[j];
@@ -552,6 +595,7 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
         S.noise_pad.push_back(st == 1 ? 0 : (kn - st) / 2);
         GET("dec.noise_convs." + si + ".weight", w);
         GET("dec.noise_convs." + si + ".bias", b);
+        MTRY(expect(w, "dec.noise_convs." + si + ".weight", ch, 1, kn));
         MTRY(make_conv(c, S, w, &b, S.noise[i]));
         S.res[i].resize(g.n_resblocks);
         for (int j = 0; j < g.n_resblocks; ++j) {
@@ -562,15 +606,18 @@ extern "C" int rvc_load_synth(rvc_ctx* c, const rvc_param* params, int n, const 
                 const std::string sm = std::to_string(m);
                 GET(rb + "convs1." + sm + ".weight", w);
                 GET(rb + "convs1." + sm + ".bias", b);
+                MTRY(expect(w, rb + "convs1." + sm + ".weight", ch, ch, g.resblock_kernel_sizes[j]));
                 MTRY(make_conv(c, S, w, &b, P.c1));
                 GET(rb + "convs2." + sm + ".weight", w2);
                 GET(rb + "convs2." + sm + ".bias", b2);
+                MTRY(expect(w2, rb + "convs2." + sm + ".weight", ch, ch, g.resblock_kernel_sizes[j]));
                 MTRY(make_conv(c, S, w2, &b2, P.c2));
                 S.res[i][j].push_back(P);
             }
         }
     }
     GET("dec.conv_post.weight", w);
+    MTRY(expect(w, "dec.conv_post.weight", 1, g.upsample_initial_channel >> nup, 7));
     MTRY(make_conv(c, S, w, nullptr, S.conv_post));
 #undef GET
     MHIP(hipDeviceSynchronize());

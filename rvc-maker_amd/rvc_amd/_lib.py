@@ -127,6 +127,7 @@ SIGNATURES = {
                         c_void_p],
     "rvc_stft_frames": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_int, c_void_p],
     "rvc_spec_mag": [c_void_p, c_void_p, c_int64, c_int64, c_void_p],
+    "rvc_stft_mag": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_int, c_int64, c_int64, c_void_p],
     "rvc_mel_image": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float, c_void_p],
     "rvc_avgpool2": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_interleave4": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
@@ -143,6 +144,8 @@ SIGNATURES = {
     "rvc_ivf_coarse_ws_bytes": [c_int64, c_int64],
     "rvc_ivf_search": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                        c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "rvc_ivf_search_ex": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                       c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "rvc_ivf_blend": [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int, c_void_p, c_int64,
                       c_double, c_void_p, c_int64, c_int64, c_void_p],
     "rvc_crepe_frames": [c_void_p, c_int64, c_int, c_int64, c_int64, c_void_p, c_void_p],
@@ -178,6 +181,7 @@ SIGNATURES = {
     "rvc_load_crepe": [c_void_p, POINTER(Param), c_int],
     "rvc_vc_out_len": [c_void_p, c_int64, POINTER(VcArgs)],
     "rvc_load_index": [c_void_p, POINTER(IvfIndex)],
+    "rvc_device_bytes_in_use": [],
     "rvc_vc_convert": [c_void_p, c_void_p, c_int64, POINTER(VcArgs), c_void_p, c_void_p],
     "rvc_crepe_f0": [c_void_p, c_void_p, c_int64, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p],
@@ -191,7 +195,7 @@ _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint,
              "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64,
              "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64,
-             "rvc_vc_out_len": c_int64}
+             "rvc_vc_out_len": c_int64, "rvc_device_bytes_in_use": c_int64}
 
 _lib = None
 

@@ -20,7 +20,7 @@ import torch
 from . import _lib
 from ._lib import check
 
-PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3, "fp32x6": 6, "f16x3": 16}
+PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3, "fp32x6": 6, "fp32sa": 7, "f16x3": 16}
 
 
 def _params(W: dict):

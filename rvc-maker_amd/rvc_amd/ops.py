@@ -58,11 +58,13 @@ X6 = os.environ.get("RVC_AMD_X6", "1") != "0"
 #   "fp32"   f32-equivalent (the default; BASELINE configs 1-2, 4): "fp32x6" everywhere except the convs where
 #            "f16x3" measured faster (conv_passes, rb_passes; F16_MIX; RVC_AMD_F16MIX=0 turns it off)
 #   "fp32x6" 6 bf16 passes, f32-accurate products (~2^-22 relative per product)
+#   "fp32sa" "fp32x6" with the 5 correction passes accumulated apart from hH (RMVPE, whose f0 is a per-frame
+#            decision: the large sum is rounded once per 32 products, scripts/conv_prec.py)
 #   "f16x3"  3 fp16 passes over power-of-2-scaled 22-bit operands (~2^-20 relative per product)
 #   "bf16x3" 3 bf16 passes, 16-bit operand mantissas (~2^-16 relative per product)
 #   "bf16"   1 pass, bf16 operands (BASELINE configs 3 and 5)
 F16X3 = 16  # RVC_ARITH_F16X3
-PASSES = {"fp32": 6, "fp32x6": 6, "f16x3": F16X3, "bf16x3": 3, "bf16": 1}
+PASSES = {"fp32": 6, "fp32x6": 6, "fp32sa": 7, "f16x3": F16X3, "bf16x3": 3, "bf16": 1}
 F16_MIX = os.environ.get("RVC_AMD_F16MIX", "1") != "0"
 
 
@@ -186,6 +188,7 @@ class ConvT:
 
 LAST_CONV_FLOPS = 0.0
 LAST_CONV_ENGINE = 0  # 0 = f32 MFMA engine, 1 = split-bf16 (x6) engine
+LAST_CONV_PASSES = 0  # the split-operand launch's pass set (PASSES values; F16X3 = split-fp16), 0 = f32 engine
 _WS = {}
 _WS_PRIVATE = None  # a workspace store owned by a captured graph (private_workspaces)
 
@@ -219,7 +222,8 @@ def _workspace(device, nbytes, kind="conv"):
     if buf is None or buf.numel() * 4 < nbytes:
         if buf is not None and _WS_PRIVATE is not None:
             pool.setdefault("_retired", []).append(buf)  # a captured node may still point at it
-        buf = torch.empty((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
+        # zeroed: the conv engine keeps its split-K arrival counters at the head and expects them zero
+        buf = torch.zeros((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
         pool[key] = buf
     return buf
 
@@ -244,7 +248,7 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
 
     ``flops`` is the launch's ALGORITHMIC FLOP count for roofline accounting (recorded in
     LAST_CONV_FLOPS); the default is 2*B*Co*(Ci/g)*K*(valid outputs)."""
-    global LAST_CONV_FLOPS, LAST_CONV_ENGINE
+    global LAST_CONV_FLOPS, LAST_CONV_ENGINE, LAST_CONV_PASSES
     if B is None:
         B, Cx, Lx = _shape3(x)
         if Lin is None:
@@ -300,6 +304,7 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
         raise RuntimeError(f"rvc_amd: conv1d plan failed: {lib.rvc_last_error().decode()}")
     ws = _workspace(out.device, need) if need else None
     LAST_CONV_ENGINE = lib.rvc_conv1d_engine(ctypes.byref(a))
+    LAST_CONV_PASSES = a.wx_passes if LAST_CONV_ENGINE == 1 else 0
     check(lib.rvc_conv1d(ctypes.byref(a), _p(ws), need, _stream()), "conv1d")
     return out
 
@@ -452,6 +457,21 @@ def stft_frames(x, win, out, N, F, nfft, hop):
     return out
 
 
+def stft_mag(x, win, mag, N, F, nfft, hop):
+    """|STFT| in f64, rounded once: x [N] or [B][N] -> mag [nfft/2+1][F] or [B][nfft/2+1][F]."""
+    B = x.shape[0] if x.dim() == 2 else 1
+    K = nfft // 2 + 1
+    if (x.shape[-1] < N or win.numel() < nfft or mag.numel() < B * K * F or mag.shape[-1] != F
+            or (B > 1 and (mag.dim() != 3 or mag.shape[0] != B))):
+        raise ValueError("stft_mag: size mismatch")
+    if x.stride(-1) != 1 or mag.stride(-1) != 1:
+        raise ValueError("stft_mag: x / mag rows must be contiguous")
+    xs = x.stride(0) if B > 1 else 0
+    ms = mag.stride(0) if B > 1 else 0
+    check(_lib.load().rvc_stft_mag(_p(x), _p(win), _p(mag), B, N, F, nfft, hop, xs, ms, _stream()), "stft_mag")
+    return mag
+
+
 def spec_mag(spec, mag, K, F):
     if spec.numel() < 2 * K * F or mag.numel() < K * F:
         raise ValueError("spec_mag: size mismatch")
@@ -574,17 +594,20 @@ class FiltFilt:
         return out, out64
 
 
-def ivf_search(q, nq, d, cs, qs, centT, nlist, nprobe, list_off, codes, ids, k, D, I, probes):
+IVF_FAISS, IVF_EXACT = 0, 1  # RVC_IVF_FAISS (faiss's own f32 arithmetic, the default) / RVC_IVF_EXACT (f64)
+
+
+def ivf_search(q, nq, d, cs, qs, centT, nlist, nprobe, list_off, codes, ids, k, D, I, probes, arithmetic=IVF_FAISS):
     """FAISS IVF-Flat search (ivf.hip): see include/rvc_amd.h."""
     if D.numel() < nq * k or I.numel() < nq * k or probes.numel() < nq * nprobe or centT.numel() < d * nlist:
         raise ValueError("ivf_search: output / index buffers too small")
-    if q.numel() < (d - 1) * cs + (nq - 1) * qs + 1:
+    if _room(q) < (d - 1) * cs + (nq - 1) * qs + 1:
         raise ValueError("ivf_search: query buffer too small")
     lib = _lib.load()
     need = lib.rvc_ivf_coarse_ws_bytes(nq, nlist)
     ws = _workspace(q.device, need, "ivf")
-    check(lib.rvc_ivf_search(_p(q), nq, d, cs, qs, _p(centT), nlist, nprobe, _p(list_off), _p(codes), _p(ids), k,
-                             _p(ws), need, _p(probes), _p(D), _p(I), _stream()), "ivf_search")
+    check(lib.rvc_ivf_search_ex(_p(q), nq, d, cs, qs, _p(centT), nlist, nprobe, _p(list_off), _p(codes), _p(ids), k,
+                                _p(ws), need, _p(probes), _p(D), _p(I), arithmetic, _stream()), "ivf_search")
 
 
 def ivf_blend(feats, nq, d, fcs, fqs, D, I, k, big, ntotal, index_rate, out, ocs, oqs):

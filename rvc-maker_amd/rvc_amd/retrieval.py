@@ -35,8 +35,9 @@ class IVFFlatDevice:
     def from_file(cls, path, device="cuda"):
         return cls(read_index(path), device)
 
-    def search_cf(self, feats_cf, k=8, nprobe=None):
-        """feats_cf [d][T] device f32 (channels-first) -> (D [T][k] f32, I [T][k] int64)."""
+    def search_cf(self, feats_cf, k=8, nprobe=None, arithmetic="faiss"):
+        """feats_cf [d][T] device f32 (channels-first) -> (D [T][k] f32, I [T][k] int64).  ``arithmetic``:
+        "faiss" = faiss's own f32 evaluation (the default; include/rvc_amd.h), "exact" = f64 (diagnostic)."""
         d, T = feats_cf.shape
         if d != self.d:
             raise ValueError(f"ivf: index dim {self.d} != features {d}")
@@ -45,7 +46,7 @@ class IVFFlatDevice:
         I = torch.empty(T, k, dtype=torch.int64, device=feats_cf.device)
         probes = torch.empty(T, nprobe, dtype=torch.int64, device=feats_cf.device)
         ops.ivf_search(feats_cf, T, d, T, 1, self.centT, self.nlist, nprobe, self.list_off, self.codes, self.ids,
-                       k, D, I, probes)
+                       k, D, I, probes, {"faiss": ops.IVF_FAISS, "exact": ops.IVF_EXACT}[arithmetic])
         return D, I
 
     def blend_cf(self, feats_cf, D, I, index_rate):

@@ -5,8 +5,8 @@ Loaded once from an ``E2E(4, 1, (2, 2))`` state dict (the reference reloads ``rm
 every ``pipeline`` call, convert.py:251 -- this build keeps it resident).  BatchNorm is folded
 into the convolutions on the host at load.  On the device:
 
-  mel       stft_frames (reflect centre, Hann) -> DFT as a K=1 MFMA GEMM (1024 -> 2x513)
-            -> spec_mag -> mel GEMM (513 -> 128) with log(clamp 1e-5) fused
+  mel       stft_mag (reflect centre, Hann, f64 FFT in LDS, |X| rounded to f32 once)
+            -> mel GEMM (513 -> 128) with log(clamp 1e-5) fused
   U-Net     images kept zero-bordered [C][H+2][W+2]; every 3x3 / 1x1 conv is the MFMA
             implicit-GEMM engine in 2-D mode (tap offsets + border masking), ReLU and the
             residual add fused; encoder skips are written straight into the decoder's concat
@@ -17,6 +17,7 @@ into the convolutions on the host at load.  On the device:
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -26,6 +27,15 @@ from .ops import ACT_LOGCLAMP, ACT_RELU, ACT_SIGMOID, pack_km
 
 N_MELS, N_CLASS, NFFT, HOP = 128, 360, 1024, 160
 EPS = 1e-5
+
+
+def _at_precision(fn):
+    """Run a RMVPEAMD stage at the model's own arithmetic (self.precision), whoever calls it."""
+    def wrapped(self, *a, **k):
+        with ops.precision(self.precision or ops.get_precision()):
+            return fn(self, *a, **k)
+    wrapped.__name__, wrapped.__doc__ = fn.__name__, fn.__doc__
+    return wrapped
 
 
 def _fold_bn(sd, name):
@@ -110,11 +120,6 @@ class RMVPEAMD:
         self.nb = n_blocks
         self.mel_basis = torch.from_numpy(melbasis.mel_filterbank(16000, NFFT, N_MELS, 30, 8000))
         self.window = torch.hann_window(NFFT).to(dev)  # float32 periodic, as RMVPE.py:166
-        n = np.arange(NFFT)
-        k = np.arange(NFFT // 2 + 1)
-        ang = 2 * np.pi * np.outer(k, n) / NFFT
-        dft = np.concatenate([np.cos(ang), -np.sin(ang)], 0)  # [1026, 1024]
-        self.dft = ops.Conv(torch.from_numpy(dft).float().unsqueeze(-1), None, device=dev)
         self.mel = ops.Conv(self.mel_basis.unsqueeze(-1), None, device=dev)
         s, t = _fold_bn(sd, "unet.encoder.bn")
         self.in_scale, self.in_shift = float(s[0]), float(t[0])
@@ -149,41 +154,33 @@ class RMVPEAMD:
         self._grans = {}
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         # The f0 is a per-frame decision (argmax over 360 bins, voicing threshold): RMVPE's convs run at the
-        # f32-accurate 6-pass arithmetic whatever ops.precision says (None = follow it).  At 3 passes the
-        # salience moves by 1.5e-2 and at 1 pass by 0.24 on the synthetic weights, which flips decisions;
-        # RMVPE is 5 % of a 48k clip's FLOPs and runs beside ContentVec (tests/test_gpu_configs.py).
-        self.precision = "fp32"
+        # 6-pass split-bf16 arithmetic with split accumulators ("fp32sa") whatever ops.precision says (None =
+        # follow it).  With one accumulator the U-Net's error against an f64 evaluation was 1.5x the reference's own
+        # f32 error (scripts/rmvpe_prec.py); at 3 passes the salience moved by 1.5e-2 and at 1 pass by 0.24 on the
+        # synthetic weights, flipping decisions.  RMVPE is 5 % of a 48k clip's FLOPs and runs beside ContentVec.
+        self.precision = os.environ.get("RVC_RMVPE_PRECISION", "fp32sa")
 
     @classmethod
     def from_file(cls, path, device="cuda"):
         return cls(torch.load(path, map_location="cpu", weights_only=True), device)
 
     # ------------------------------------------------------------------ pieces
+    @_at_precision
     def mel_spectrogram(self, audio: torch.Tensor) -> torch.Tensor:
         """MelSpectrogram.forward (RMVPE.py:162-181): audio [N] f32 -> log-mel [128][F]."""
         N = audio.numel()
         F = 1 + N // HOP
-        dev = audio.device
-        frames = torch.empty(NFFT, F, device=dev)
-        ops.stft_frames(audio, self.window, frames, N, F, NFFT, HOP)
-        # algorithmic count of the reference's FFT-based stft (5 N log2 N / 2 per real frame)
-        spec = self.dft(frames, flops=2.5 * NFFT * math.log2(NFFT) * F)
-        mag = torch.empty(NFFT // 2 + 1, F, device=dev)
-        ops.spec_mag(spec, mag, NFFT // 2 + 1, F)
+        mag = torch.empty(NFFT // 2 + 1, F, device=audio.device)
+        ops.stft_mag(audio, self.window, mag, N, F, NFFT, HOP)
         return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
 
+    @_at_precision
     def mel_spectrogram_batch(self, xb: torch.Tensor) -> torch.Tensor:
         """B equal-length signals [B][N] -> log-mel [B][128][F] (the GEMMs batched, framing per signal)."""
         B, N = xb.shape
         F = 1 + N // HOP
-        dev = xb.device
-        frames = torch.empty(B, NFFT, F, device=dev)
-        for b in range(B):
-            ops.stft_frames(xb[b], self.window, frames[b], N, F, NFFT, HOP)
-        spec = self.dft(frames, flops=2.5 * NFFT * math.log2(NFFT) * F * B)
-        mag = torch.empty(B, NFFT // 2 + 1, F, device=dev)
-        for b in range(B):
-            ops.spec_mag(spec[b], mag[b], NFFT // 2 + 1, F)
+        mag = torch.empty(B, NFFT // 2 + 1, F, device=xb.device)
+        ops.stft_mag(xb, self.window, mag, N, F, NFFT, HOP)
         return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
 
     def _cbr(self, blk, x, H, W, out):
@@ -211,6 +208,7 @@ class RMVPEAMD:
         ops.mel_image(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
         return x, Tp
 
+    @_at_precision
     def unet_seq(self, x: torch.Tensor, H: int) -> torch.Tensor:
         """E2E up to the GRU input (RMVPE.py:143-144, 254): bordered image [1][H+2][130] (H % 32 == 0)
         -> cnn head rows [384][H]."""
@@ -256,6 +254,7 @@ class RMVPEAMD:
             self._grans[key] = g
         return g
 
+    @_at_precision
     def head(self, seq: torch.Tensor) -> torch.Tensor:
         """BiGRU + Linear + Sigmoid (RMVPE.py:254-260, 141): seq [384][Tp] -> salience [360][Tp]."""
         Tp = seq.shape[-1]
@@ -264,6 +263,7 @@ class RMVPEAMD:
         ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran_ws(), self.err, Tp)
         return self.fc(y, out_act=ACT_SIGMOID)
 
+    @_at_precision
     def salience(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
         """mel2hidden + E2E (RMVPE.py:210-215, 143-144): mel [128][F] -> salience [360][Tp] (Tp = F rounded up to 32)."""
         x, Tp = self.mel_image(mel)
@@ -278,6 +278,7 @@ class RMVPEAMD:
         ops.rmvpe_decode(sal, Tp, F, thred, math.pow(2, pitch_shift / 12), f0, coarse, pitchf, post)
         return coarse, pitchf, f0
 
+    @_at_precision
     def salience_batch(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
         """salience for B clips at once: mel [B][128][F] -> [B][360][Tp].  Every conv of the U-Net, the
         W_ih / fc GEMMs and the BiGRU (B recurrences side by side) run batched; the per-image glue

@@ -443,10 +443,147 @@ def gen_denoise(seed):
     print("denoise", {k: v.shape for k, v in out.items()})
 
 
+class InjectNoise:
+    """Replaces torch.randn_like during a reference VC.pipeline run with the draws the GPU parity tests inject
+    (tests/test_gpu_configs.py SeededNoise): per segment s, the z_p draw then the SineGen draw, each
+    torch.randn(shape, generator=manual_seed(salt + 13 s + len(kind))).  The reference's torch.rand draw
+    (SineGen's random initial phase, zeroed at synthesizers.py:95) is left alone."""
+
+    def __init__(self, salt):
+        self.salt, self.n = salt, 0
+        self._rl = torch.randn_like
+
+    def __enter__(self):
+        def rl(t, *a, **k):
+            seg, kind = self.n // 2, ("z", "sine")[self.n % 2]
+            self.n += 1
+            g = torch.Generator().manual_seed(self.salt + 13 * seg + len(kind))
+            return torch.randn(*t.shape, generator=g).to(t.dtype)
+        torch.randn_like = rl
+        return self
+
+    def __exit__(self, *a):
+        torch.randn_like = self._rl
+
+
+def gen_ref_spread(seconds=30.0, seed=201, threads=(8, 7, 6, 5, 4, 3, 2, 1)):
+    """The reference's OWN numerical spread on the headline clip (BASELINE configs[1]: 48k v2, RMVPE, 30 s,
+    the models and input of tests/test_gpu_configs.py::test_cfg2_headline_30s_48k_fp32_vs_oracle): the
+    reference's VC.pipeline (convert.py:388-458) run on CPU at several torch thread counts -- each an equally
+    valid f32 evaluation of the same model -- plus one run whose f0 comes from the reference's RMVPE evaluated
+    in float64 (model.double(), f64 mel), with the parity tests' injected noise so only arithmetic differs.
+    Stored: every run's raw f0 track and salience-derived per-frame statistics, the pairwise waveform RMS
+    spread, and the f64 salience's per-frame decision margins.  The headline parity test bounds the device
+    against this spread."""
+    import main.inference.convert as conv
+    from main.library.predictors import RMVPE as RR
+    ck = synthetic.make_synth_ckpt(48000, "v2", seed=seed)
+    net_g = build_ref_synth(ck)
+    from main.library.architectures import fairseq
+    cpath = os.path.join("assets", "models", "embedders", "contentvec_synth.pt")
+    torch.save(synthetic.make_contentvec_ckpt(seed + 1), cpath)
+    hub = fairseq.load_model(cpath)[0][0].float().eval()
+    rpath = os.path.join("assets", "models", "predictors", "rmvpe.pt")
+    torch.save(synthetic.rmvpe_state_dict(seed + 2), rpath)
+    audio = synthetic.synthetic_audio(seconds, seed=1000)
+    sal_rec = []
+    m2h0 = RR.RMVPE.mel2hidden
+
+    def m2h(self, mel):
+        h = m2h0(self, mel)
+        sal_rec.append(h.squeeze(0).numpy().astype(np.float64))
+        return h
+    RR.RMVPE.mel2hidden = m2h
+
+    def run(f0_override=None):
+        vc = conv.VC(48000, conv.config)
+        f0s = []
+        g0 = vc.get_f0_rmvpe
+
+        def gf(x, *a, **k):
+            f = f0_override.copy() if f0_override is not None else g0(x, *a, **k)
+            f0s.append(np.array(f, dtype=np.float64))
+            return f
+        vc.get_f0_rmvpe = gf
+        with torch.no_grad(), InjectNoise(5):
+            out = vc.pipeline(model=hub, net_g=net_g, sid=0, audio=audio.copy(), pitch=0, f0_method="rmvpe",
+                              file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3, volume_envelope=1,
+                              version="v2", protect=0.33, hop_length=64, f0_autotune=False, f0_autotune_strength=1,
+                              suffix=".pth", embed_suffix=".pt", f0_file=None, f0_onnx=False, pbar=Pbar())
+        assert len(f0s) == 1
+        return np.asarray(out, np.float32), f0s[0]
+
+    names, outs, f0s, sals = [], [], [], []
+    for n in threads:
+        torch.set_num_threads(n)
+        sal_rec.clear()
+        o, f = run()
+        names.append(f"f32_threads{n}")
+        outs.append(o)
+        f0s.append(f)
+        sals.append(sal_rec[0])
+        print(names[-1], o.shape, float(np.sqrt(np.mean(o.astype(np.float64) ** 2))), flush=True)
+    # the reference's RMVPE in float64 on the same filtered, reflect-padded signal (convert.py:403,416,436)
+    torch.set_num_threads(max(threads))
+    r = RR.RMVPE(rpath, is_half=False, device="cpu")
+    a = conv.signal.filtfilt(conv.bh, conv.ah, audio)
+    ap = np.pad(a, (16000, 16000), mode="reflect")
+    torch.set_default_dtype(torch.float64)
+    try:
+        me = RR.MelSpectrogram(False, 128, 16000, 1024, 160, None, 30, 8000).double()
+        with torch.no_grad():
+            mel = me(torch.from_numpy(ap).unsqueeze(0), center=True)
+            nf = mel.shape[-1]
+            mel = torch.nn.functional.pad(mel, (0, 32 * ((nf - 1) // 32 + 1) - nf), mode="reflect")
+            s64 = r.model.double()(mel)[:, :nf].squeeze(0).numpy()
+    finally:
+        torch.set_default_dtype(torch.float32)
+    f64 = r.decode(s64, thred=0.03)
+    o64, _ = run(f0_override=f64)
+    names.append("f64_rmvpe")
+    outs.append(o64)
+    f0s.append(f64)
+    sals.append(s64)
+    print("f64 rmvpe", flush=True)
+    RR.RMVPE.mel2hidden = m2h0
+    k = len(names)
+    wav_rms = np.zeros((k, k))
+    sal_max = np.zeros((k, k))
+    for i in range(k):
+        for j in range(k):
+            wav_rms[i, j] = np.sqrt(np.mean((outs[i].astype(np.float64) - outs[j]) ** 2))
+            sal_max[i, j] = np.abs(sals[i] - sals[j]).max()
+    srt = np.sort(s64, axis=1)
+    margin64 = np.minimum(srt[:, -1] - srt[:, -2], np.abs(srt[:, -1] - 0.03))
+    # per frame: the largest |salience - f64 salience| over the f32 runs, and each run's decisions
+    frame_spread = np.max([np.abs(s - s64).max(1) for s in sals[:-1]], 0)
+    argmax = np.stack([s.argmax(1) for s in sals]).astype(np.int16)
+    voiced = np.stack([s.max(1) > 0.03 for s in sals])
+    # each run's salience at the f64 run's top-2 bins: the two values a frame's f0 decision compares
+    # (argmax: top1 vs top2; voicing: top1 vs 0.03), so the reference's own decision noise per frame
+    top2 = np.argsort(s64, axis=1)[:, -2:][:, ::-1].T.astype(np.int16)  # [2][F]: f64 top-1, top-2 bin
+    fi = np.arange(s64.shape[0])
+    sal_top2 = np.stack([np.stack([s[fi, top2[0]], s[fi, top2[1]]]) for s in sals])  # [runs][2][F] f64
+    np.savez_compressed(os.path.join(OUT, "ref_spread_cfg2.npz"), seed=seed, seconds=seconds,
+                        names=np.array(names), f0=np.stack(f0s), wav_rms=wav_rms, sal_max=sal_max,
+                        out_rms=np.array([np.sqrt(np.mean(o.astype(np.float64) ** 2)) for o in outs]),
+                        margin64=margin64.astype(np.float32), frame_spread=frame_spread.astype(np.float32),
+                        argmax=argmax, voiced=voiced, sal64_max=srt[:, -1].astype(np.float32), top2=top2,
+                        sal_top2=sal_top2)
+    print("names", names)
+    print("wav rms spread\n", np.array2string(wav_rms, precision=3))
+    print("salience max abs spread\n", np.array2string(sal_max, precision=3))
+    flips = [np.flatnonzero((argmax[i] != argmax[-1]) | (voiced[i] != voiced[-1])).tolist() for i in range(k - 1)]
+    print("decision flips vs f64:", flips)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     setup_harness()
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "spread":
+        gen_ref_spread()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "crepe":
         gen_crepe(6.0, seed=81)
         return

@@ -80,3 +80,39 @@ def test_blend_matches_reference_formula():
     w /= w.sum(1, keepdims=True)
     ref = 0.75 * (big[I] * w[..., None]).sum(1) + 0.25 * feats
     np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_faiss_arithmetic_restatement():
+    """oracle/ivf.py's faiss-f32 arithmetic: the AVX2-structured f32 sums equal an explicit loop in that order,
+    the BLAS coarse decomposition (nq >= 20) clamps the roundoff of an exact hit at 0, the direct path (nq < 20)
+    gives 0 exactly, and both stay within f32 rounding of the exact (f64) distances."""
+    rng = np.random.default_rng(5)
+    for d in (768, 13):
+        x, y = rng.standard_normal(d).astype(np.float32), rng.standard_normal(d).astype(np.float32)
+        t = (x - y) * (x - y)
+        lanes = [np.float32(0)] * 8
+        for j in range(d // 8 * 8):
+            lanes[j % 8] = np.float32(lanes[j % 8] + t[j])
+        s4 = [np.float32(lanes[4 + i] + lanes[i]) for i in range(4)]
+        rest = list(t[d // 8 * 8:]) + [np.float32(0)] * 8
+        if d % 8 >= 4:
+            s4 = [np.float32(s4[i] + rest[i]) for i in range(4)]
+            rest = rest[4:]
+        if d % 4:
+            s4 = [np.float32(s4[i] + rest[i]) for i in range(4)]
+        want = np.float32(np.float32(s4[0] + s4[1]) + np.float32(s4[2] + s4[3]))
+        assert ivf.fvec_l2sqr(x[None], y[None])[0] == want
+    c = rng.standard_normal((30, 64)).astype(np.float32) * 3
+    q = np.concatenate([c[:25], rng.standard_normal((5, 64)).astype(np.float32)])
+    blas = ivf.coarse_distances(q, c)                 # 30 queries: the BLAS decomposition
+    direct = ivf.coarse_distances(q[:10], c)          # 10 queries: fvec_L2sqr
+    exact = ivf.coarse_distances(q, c, "exact")
+    assert (blas >= 0).all() and (direct[np.arange(10), np.arange(10)] == 0).all()
+    np.testing.assert_allclose(blas, exact, rtol=2e-5, atol=2e-3)
+    np.testing.assert_allclose(direct, exact[:10], rtol=1e-5, atol=1e-5)
+    idx, _ = make_index(n=800, d=32, nlist=12)
+    qq = rng.standard_normal((40, 32)).astype(np.float32)
+    Df, If = ivf.search(idx, qq, k=8)
+    De, Ie = ivf.search(idx, qq, k=8, arithmetic="exact")
+    assert (If == Ie).mean() > 0.99  # near-ties within f32 rounding may order differently
+    np.testing.assert_allclose(Df, De, rtol=1e-5, atol=1e-5)

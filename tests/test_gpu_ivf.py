@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 import torch
 
+import f0check
 from oracle import ivf as oivf
 from rvc_amd.faiss_index import IVFFlatIndex
 
@@ -21,18 +22,25 @@ def make(n, d, nlist, nprobe=1, seed=0, dups=0):
     return IVFFlatIndex.build(cent, xb, nprobe=nprobe), xb
 
 
+@pytest.mark.parametrize("arithmetic", ["faiss", "exact"])
 @pytest.mark.parametrize("n,d,nlist,nprobe,nq", [(6000, 768, 153, 1, 400), (3000, 256, 60, 3, 300),
-                                                 (500, 768, 64, 1, 200)])
-def test_search_matches_oracle(n, d, nlist, nprobe, nq):
+                                                 (500, 768, 64, 1, 200), (800, 256, 16, 2, 12)])
+def test_search_matches_oracle(n, d, nlist, nprobe, nq, arithmetic):
+    """Identical neighbour lists and distances, in both arithmetics (the last case has nq < 20: faiss's direct
+    coarse distances instead of the BLAS decomposition)."""
     from rvc_amd.retrieval import IVFFlatDevice
     idx, xb = make(n, d, nlist, nprobe, dups=8)
     rng = np.random.default_rng(7)
-    q = np.concatenate([xb[:20] + 0.0, rng.standard_normal((nq - 20, d)).astype(np.float32)])  # exact hits too
+    nh = min(20, nq // 2)
+    q = np.concatenate([xb[:nh] + 0.0, rng.standard_normal((nq - nh, d)).astype(np.float32)])  # exact hits too
     dev = IVFFlatDevice(idx, DEV)
-    Dg, Ig = dev.search_cf(torch.from_numpy(np.ascontiguousarray(q.T)).to(DEV), k=8)
-    Do, Io = oivf.search(idx, q, k=8)
+    Dg, Ig = dev.search_cf(torch.from_numpy(np.ascontiguousarray(q.T)).to(DEV), k=8, arithmetic=arithmetic)
+    Do, Io = oivf.search(idx, q, k=8, arithmetic=arithmetic)
     np.testing.assert_array_equal(Ig.cpu().numpy(), Io)
-    np.testing.assert_allclose(Dg.cpu().numpy(), Do, rtol=1e-6, atol=1e-6)
+    if arithmetic == "faiss":  # the same f32 operations in the same order: bit-identical distances
+        np.testing.assert_array_equal(Dg.cpu().numpy(), Do)
+    else:
+        np.testing.assert_allclose(Dg.cpu().numpy(), Do, rtol=1e-6, atol=1e-6)
 
 
 def test_blend_matches_oracle():
@@ -82,10 +90,9 @@ def test_pipeline_with_index_vs_oracle(tmp_path):
                       ".pth", ".pt")
     ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
     torch.set_num_threads(16)
-    ref = opl.pipeline(ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1)), osy.load_weights(ck["weight"]),
-                       orm.load_weights(synthetic.rmvpe_state_dict(seed + 2)),
-                       torch.from_numpy(melbasis.mel_filterbank()), ck["config"], 0, audio, 0.0, version, 0.33, noise,
-                       index=idx, index_rate=0.75)
-    assert out.shape == ref.shape
-    err = float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2)))
-    assert err < 1e-4, err
+    Wc, Ws = ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1)), osy.load_weights(ck["weight"])
+    Wr = orm.load_weights(synthetic.rmvpe_state_dict(seed + 2))
+    mb = torch.from_numpy(melbasis.mel_filterbank())
+    # f0 decisions vs the exact model (tests/f0check.py), then the waveform within 1e-4 RMS of the oracle
+    f0check.assert_pipeline(vc, out, synthetic.rmvpe_state_dict(seed + 2), audio, lambda f0: opl.pipeline(
+        Wc, Ws, Wr, mb, ck["config"], 0, audio, 0.0, version, 0.33, noise, index=idx, index_rate=0.75, f0_track=f0))

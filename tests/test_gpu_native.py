@@ -297,3 +297,43 @@ def test_native_vc_convert_with_index_equals_pipeline_device():
     torch.cuda.synchronize()
     assert torch.equal(got, ref), rms(got, ref)
     assert not torch.equal(got, plain)
+
+
+def test_load_index_validates_and_replaces():
+    """rvc_load_index rejects a malformed index on the host (a load error, not a device read out of bounds
+    later) and frees the previous index's device arrays when it replaces one: device memory stays flat
+    over repeated reloads of a ~60 MB index."""
+    import ctypes
+    from rvc_amd import _lib
+    from rvc_amd.native import _Ctx
+    lib = _lib.load()
+    ctx = _Ctx(DEV)
+    rng = np.random.default_rng(0)
+    d, nlist, n = 768, 64, 20000
+    cent = rng.standard_normal((nlist, d)).astype(np.float32)
+    codes = rng.standard_normal((n, d)).astype(np.float32)
+    off = np.linspace(0, n, nlist + 1).astype(np.int64)
+    ids = np.arange(n, dtype=np.int64)
+
+    def load(cent=cent, off=off, codes=codes, ids=ids, big=codes, d=d, nlist=nlist, ntotal=n, nprobe=1):
+        x = _lib.IvfIndex()
+        x.d, x.nlist, x.ntotal, x.nprobe = d, nlist, ntotal, nprobe
+        keep = [np.ascontiguousarray(a) for a in (cent, off, codes, ids, big)]
+        x.centroids, x.list_off, x.codes, x.ids, x.big = (ctypes.c_void_p(a.ctypes.data) for a in keep)
+        return lib.rvc_load_index(ctx.ctx, ctypes.byref(x))
+
+    bad_off = off.copy()
+    bad_off[5] = bad_off[7]  # decreasing at list 5 -> 6
+    bad_ids = ids.copy()
+    bad_ids[123] = n
+    for kw in (dict(off=bad_off), dict(ids=bad_ids), dict(d=767), dict(ntotal=0), dict(d=2048)):
+        assert load(**kw) != 0, kw
+        assert lib.rvc_last_error()
+    assert load() == 0
+    torch.cuda.synchronize()
+    base = lib.rvc_device_bytes_in_use()
+    for _ in range(6):
+        assert load() == 0
+    torch.cuda.synchronize()
+    grown = lib.rvc_device_bytes_in_use() - base
+    assert grown < 16 << 20, grown  # one index is ~124 MB (codes + big): a leak would grow by 6x that

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 import torch
 
+import f0check
 from rvc_amd import synthetic
 
 pytestmark = pytest.mark.gpu
@@ -86,12 +87,12 @@ def test_long_input_segments_vs_oracle():
                       ".pt")
     ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
     torch.set_num_threads(16)
-    ref = opl.pipeline(ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1)), osy.load_weights(ck["weight"]),
-                       orm.load_weights(synthetic.rmvpe_state_dict(seed + 2)),
-                       torch.from_numpy(melbasis.mel_filterbank()), ck["config"], 0, audio, 0.0, version, 0.33, noise)
-    assert out.shape == ref.shape
-    err = float(np.sqrt(np.mean((out.astype(np.float64) - ref) ** 2)))
-    assert err < 1e-4, err
+    Wc, Ws = ocv.load_weights(synthetic.make_contentvec_ckpt(seed + 1)), osy.load_weights(ck["weight"])
+    Wr = orm.load_weights(synthetic.rmvpe_state_dict(seed + 2))
+    mb = torch.from_numpy(melbasis.mel_filterbank())
+    # f0 decisions vs the exact model (tests/f0check.py), then the waveform within 1e-4 RMS of the oracle
+    f0check.assert_pipeline(vc, out, synthetic.rmvpe_state_dict(seed + 2), audio, lambda f0: opl.pipeline(
+        Wc, Ws, Wr, mb, ck["config"], 0, audio, 0.0, version, 0.33, noise, f0_track=f0))
 
 
 def test_change_rms_matches_reference(golden):

@@ -156,3 +156,26 @@ def test_crepe_oracle_matches_reference_golden(golden):
     np.testing.assert_allclose(tr["probs"], g["probs"], rtol=0, atol=2e-6)
     assert f0.shape == g["f0"].shape
     np.testing.assert_allclose(f0, g["f0"], rtol=1e-5, atol=1e-3)
+
+
+def test_rmvpe_f64_matches_reference_f64_and_spread_fixture():
+    """The oracle's RMVPE evaluated in float64 (the "exact model" tests/f0check.py measures every f32 evaluation
+    against) reproduces the REFERENCE's own f64 evaluation on the headline clip (tests/golden/ref_spread_cfg2.npz,
+    make_golden.py spread: its RMVPE model.double() on the same filtered input) at the f64 run's top-2 bins,
+    and the fixture's statistics are those the GPU tests read."""
+    import f0check
+    z = np.load(f0check.GOLDEN)
+    ref = f0check.reference_noise()
+    audio = synthetic.synthetic_audio(float(z["seconds"]), seed=1000)
+    torch.set_num_threads(8)
+    s64 = f0check.oracle_salience(synthetic.rmvpe_state_dict(int(z["seed"]) + 2), audio, torch.float64)
+    top2, st = z["top2"].astype(np.int64), z["sal_top2"]
+    fi = np.arange(s64.shape[0])
+    assert np.array_equal(np.argsort(s64, 1)[:, -1], top2[0])  # same f64 argmax on every frame
+    # the reference's f64 run builds its Hann window in f64, the oracle upcasts torch's f32 window (RMVPE.py:166)
+    assert np.abs(s64[fi, top2[0]] - st[-1, 0]).max() < 1e-6
+    assert np.abs(s64[fi, top2[1]] - st[-1, 1]).max() < 1e-6
+    # the reference's f32 runs: decision errors of 1e-4 order, no decision different from f64 on this clip
+    assert 1e-5 < ref["decision_noise_max"] < 1e-3 and ref["decision_noise_rms"] < 2e-5
+    assert not (z["argmax"][:-1] != z["argmax"][-1]).any() and not (z["voiced"][:-1] != z["voiced"][-1]).any()
+    assert ref["wav_spread"] < 1e-4
