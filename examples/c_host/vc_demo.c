@@ -1,7 +1,8 @@
 /*
- * A plain-C host of the whole VC.pipeline segment (convert.py:388-458) through the model-level ABI: ContentVec,
- * RMVPE and the voice model loaded from safetensors exports of their checkpoints (rvc_amd/native.py:
- * export_safetensors), one rvc_vc_convert call on a 16 kHz clip, the waveform at tgt_sr written out.
+ * A plain-C host of the whole VC.pipeline (convert.py:388-458) through the model-level ABI: ContentVec, RMVPE and
+ * the voice model loaded from safetensors exports of their checkpoints (rvc_amd/native.py: export_safetensors),
+ * one rvc_vc_convert_ex call on a 16 kHz clip of any length (inputs over 41 s are segmented at quiet points by
+ * the library), the waveform at tgt_sr written out.
  *
  *   vc_demo hubert.safetensors rmvpe.safetensors model.safetensors audio16k.f32 out.f32 [pitch protect seed]
  *
@@ -61,15 +62,16 @@ int main(int argc, char** argv) {
     for (int i = 0; i < syn.n; ++i)
         if (!strcmp(syn.params[i].name, "enc_p.emb_phone.weight"))
             va.version = syn.params[i].shape[1] == hc.encoder_embed_dim ? 2 : 1;
-    const int64_t n_out = rvc_vc_out_len(ctx, N, &va);
-    if (n_out <= 0) DIE("rvc_vc_out_len: %s", rvc_last_error());
+    const int64_t n_cap = rvc_vc_out_len(ctx, N, &va); /* exact for one segment, an upper bound beyond 41 s */
+    if (n_cap <= 0) DIE("rvc_vc_out_len: %s", rvc_last_error());
     void *d_audio, *d_out;
     HIPOK(hipMalloc(&d_audio, (size_t)N * 4));
-    HIPOK(hipMalloc(&d_out, (size_t)n_out * 4));
+    HIPOK(hipMalloc(&d_out, (size_t)n_cap * 4));
     HIPOK(hipMemcpy(d_audio, audio, (size_t)N * 4, hipMemcpyHostToDevice));
     hipStream_t s;
     HIPOK(hipStreamCreate(&s));
-    RVCOK(rvc_vc_convert(ctx, (const float*)d_audio, N, &va, (float*)d_out, (rvc_stream_t)s));
+    int64_t n_out = 0;
+    RVCOK(rvc_vc_convert_ex(ctx, (const float*)d_audio, N, &va, NULL, (float*)d_out, n_cap, &n_out, (rvc_stream_t)s));
     HIPOK(hipStreamSynchronize(s));
     RVCOK(rvc_rmvpe_check(ctx));
     float* out = (float*)malloc((size_t)n_out * 4);

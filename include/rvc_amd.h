@@ -100,10 +100,8 @@ typedef struct rvc_conv1d_args {
 } rvc_conv1d_args;
 
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned
- * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args).  Its first
- * 64 KB hold the split blocks' arrival counters: the workspace must be ZERO when first used, and every
- * completed launch leaves them zero again (the partial tiles are reduced inside the launch).  Launches that
- * may run concurrently need separate workspaces. */
+ * device workspace of rvc_conv1d_workspace_bytes(a) bytes (0 when not split; -1 on bad args).  Launches
+ * that may run concurrently need separate workspaces. */
 int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a);
 /* Which engine a call would run on: 0 = f32 MFMA, 1 = split-bf16 (x6); -1 on bad args. */
 int rvc_conv1d_engine(const rvc_conv1d_args* a);
@@ -127,7 +125,8 @@ int rvc_conv1d_pack_f16(const float* w_km, int64_t nphase, int64_t Ci, int K, in
  * (the generator's last two stages, synthesizers.py:157-159), odd K <= 15, (K-1)*dil <= 64.
  * w1x / w2x: the convs' rvc_conv1d_pack_x6 images (nphase 1, Ci = Co = C; nmf1 / nmf2 their wx_nmf);
  * b1 / b2: f32 biases [C]; passes 6 / 3 / 1 as rvc_conv1d_args.wx_passes; slope: the lrelu slope (0.1).
- * x and y must not alias.  Bit-identical to the two rvc_conv1d launches it replaces. */
+ * x and y must not alias.  Bit-identical to the two rvc_conv1d launches it replaces.
+ * B clips (0 = 1): x, y are [B][C][L] (dense); each clip's result is bit-identical to a B = 1 call on it. */
 typedef struct rvc_resblock_args {
     const float* x;
     float* y;
@@ -138,7 +137,7 @@ typedef struct rvc_resblock_args {
     int64_t C, L;
     int K, dil, nmf1, nmf2, passes, accumulate;
     float slope;
-    int _pad0;
+    int B;
 } rvc_resblock_args;
 
 int64_t rvc_resblock_lds_bytes(int64_t C, int K, int dil, int passes);
@@ -270,6 +269,8 @@ int64_t rvc_pm_frames(int64_t n);
 int64_t rvc_pm_work_bytes(int64_t n);
 int rvc_pm_f0(const double* x, int64_t n, const double* window, const double* window_r, void* work,
               int64_t work_bytes, double* f0, rvc_stream_t stream);
+/* rvc_pm_windows: the window [958] and window_r [480] rvc_pm_f0 takes, computed on the HOST (host pointers). */
+int rvc_pm_windows(double* window, double* window_r);
 int rvc_pm_post(const double* f0, int64_t nf, int64_t p_len, double shift, const rvc_f0_post* post,
                 int64_t* coarse, float* pitchf, rvc_stream_t stream);
 
@@ -288,6 +289,15 @@ int rvc_filtfilt_pad(const float* x, int64_t N, const double* b, const double* a
 int rvc_phone_upsample(const float* feats, const float* feats0, const float* pitchf, float* out, int64_t C, int64_t Tf,
                        int64_t T, float protect, rvc_stream_t stream);
 int rvc_peak_normalize(float* x, int64_t n, void* ws, float* scale_out, rvc_stream_t stream);
+/* quiet_points: VC.pipeline's segmentation of inputs over x_max (convert.py:404-412) on the filtered f64 signal
+ *   x [n] (before the t_pad reflect padding): for n + window > t_max, one quiet point per t in
+ *   range(t_center, n, t_center): t - t_query + the first argmin of |moving window-sum| over [t - t_query,
+ *   t + t_query) (the reference's f64 sums, in its order) -> opt_ts int64 [count] (device).  count =
+ *   rvc_quiet_points_count(...) (0 for short inputs); ws: rvc_quiet_points_ws_bytes(...) bytes. */
+int64_t rvc_quiet_points_count(int64_t n, int window, int64_t t_center, int64_t t_max);
+int64_t rvc_quiet_points_ws_bytes(int64_t n, int window, int64_t t_center, int64_t t_query, int64_t t_max);
+int rvc_quiet_points(const double* x, int64_t n, int window, int64_t t_center, int64_t t_query, int64_t t_max,
+                     void* ws, int64_t ws_bytes, int64_t* opt_ts, rvc_stream_t stream);
 /* change_rms (convert.py:150-152, VC.pipeline volume_envelope != 1, convert.py:449):
  *   rms_frames: librosa.feature.rms(y, frame_length = 2*hop, hop_length = hop) (center, zero pad)
  *     of y [n] (f64 when y64 != NULL, else f32 y32) -> out f32 [1 + n / hop] (mean square in f64).
@@ -462,11 +472,19 @@ int rvc_rmvpe_check(rvc_ctx* ctx);
  *   probs (optional, device f32 [360][T]) receives the sigmoid outputs. */
 int rvc_load_crepe(rvc_ctx* ctx, const rvc_param* params, int n);
 
-/* One VC.pipeline segment (convert.py:388-458 for N + 160 <= x_max s, f0_method "rmvpe", volume envelope 1): filtfilt + reflect padding by x_pad s, RMVPE f0 (thred 0.03, pitch shift), ContentVec (v2: layer 12;
- * v1: layer 9 + final_proj), phone upsample + protect, Synthesizer.infer with device noise at `seed`, the
- * x_pad trim at tgt_sr and the peak normalisation.  Needs ContentVec, RMVPE and the synthesizer loaded on the
- * context; audio f32 [N] 16 kHz (device) -> out f32 [rvc_vc_out_len(ctx, N, args)] (device).  Equal to
- * rvc_amd.pipeline.VC.pipeline_device on the same models and seed (tests/test_gpu_native.py). */
+/* VC.pipeline (convert.py:388-458) with inputs and output in device memory: filtfilt + reflect padding by
+ * x_pad s; for inputs over x_max s the quiet-point segmentation (convert.py:404-412, rvc_quiet_points -- the
+ * one device->host read-back: the segment plan needs the points); f0 over the whole padded input on a side
+ * stream (RMVPE thred 0.03, CREPE or pm; pitch shift, then the optional autotune and f0-file override of
+ * get_f0, convert.py:304-323); per segment ContentVec (v2: layer 12; v1: layer 9 + final_proj), the optional
+ * FAISS retrieval (index_rate, rvc_load_index), phone upsample + protect, Synthesizer.infer with device noise
+ * at seed + segment, the x_pad trim at tgt_sr; the optional volume envelope (change_rms, convert.py:449) and
+ * the peak normalisation.  Needs ContentVec, the synthesizer and the chosen f0 model loaded on the context;
+ * audio f32 [N] 16 kHz (device) -> out f32 (device).  Equal to rvc_amd.pipeline.VC.pipeline_device on the
+ * same models, options and seed (tests/test_gpu_native.py).
+ *   rvc_vc_out_len: the output length for inputs of one segment (N + 160 <= x_max s); for longer inputs an
+ *   upper bound (the quiet points decide the exact length).  rvc_vc_convert_ex writes the exact length to
+ *   *out_len; rvc_vc_convert = rvc_vc_convert_ex with default options and one-segment inputs only. */
 typedef struct rvc_vc_args {
     int64_t sid;
     double pitch_shift; /* semitones */
@@ -498,9 +516,27 @@ int rvc_load_index(rvc_ctx* ctx, const rvc_ivf_index* index);
 /* device memory in use on the current device (hipMemGetInfo total - free), for load / reload accounting */
 int64_t rvc_device_bytes_in_use(void);
 
+enum { RVC_F0_RMVPE = 0, RVC_F0_CREPE = 1, RVC_F0_PM = 2 };
+typedef struct rvc_vc_opts {
+    int f0_method;               /* RVC_F0_RMVPE (default), RVC_F0_CREPE (the model of rvc_load_crepe), RVC_F0_PM */
+    int f0_autotune;             /* != 0: Autotune.autotune_f0 at f0_autotune_strength (convert.py:311-313) */
+    double f0_autotune_strength;
+    const float* f0_file;        /* HOST f32 [f0_file_rows][2] "time, f0" rows (read_f0_file, convert.py:425-436) */
+    int64_t f0_file_rows;        /*   0 = none; resampled to 100 frames/s as np.interp (convert.py:316-318) */
+    double volume_envelope;      /* != 1: change_rms of the output against the filtered input (convert.py:449) */
+    const float* crepe_dither;   /* CREPE: device f32 [1 + (N + 2 x_pad 16000) / 160] cents, or NULL = drawn on the
+                                    device from seed (the triangular law of CREPE.py:119) */
+} rvc_vc_opts;
+
 int64_t rvc_vc_out_len(const rvc_ctx* ctx, int64_t N, const rvc_vc_args* args);
+/* the f0-file override values rvc_vc_convert_ex writes from opts.f0_file (host; convert.py:316-318's np.interp of
+ * the rows at 100 frames/s): returns their count n and writes min(n, cap) of them to out (HOST f64); -1 on bad
+ * input.  Exposed for the parity test against the reference's numpy. */
+int64_t rvc_f0_file_resample(const float* rows, int64_t nrows, double* out, int64_t cap);
 int rvc_vc_convert(rvc_ctx* ctx, const float* audio, int64_t N, const rvc_vc_args* args, float* out,
                    rvc_stream_t stream);
+int rvc_vc_convert_ex(rvc_ctx* ctx, const float* audio, int64_t N, const rvc_vc_args* args, const rvc_vc_opts* opts,
+                      float* out, int64_t out_cap, int64_t* out_len, rvc_stream_t stream);
 int rvc_crepe_f0(rvc_ctx* ctx, const float* audio, int64_t N, const float* dither, uint64_t seed, double pitch_shift,
                  const rvc_f0_post* post, float* probs, int64_t* coarse, float* pitchf, rvc_stream_t stream);
 

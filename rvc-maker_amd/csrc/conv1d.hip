@@ -9,8 +9,8 @@
 // Block = 256 threads = 4 wave64s (WM x WN); a wave owns a (16*FM) x (16*FN) tile in FM*FN
 // accumulators.  Chunks are software-pipelined through registers: chunk i+1's global loads are
 // issued before chunk i's MFMAs and written to LDS after them (one LDS buffer, two barriers).
-// Small grids split the k range over blockIdx.z (split-K); partial tiles go to a workspace and the
-// last of a tile's split blocks to finish sums them (in split order) and applies the epilogue.  The epilogue fuses bias, a second bias (speaker
+// Small grids split the k range over blockIdx.z (split-K); partial tiles go to a workspace and
+// conv_splitk_reduce applies the epilogue.  The epilogue fuses bias, a second bias (speaker
 // conditioning), activation, residual add, accumulate, polyphase/strided stores (ConvTranspose)
 // and border masking (2-D mode).
 #include "rvc_common.h"
@@ -22,10 +22,6 @@
 namespace {
 
 constexpr int KCH = 32;     // flattened k per chunk
-// Split-K arrival counters, one per (output tile, compute wave), at the head of the workspace; zero when
-// the workspace is first used, and left zero by every launch (the last arriver resets its counter).
-constexpr int SPLITK_CNT = 16384;
-constexpr int64_t SPLITK_CNT_BYTES = SPLITK_CNT * 4;
 constexpr int NB_MAX = 16;  // staged B elements per thread (rows * span <= 256 * NB_MAX)
 
 struct ConvParams {
@@ -36,8 +32,6 @@ struct ConvParams {
     const float* res;
     float* y;
     float* ws;  // split-K partials [ksplit][B*nphase][Co][ncols]
-    unsigned* cnt;  // split-K arrival counters [tile]
-    int splitk_fused;  // 1: the last-arriving split block reduces; 0: conv_splitk_reduce after the launch
     int64_t B, Ci, Co, Lin, Lout, ncols;
     int64_t x_bstride, y_bstride, res_bstride, w_bstride;
     int K, stride, dil, pad, groups;
@@ -98,24 +92,16 @@ __device__ __forceinline__ void apply_act(floatx4 (&acc)[FM][FN], float slope, f
 }
 
 // Shared epilogue of the conv engines (both produce the MFMA 16x16 C layout: lane l holds column
-// l&15, rows (l>>4)*4 + r of each fragment).  Split-K: each split block stores its partial tile to the
-// workspace and counts in on the tile's arrival counter; the block that arrives last sums the ksplit
-// partials in split order -- the order of the separate reduce pass this replaced, so results are
-// unchanged -- and stores through epilogue_store (cdna_hip_programming.md, in-launch split-K: plain
-// stores, vmcnt drain, barrier, one agent release + relaxed ticket; the last arriver one agent acquire).
-// `lflag` is an LDS word of the kernel's own array, free by the time the epilogue runs.  Otherwise
-// bias, 2nd bias, activation, scale, residual, accumulate and the (strided / polyphase / masked) store
-// are fused here.
+// l&15, rows (l>>4)*4 + r of each fragment).  Split-K partial tiles go to the workspace (summed in split
+// order by conv_splitk_reduce); otherwise bias, 2nd bias, activation, scale, residual, accumulate and the
+// (strided / polyphase / masked) store are fused here.
 template <int FM, int FN, int WM, int WN>
 __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc)[FM][FN], int lane, int wm, int wn,
-                                              int split, int phase, int b, int g, int Cog, int m0g, int64_t n0,
-                                              unsigned* lflag) {
+                                              int split, int phase, int b, int g, int Cog, int m0g, int64_t n0) {
     const int ln = lane & 15;
     const int lr = (lane >> 4) * 4;
     if (p.ksplit > 1) {
-        const int64_t bp = (int64_t)b * p.nphase + phase;
-        const int64_t sstride = p.B * p.nphase * p.Co * p.ncols;
-        float* wsb = p.ws + split * sstride + bp * p.Co * p.ncols;
+        float* wsb = p.ws + (((int64_t)split * p.B * p.nphase + (int64_t)b * p.nphase + phase) * p.Co) * p.ncols;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -126,58 +112,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
                 for (int j = 0; j < FN; ++j) {
                     const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
                     if (mg < Cog && n < p.ncols) wsb[m * p.ncols + n] = acc[i][j][r];
-                }
-            }
-        if (!p.splitk_fused) return;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // every compute wave's partial stores done (loader waves have exited)
-        if (threadIdx.x == 0) {
-            const int64_t tile = ((int64_t)(blockIdx.z / p.ksplit) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned prev = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool last = prev == (unsigned)p.ksplit - 1;
-            if (last) {
-                __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            *lflag = last ? 1u : 0u;
-        }
-        __syncthreads();
-        if (!*lflag) return;
-        // the k loop outermost (one independent load per element per step), each element summed from 0 in
-        // split order, then stored element by element through epilogue_store as the reduce pass did
-        const float* src0 = p.ws + bp * p.Co * p.ncols;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < p.ksplit; ++k) {
-            const float* srck = src0 + k * sstride;
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
-                    const int64_t m = (int64_t)g * Cog + (mg < Cog ? mg : 0);
-#pragma unroll
-                    for (int j = 0; j < FN; ++j) {
-                        const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
-                        acc[i][j][r] += srck[m * p.ncols + (n < p.ncols ? n : 0)];
-                    }
-                }
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int mg = m0g + wm * 16 * FM + i * 16 + lr + r;
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    const int64_t n = n0 + wn * 16 * FN + j * 16 + ln;
-                    if (mg < Cog && n < p.ncols)
-                        epilogue_store(p, acc[i][j][r], b, (int64_t)g * Cog + mg, out_pos(p, n, phase));
                 }
             }
         return;
@@ -424,7 +358,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvParams p) {
         __syncthreads();
     }
 
-    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, g, Cog, m0g, n0, (unsigned*)koff);
+    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, g, Cog, m0g, n0);
 }
 
 // ------------------------------------------------------------------ split-bf16 ("x6") engine
@@ -748,10 +682,13 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 for (int j = 0; j < FN; ++j) acc[i][j][r] *= f;
             }
     }
-    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0, reinterpret_cast<unsigned*>(tmax));
+    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
 }
 
-// The separate split-K reduce (RVC_SPLITK_FUSED=0): sums the ksplit partials in split order, then the epilogue
+// The split-K reduce: sums the ksplit partials in split order, then the epilogue.  (A last-arriving-block
+// reduce inside the conv launch -- plain slab stores, an agent release per split block, an acquire in the
+// last -- measured 11 % slower end to end, 780 vs 880 xRT on one box: each block's release writes back a
+// 64 KB+ partial tile and the last arriver sums up to 16 of them alone; profiles/r3_ab_splitk_fused_rmvpe_sa.txt.)
 __global__ void conv_splitk_reduce(ConvParams p) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = blockIdx.y;
@@ -800,13 +737,6 @@ hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) 
 
 void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y; p.ws = nullptr;
-    p.cnt = nullptr;
-    // in-launch split-K reduce (RVC_SPLITK_FUSED=1): measured 11 % slower end to end than the separate
-    // reduce pass (780 vs 880 xRT, same box): each split block's agent release writes back its 64 KB+ partial
-    // tile and the last arriver sums up to 16 of them alone -- the guide's bound for in-launch combines is a
-    // few tens of KB per tile.  Off by default.
-    static const int fused = getenv("RVC_SPLITK_FUSED") ? atoi(getenv("RVC_SPLITK_FUSED")) : 0;
-    p.splitk_fused = fused;
     p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout;
     p.ncols = a->ncols > 0 ? a->ncols : a->Lout;
     p.x_bstride = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
@@ -836,7 +766,7 @@ void split_k(ConvParams& p, int64_t tiles, int nch) {
     // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU
     static const int target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
     int ks = 1;
-    if (tiles < target && nch >= 4 && tiles * 8 <= SPLITK_CNT) {
+    if (tiles < target && nch >= 4) {
         ks = (int)((target + tiles - 1) / tiles);
         if (ks > 16) ks = 16;
         if (ks > nch / 2) ks = nch / 2;
@@ -1113,7 +1043,7 @@ extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {
     size_t lds;
     if (plan(a, p, cfg, grid, lds) != RVC_OK) return -1;
     if (p.ksplit <= 1) return 0;
-    return SPLITK_CNT_BYTES + (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+    return (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
 }
 
 extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
@@ -1124,11 +1054,10 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     int rc = plan(a, p, cfg, grid, lds);
     if (rc != RVC_OK) return rc;
     if (p.ksplit > 1) {
-        const int64_t need = SPLITK_CNT_BYTES + (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+        const int64_t need = (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
         RVC_CHECK_ARG(ws && ws_bytes >= need, "conv1d: split-K needs %lld B of workspace (got %lld)",
                       (long long)need, (long long)ws_bytes);
-        p.cnt = (unsigned*)ws;
-        p.ws = (float*)((char*)ws + SPLITK_CNT_BYTES);
+        p.ws = (float*)ws;
     }
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
@@ -1150,7 +1079,7 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     else if (cfg.FN == 4) e = launch<2, 4, 2, 2>(p, grid, lds, s);
     else e = launch<2, 2, 2, 2>(p, grid, lds, s);
     RVC_HIP(e);
-    if (p.ksplit > 1 && !p.splitk_fused) {
+    if (p.ksplit > 1) {
         hipLaunchKernelGGL(conv_splitk_reduce, dim3(cdiv(p.ncols, 256), (unsigned)p.Co, (unsigned)(p.B * p.nphase)),
                            dim3(256), 0, s, p);
         RVC_HIP(hipGetLastError());

@@ -437,3 +437,25 @@ extern "C" int rvc_pm_post(const double* f0, int64_t nf, int64_t p_len, double s
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }
+
+// Praat's Hanning window of Sound_to_Pitch_any (nsamp_window 958 at 16 kHz, pitch floor 50 Hz) and its
+// normalised autocorrelation, on the host: window[i] = 0.5 - 0.5 cos((i + 1) 2 pi / 959), window_r[k] =
+// sum_i w[i] w[i + k] / sum_i w[i]^2 for k <= 479 (sequential f64 sums, libm cos, contraction off).  The
+// Python host (rvc_amd/pm.py) and the model-level C ABI (rvc_vc_convert_ex) both take them from here.
+extern "C" int rvc_pm_windows(double* window, double* window_r) {
+#pragma clang fp contract(off)
+    RVC_CHECK_ARG(window && window_r, "pm_windows: null pointer");
+    for (int i = 0; i < PM_NW; ++i) {
+        const double a = (double)(i + 1) * 2.0 * M_PI / (double)(PM_NW + 1);
+        window[i] = 0.5 - 0.5 * cos(a);
+    }
+    double r0 = 0.0;
+    for (int k = 0; k <= PM_BIX; ++k) {
+        double s = 0.0;
+        for (int i = 0; i < PM_NW - k; ++i) s += window[i] * window[i + k];
+        if (k == 0) r0 = s;
+        window_r[k] = s;
+    }
+    for (int k = 0; k <= PM_BIX; ++k) window_r[k] /= r0;
+    return RVC_OK;
+}

@@ -24,13 +24,14 @@
 namespace {
 
 struct RbParams {
-    const float* x;    // [C][L] chain state in (also the residual)
-    float* y;          // [C][L] out (accumulated into when accumulate)
+    const float* x;    // [B][C][L] chain state in (also the residual)
+    float* y;          // [B][C][L] out (accumulated into when accumulate)
     const uint4* w1x;  // c1 split-bf16 image [K][C/32][nmf][3][64]
     const uint4* w2x;  // c2 image
     const float* b1;
     const float* b2;
     int L, K, dil, nmf1, nmf2, accumulate;
+    int B;             // clips: tiles are numbered clip-major, tile g = clip g / ntc, time tile g % ntc
     float slope;
 };
 
@@ -88,7 +89,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     float* Rs = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [C][RSTR]
     float* xmax = Rs + C * RSTR;  // F16: [2 tile parities][4 loader waves] x tile |max|
     float* tmaxs = xmax + 8;      // F16: [8 compute waves] T tile |max|
-    const int ntiles = (L + N - 1) / N;
+    const int ntc = (L + N - 1) / N;  // time tiles per clip
+    const int ntiles = p.B * ntc;
     const int my_n = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
@@ -108,14 +110,16 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             pos = rem - g8 * Wx;
         };
         auto xload = [&](int tile) __attribute__((always_inline)) {
-            const int base = tile * N - H;
+            const int cb = tile / ntc;
+            const int base = (tile - cb * ntc) * N - H;
+            const float* xb = p.x + (int64_t)cb * C * L;
 #pragma unroll
             for (int it = 0; it < G::NI; ++it) {
                 int ch, g8, pos;
                 item(it, ch, g8, pos);
                 int q = base + pos;
                 q = q < 0 ? 0 : (q >= L ? L - 1 : q);
-                const float* src = p.x + (int64_t)(ch * 32 + g8 * 8) * L + q;
+                const float* src = xb + (int64_t)(ch * 32 + g8 * 8) * L + q;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) xr[it][e] = src[(int64_t)e * L];
             }
@@ -135,7 +139,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                                            fmaxf(xmax[par * 4 + 2], xmax[par * 4 + 3]))));
         };
         auto xstore = [&](int tile) __attribute__((always_inline)) {
-            const int base = tile * N - H;
+            const int base = (tile % ntc) * N - H;
 #pragma unroll
             for (int it = 0; it < G::NI; ++it) {
                 if (ltid + 256 * it < nitems) {
@@ -260,6 +264,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
         if (i < S_end) aload(i, abuf[i]);
     float yold[FM][FN][4];
     int n0 = 0;
+    float* yb = p.y;  // the current tile's clip
     // F16: row reciprocal scales of both images (after each image), the x tile's and T tile's reciprocals
     const float* rs1 = reinterpret_cast<const float*>(p.w1x + (int64_t)K * NCH * p.nmf1 * 3 * 64);
     const float* rs2 = reinterpret_cast<const float*>(p.w2x + (int64_t)K * NCH * p.nmf2 * 3 * 64);
@@ -275,7 +280,10 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             if (S < S_end) {
                 const int k = S / SPT, ss = S - k * SPT;
                 if (ss == 0) {  // ---- tile start: X of tile k staged
-                    n0 = ((int)blockIdx.x + k * (int)gridDim.x) * N;
+                    const int g = (int)blockIdx.x + k * (int)gridDim.x;
+                    const int cb = g / ntc;
+                    n0 = (g - cb * ntc) * N;
+                    yb = p.y + (int64_t)cb * C * L;
                     __syncthreads();  // S0(k)
 #pragma unroll
                     for (int i = 0; i < FM; ++i)
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                                 q = q < L ? q : L - 1;
 #pragma unroll
                                 for (int r = 0; r < 4; ++r)
-                                    yold[i][j][r] = p.y[(int64_t)((rg * FM + i) * 16 + 4 * lg + r) * L + q];
+                                    yold[i][j][r] = yb[(int64_t)((rg * FM + i) * 16 + 4 * lg + r) * L + q];
                             }
                     }
                 }
@@ -389,8 +397,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                                 for (int r = 0; r < 4; ++r) {
                                     float v = (F16 ? acc[i][j][r] * (rs2[m0 + r] * t_rs) : acc[i][j][r]) + p.b2[m0 + r];
                                     v = v + Rs[(m0 + r) * RSTR + col];
-                                    if (p.accumulate) v += RB_YREG ? yold[i][j][r] : p.y[(int64_t)(m0 + r) * L + q];
-                                    p.y[(int64_t)(m0 + r) * L + q] = v;
+                                    if (p.accumulate) v += RB_YREG ? yold[i][j][r] : yb[(int64_t)(m0 + r) * L + q];
+                                    yb[(int64_t)(m0 + r) * L + q] = v;
                                 }
                             }
                         }
@@ -420,7 +428,7 @@ int launch_rb(const RbParams& p, hipStream_t s) {
     // workgroups per CU: 1 = persistent; more = shorter tile runs that the dispatcher hands to CUs as they free
     // up (a CU held by a concurrent stream's kernel then delays fewer tiles)
     static const int per_cu = getenv("RVC_RB_PER_CU") ? atoi(getenv("RVC_RB_PER_CU")) : 1;
-    const int ntiles = (p.L + RbGeom<C>::N - 1) / RbGeom<C>::N;
+    const int ntiles = p.B * ((p.L + RbGeom<C>::N - 1) / RbGeom<C>::N);
     const int nwg = ncu * (per_cu > 0 ? per_cu : 1);
     hipLaunchKernelGGL((resblock_x6_kernel<C, NP, F16>), dim3(ntiles < nwg ? ntiles : nwg), dim3(768), lds, s, p);
     RVC_HIP(hipGetLastError());
@@ -431,6 +439,7 @@ int rb_check(const rvc_resblock_args* a) {
     RVC_CHECK_ARG(a && a->x && a->y && a->w1x && a->w2x && a->b1 && a->b2, "resblock: null pointer");
     RVC_CHECK_ARG(a->C == 32 || a->C == 64, "resblock: C must be 32 or 64 (got %lld)", (long long)a->C);
     RVC_CHECK_ARG(a->L > 0 && a->C * a->L < (1ll << 31), "resblock: bad length");
+    RVC_CHECK_ARG(a->B >= 0 && (int64_t)(a->B > 1 ? a->B : 1) * ((a->L + 15) / 16) < (1ll << 31), "resblock: bad B");
     RVC_CHECK_ARG(a->K >= 1 && a->K % 2 == 1 && a->K <= 15 && a->dil >= 1 && (a->K - 1) * a->dil <= RB_MAXSPAN,
                   "resblock: odd K <= 15 with (K-1)*dil <= %d expected", RB_MAXSPAN);
     RVC_CHECK_ARG(a->passes == 6 || a->passes == 3 || a->passes == 1 || a->passes == RVC_ARITH_F16X3,
@@ -468,6 +477,7 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     p.nmf2 = a->nmf2;
     p.accumulate = a->accumulate;
     p.slope = a->slope;
+    p.B = a->B > 1 ? a->B : 1;
     hipStream_t s = (hipStream_t)stream;
     if (a->C == 32) {
         if (a->passes == RVC_ARITH_F16X3) return launch_rb<32, 3, true>(p, s);

@@ -890,9 +890,9 @@ int contentvec_cf(rvc_ctx* c, const float* wav, int64_t N, int out_layer, int fi
     return cv_one(c, M, run, wav, N, out_layer, final_proj, feats_cf, s, true);
 }
 
-// ------------------------------------------------------------------ one VC.pipeline segment (rvc_amd/pipeline.py)
-// rvc_vc_convert's scratch plus its f0 side stream: RMVPE runs there, concurrently with ContentVec on the
-// caller's stream (as VC._pipeline_on_device does), joined by an event before the phone upsample
+// ------------------------------------------------------------------ VC.pipeline (rvc_amd/pipeline.py pipeline_device)
+// rvc_vc_convert_ex's scratch plus its f0 side stream: the f0 estimator runs there, concurrently with ContentVec on
+// the caller's stream (as VC._pipeline_on_device does), joined by an event before the first phone upsample.
 // the retrieval index (rvc_load_index): device copies, owned here and freed as a whole when replaced
 struct IvfIndex : ModelBase {
     int64_t d = 0, nlist = 0, ntotal = 0;
@@ -901,12 +901,14 @@ struct IvfIndex : ModelBase {
     int64_t *list_off = nullptr, *ids = nullptr;
 };
 
-struct VcState : ModelBase {
+struct VcState : ModelBase {  // arena: the whole-input buffers (filtfilt, f0, quiet points, f0-file values)
     hipStream_t side = nullptr;
     hipEvent_t ev_in = nullptr, ev_f0 = nullptr;
     IvfIndex* ix = nullptr;
     void* ivf_ws = nullptr;
     int64_t ivf_ws_bytes = 0;
+    ModelBase seg;  // arena: one segment's buffers (features, retrieval, phone, waveform), reused per segment
+    double* pm_win = nullptr;  // Praat's window + its autocorrelation (rvc_pm_windows), uploaded once
 };
 
 void vc_delete(VcState* v) {
@@ -919,6 +921,7 @@ void vc_delete(VcState* v) {
     if (v->side) (void)hipStreamDestroy(v->side);
     if (v->ev_in) (void)hipEventDestroy(v->ev_in);
     if (v->ev_f0) (void)hipEventDestroy(v->ev_f0);
+    v->seg.release();
     v->release();
     delete v;
 }
@@ -932,53 +935,179 @@ const double kAH[6] = {1, -4.9390018191683636, 9.757863526739543, -9.63954484941
                        -0.94082365320546057};
 const double kZI[5] = {-0.96996047969958465, 3.8798419288925783, -5.8197629081730433, 3.879841948472456,
                        -0.96996048949233871};
+constexpr int64_t kSr = 16000, kXQuery = 6, kXCenter = 38;  // Config (fp32): x_query 6, x_center 38
 
-struct VcPlan {
-    int64_t tpad, Np, F, ld, Tf, T, L, tp, out_len, C;
+struct VcSeg {
+    int64_t a, b, fa;  // padded-signal samples [a, b), f0 frames from fa
+    int64_t Tf, T, L;  // ContentVec frames, synth frames (2 Tf), waveform samples (T upp)
 };
 
-int vc_plan(const rvc_ctx* c, int64_t N, const rvc_vc_args* a, VcPlan& p) {
+struct VcPlan {
+    int64_t tpad, Np, F, ld, p_len, C, tp, upp, emb;
+    int64_t t_max, t_query, t_center;
+    bool long_input;
+};
+
+int vc_basic(const rvc_ctx* c, int64_t N, const rvc_vc_args* a, const rvc_vc_opts* o, VcPlan& p) {
     int emb_dim = 0, upp = 0;
-    MCHECK(c->cv && c->cv->loaded && c->rm && c->rm->loaded && synth_info(c, &emb_dim, &upp),
-           "rvc_vc_convert: load ContentVec, RMVPE and the synthesizer first");
+    MCHECK(c->cv && c->cv->loaded && synth_info(c, &emb_dim, &upp),
+           "rvc_vc_convert: load ContentVec and the synthesizer first");
+    const int f0m = o ? o->f0_method : RVC_F0_RMVPE;
+    MCHECK(f0m == RVC_F0_RMVPE || f0m == RVC_F0_CREPE || f0m == RVC_F0_PM, "rvc_vc_convert: unknown f0 method %d", f0m);
+    MCHECK(f0m != RVC_F0_RMVPE || (c->rm && c->rm->loaded), "rvc_vc_convert: f0 \"rmvpe\" needs rvc_load_rmvpe");
+    MCHECK(f0m != RVC_F0_CREPE || (c->cr && c->cr->loaded), "rvc_vc_convert: f0 \"crepe\" needs rvc_load_crepe");
     MCHECK(a && (a->version == 1 || a->version == 2) && a->x_pad >= 0 && a->x_max > 0 && a->tgt_sr > 0,
            "rvc_vc_convert: bad args");
-    p.tpad = 16000LL * a->x_pad;
-    MCHECK(N >= 1 && N + 160 <= 16000LL * a->x_max,
-           "rvc_vc_convert: %lld samples: one segment only (N + 160 <= x_max s; longer inputs need the quiet-point "
-           "search, VC.pipeline)", (long long)N);
+    MCHECK(N >= 1, "rvc_vc_convert: empty input");
+    p.tpad = kSr * a->x_pad;
     p.Np = N + 2 * p.tpad;
     p.F = 1 + p.Np / kHop;
     p.ld = rvc_rmvpe_salience_ld(p.Np);
-    p.Tf = rvc_contentvec_frames(p.Np);
-    const int64_t p_len = p.Np / kHop;
-    MCHECK(p.Tf >= 1 && 2 * p.Tf <= p_len, "rvc_vc_convert: input too short");
-    p.T = 2 * p.Tf;  // min(2 T_f, p_len), convert.py:364-370
+    p.p_len = p.Np / kHop;
     p.C = a->version == 1 ? c->cv->final_proj.Co : c->cv->E;
     MCHECK(p.C == emb_dim, "rvc_vc_convert: features of %lld channels, the synthesizer takes %d", (long long)p.C,
            emb_dim);
     MCHECK(a->index_rate == 0.0 || (c->vc && c->vc->ix && c->vc->ix->d == p.C),
            "rvc_vc_convert: index_rate %g needs an index of the features' width (rvc_load_index)", a->index_rate);
-    p.L = p.T * upp;
+    p.upp = upp;
+    p.emb = emb_dim;
     p.tp = (int64_t)a->tgt_sr * a->x_pad;
-    p.out_len = p.L - 2 * p.tp;
-    MCHECK(p.out_len > 0, "rvc_vc_convert: input too short");
+    p.t_max = kSr * a->x_max;
+    p.t_query = kSr * kXQuery;
+    p.t_center = kSr * kXCenter;
+    p.long_input = N + kHop > p.t_max;  // convert.py:406 (audio padded by window / 2 on each side)
+    return RVC_OK;
+}
+
+// one segment's sizes; `T <= frames available` as VC.voice_conversion needs (convert.py:364-370)
+int vc_seg(const VcPlan& p, int64_t a, int64_t b, int64_t fa, int64_t fb, VcSeg& g) {
+    g.a = a;
+    g.b = b;
+    g.fa = fa;
+    const int64_t Ns = b - a;
+    g.Tf = rvc_contentvec_frames(Ns);
+    MCHECK(g.Tf >= 1 && 2 * g.Tf <= Ns / kHop, "rvc_vc_convert: segment of %lld samples too short", (long long)Ns);
+    g.T = 2 * g.Tf;  // min(2 T_f, p_len)
+    MCHECK(fa + g.T <= fb, "rvc_vc_convert: pitch shorter than the phone sequence");
+    g.L = g.T * p.upp;
+    MCHECK(g.L > 2 * p.tp, "rvc_vc_convert: input too short");
+    return RVC_OK;
+}
+
+// Segments of convert.py:419-440 (VC._pipeline_on_device): [s, t + t_pad2 + w) for each quiet point t, then [t, end)
+int vc_segments(const VcPlan& p, const std::vector<int64_t>& opt_ts, std::vector<VcSeg>& segs) {
+    segs.clear();
+    int64_t s = 0, last = 0;
+    for (int64_t t : opt_ts) {
+        t = t / kHop * kHop;
+        VcSeg g;
+        MTRY(vc_seg(p, s, t + 2 * p.tpad + kHop, s / kHop, (t + 2 * p.tpad) / kHop, g));
+        segs.push_back(g);
+        s = t;
+        last = t;
+    }
+    VcSeg g;
+    MTRY(vc_seg(p, last, p.Np, last / kHop, p.p_len, g));
+    segs.push_back(g);
+    return RVC_OK;
+}
+
+// convert.py:316-318 on the host: the f0 file (rows "time,f0", f32 as read_f0_file gives them) resampled to 100
+// frames/s by numpy's np.interp (f64, its branch structure), n = np.round((max t - min t) * 100 + 1) in f32
+int f0_file_rep(const float* rows, int64_t nrows, std::vector<double>& rep) {
+#pragma clang fp contract(off)
+    MCHECK(rows && nrows >= 1, "rvc_vc_convert: empty f0 file");
+    float tmin = rows[0], tmax = rows[0];
+    for (int64_t i = 1; i < nrows; ++i) {
+        tmin = rows[2 * i] < tmin ? rows[2 * i] : tmin;
+        tmax = rows[2 * i] > tmax ? rows[2 * i] : tmax;
+    }
+    const float span = tmax - tmin;
+    const float v = span * 100.f + 1.f;
+    const int64_t n = (int16_t)rintf(v);  // np.round (half to even), astype(np.int16)
+    rep.assign(n > 0 ? n : 0, 0.0);
+    std::vector<double> xp(nrows), fp(nrows);
+    for (int64_t i = 0; i < nrows; ++i) {
+        xp[i] = (double)(rows[2 * i] * 100.f);  // inp_f0[:, 0] * 100 is f32, np.interp takes it as f64
+        fp[i] = (double)rows[2 * i + 1];
+    }
+    for (int64_t k = 0; k < (int64_t)rep.size(); ++k) {
+        const double x = (double)k;
+        if (x < xp[0]) {
+            rep[k] = fp[0];
+            continue;
+        }
+        if (x > xp[nrows - 1]) {
+            rep[k] = fp[nrows - 1];
+            continue;
+        }
+        int64_t j = 0;  // xp[j] <= x < xp[j + 1] (binary search over a sorted xp)
+        int64_t lo = 0, hi = nrows - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (xp[mid] <= x) lo = mid;
+            else hi = mid - 1;
+        }
+        j = lo;
+        if (j == nrows - 1 || xp[j] == x) {
+            rep[k] = fp[j];
+            continue;
+        }
+        const double slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]);
+        rep[k] = slope * (x - xp[j]) + fp[j];
+    }
+    return RVC_OK;
+}
+
+// a grow-only device buffer of a ModelBase-owned arena slice is not enough for the f0-file values: own buffer
+int ensure_buf(void** buf, int64_t* cap, int64_t bytes, hipStream_t s) {
+    if (bytes <= *cap) return RVC_OK;
+    if (*buf) {
+        MHIP(hipStreamSynchronize(s));
+        MHIP(hipFree(*buf));
+        *buf = nullptr;
+        *cap = 0;
+    }
+    MHIP(hipMalloc(buf, bytes));
+    *cap = bytes;
     return RVC_OK;
 }
 
 }  // namespace
 
-extern "C" int64_t rvc_vc_out_len(const rvc_ctx* c, int64_t N, const rvc_vc_args* a) {
-    VcPlan p;
-    if (!c || vc_plan(c, N, a, p) != RVC_OK) return -1;
-    return p.out_len;
+extern "C" int64_t rvc_f0_file_resample(const float* rows, int64_t nrows, double* out, int64_t cap) {
+    std::vector<double> rep;
+    if (!rows || nrows < 1 || f0_file_rep(rows, nrows, rep) != RVC_OK) return -1;
+    for (int64_t i = 0; i < (int64_t)rep.size() && i < cap && out; ++i) out[i] = rep[i];
+    return (int64_t)rep.size();
 }
 
-extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const rvc_vc_args* a, float* out,
-                              rvc_stream_t stream) {
-    MCHECK(c && audio && out, "rvc_vc_convert: null argument");
+extern "C" int64_t rvc_vc_out_len(const rvc_ctx* c, int64_t N, const rvc_vc_args* a) {
     VcPlan p;
-    MTRY(vc_plan(c, N, a, p));
+    if (!c || !a || vc_basic(c, N, a, nullptr, p) != RVC_OK) return -1;
+    if (!p.long_input) {
+        std::vector<VcSeg> segs;
+        if (vc_segments(p, {}, segs) != RVC_OK) return -1;
+        return segs[0].L - 2 * p.tp;
+    }
+    // longer inputs: an upper bound (the quiet points are only known after the filtfilt; rvc_vc_convert_ex
+    // reports the exact length).  Segments overlap by t_pad2 + window; each gives at most its frames * upp.
+    const int64_t nq = rvc_quiet_points_count(N, (int)kHop, p.t_center, p.t_max);
+    if (nq < 0) return -1;
+    const int64_t nseg = nq + 1;
+    return ((p.Np + nseg * (2 * p.tpad + kHop)) / kHop + nseg) * p.upp;
+}
+
+extern "C" int rvc_vc_convert_ex(rvc_ctx* c, const float* audio, int64_t N, const rvc_vc_args* a,
+                                 const rvc_vc_opts* o, float* out, int64_t out_cap, int64_t* out_len,
+                                 rvc_stream_t stream) {
+    MCHECK(c && audio && out, "rvc_vc_convert: null argument");
+    if (out_len) *out_len = 0;
+    VcPlan p;
+    MTRY(vc_basic(c, N, a, o, p));
+    const int f0m = o ? o->f0_method : RVC_F0_RMVPE;
+    const double venv = o ? o->volume_envelope : 1.0;
+    MCHECK(!o || o->f0_file_rows == 0 || o->f0_file, "rvc_vc_convert: f0_file rows without data");
     hipStream_t s = (hipStream_t)stream;
     MHIP(hipSetDevice(c->device));
     if (!c->vc) c->vc = new VcState();
@@ -990,28 +1119,80 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
         MHIP(hipEventCreateWithFlags(&V.ev_in, hipEventDisableTiming));
         MHIP(hipEventCreateWithFlags(&V.ev_f0, hipEventDisableTiming));
     }
+    const bool need64 = p.long_input || venv != 1.0 || f0m == RVC_F0_PM;
+    // f0 track length: RMVPE / CREPE 1 + Np / 160 frames; pm max(p_len, Praat frames) (get_f0_pm's padding)
+    const int64_t nf_pm = f0m == RVC_F0_PM ? rvc_pm_frames(p.Np) : 0;
+    MCHECK(f0m != RVC_F0_PM || nf_pm > 0, "rvc_vc_convert: pm: input shorter than one 60 ms window");
+    const int64_t Ftr = f0m == RVC_F0_PM ? (p.p_len > nf_pm ? p.p_len : nf_pm) : p.F;
+    const int64_t nq = rvc_quiet_points_count(N, (int)kHop, p.t_center, p.t_max);
+    const int64_t qws = nq > 0 ? rvc_quiet_points_ws_bytes(N, (int)kHop, p.t_center, p.t_query, p.t_max) : 0;
+    const int64_t pmw = f0m == RVC_F0_PM ? rvc_pm_work_bytes(p.Np) : 0;
+    std::vector<double> rep;
+    if (o && o->f0_file_rows > 0) MTRY(f0_file_rep(o->f0_file, o->f0_file_rows, rep));
     const int64_t fw = (rvc_filtfilt_work_bytes(N) + 7) / 8;
-    MCHECK(fw > 0, "rvc_vc_convert: filtfilt work size");
-    Plan pl;  // f32 slots; the int64 / f64 buffers take two each
-    const int64_t o_work = pl.take(2 * fw), o_xp = pl.take(p.Np), o_sal = pl.take(kClass * p.ld),
-                  o_coarse = pl.take(2 * p.F), o_pitchf = pl.take(p.F), o_feats = pl.take(p.C * p.Tf),
-                  o_phone = pl.take(p.C * p.T), o_wav = pl.take(p.L), o_ws = pl.take(16),
-                  o_blend = pl.take(p.C * p.Tf), o_D = pl.take(8 * p.Tf), o_I = pl.take(2 * 8 * p.Tf),
-                  o_probes = pl.take(2 * (int64_t)(V.ix ? V.ix->nprobe : 1) * p.Tf);
+    MCHECK(fw > 0 && qws >= 0 && pmw >= 0, "rvc_vc_convert: work sizes");
+    Plan pl;  // f32 slots; int64 / f64 buffers take two each
+    const int64_t o_work = pl.take(2 * fw), o_xp = pl.take(p.Np), o_xp64 = pl.take(need64 ? 2 * p.Np : 0),
+                  o_sal = pl.take(f0m == RVC_F0_RMVPE ? kClass * p.ld : 0), o_coarse = pl.take(2 * Ftr),
+                  o_pitchf = pl.take(Ftr), o_opt = pl.take(2 * (nq > 0 ? nq : 1)), o_qws = pl.take((qws + 3) / 4),
+                  o_pmw = pl.take((pmw + 3) / 4), o_pmf0 = pl.take(2 * (nf_pm > 0 ? nf_pm : 1)),
+                  o_rep = pl.take(2 * (int64_t)rep.size()), o_ws = pl.take(16);
     if (pl.off > V.arena_floats && V.side) MHIP(hipStreamSynchronize(V.side));  // the old arena may be in use there
     MTRY(ensure_arena(V, pl.off, s));
     float* A = V.arena;
     float* xp = A + o_xp;
+    double* xp64 = need64 ? (double*)(A + o_xp64) : nullptr;
     // filtfilt + reflect padding (convert.py:403, 416), f64 on the device
-    MTRY(rvc_filtfilt_pad(audio, N, kBH, kAH, kZI, p.tpad, (double*)(A + o_work), xp, nullptr, s));
-    // f0: RMVPE over the padded signal, thred 0.03, pitch shift (VC.get_f0, convert.py:248-255, 304-323)
-    float* sal = A + o_sal;
+    MTRY(rvc_filtfilt_pad(audio, N, kBH, kAH, kZI, p.tpad, (double*)(A + o_work), xp, xp64, s));
+    // quiet-point segmentation (convert.py:404-412): on the device, read back for the segment plan
+    std::vector<int64_t> opt_ts;
+    if (nq > 0) {
+        int64_t* dopt = (int64_t*)(A + o_opt);
+        MTRY(rvc_quiet_points(xp64 + p.tpad, N, (int)kHop, p.t_center, p.t_query, p.t_max, A + o_qws, qws, dopt,
+                              (rvc_stream_t)s));
+        opt_ts.resize(nq);
+        MHIP(hipMemcpyAsync(opt_ts.data(), dopt, nq * 8, hipMemcpyDeviceToHost, s));
+        MHIP(hipStreamSynchronize(s));
+    }
+    std::vector<VcSeg> segs;
+    MTRY(vc_segments(p, opt_ts, segs));
+    int64_t total = 0;
+    for (const VcSeg& g : segs) total += g.L - 2 * p.tp;
+    MCHECK(out_cap >= total, "rvc_vc_convert: output needs %lld samples, the buffer holds %lld", (long long)total,
+           (long long)out_cap);
+    MCHECK(out_len || !p.long_input, "rvc_vc_convert: inputs over x_max need rvc_vc_convert_ex's out_len");
+    // get_f0's optional steps (convert.py:311-318) for the decode kernels
+    rvc_f0_post post{};
+    const rvc_f0_post* postp = nullptr;
+    if ((o && o->f0_autotune) || !rep.empty()) {
+        if (o && o->f0_autotune) {
+            post.autotune = 1;
+            post.strength = o->f0_autotune_strength;
+        }
+        const int64_t rep_off = (int64_t)a->x_pad * 100;
+        if (!rep.empty() && rep_off < Ftr) {
+            double* drep = (double*)(A + o_rep);
+            MHIP(hipMemcpyAsync(drep, rep.data(), rep.size() * 8, hipMemcpyHostToDevice, s));
+            post.rep = drep;
+            post.rep_off = rep_off;
+            post.rep_len = (int64_t)rep.size() < Ftr - rep_off ? (int64_t)rep.size() : Ftr - rep_off;
+        }
+        postp = &post;
+    }
+    if (f0m == RVC_F0_PM && !V.pm_win) {
+        std::vector<double> w(958 + 480);
+        MTRY(rvc_pm_windows(w.data(), w.data() + 958));
+        MTRY(dev_alloc(V, w.size() * 8, (void**)&V.pm_win));
+        MHIP(hipMemcpy(V.pm_win, w.data(), w.size() * 8, hipMemcpyHostToDevice));
+    }
+    // f0 over the whole padded input on the side stream (VC.get_f0, convert.py:304-323, 436)
     int64_t* coarse = (int64_t*)(A + o_coarse);
     float* pitchf = A + o_pitchf;
+    const double shift = pow(2.0, a->pitch_shift / 12.0);
     MHIP(hipEventRecord(V.ev_in, s));
     MHIP(hipStreamWaitEvent(V.side, V.ev_in, 0));
-    // from the fork on, every return joins the side stream back into s (its writes to V.arena must be
-    // ordered before the next call's arena use on s)
+    // from the fork on, every return joins the side stream back into s (its writes to the arenas must be
+    // ordered before the next call's use of them on s)
     struct Join {
         hipStream_t s, side;
         hipEvent_t ev;
@@ -1020,44 +1201,86 @@ extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const r
             if (armed && hipEventRecord(ev, side) == hipSuccess) (void)hipStreamWaitEvent(s, ev, 0);
         }
     } join{s, V.side, V.ev_f0};
-    MTRY(rvc_rmvpe_forward(c, xp, 1, p.Np, sal, (rvc_stream_t)V.side));
-    MTRY(rvc_rmvpe_decode(sal, p.ld, p.F, 0.03, pow(2.0, a->pitch_shift / 12.0), nullptr, nullptr, coarse, pitchf,
-                          (rvc_stream_t)V.side));
-    MHIP(hipEventRecord(V.ev_f0, V.side));
-    // features (convert.py:337-340), phone upsample + protect (:361-378)
-    float* feats = A + o_feats;
-    MTRY(contentvec_cf(c, xp, p.Np, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
-    const float* fb = feats;  // convert.py:347: the protect blend keeps the pre-retrieval features
-    if (a->index_rate != 0.0) {  // search(k = 8) + blend (convert.py:349-359) on the channels-first features
-        const IvfIndex& X = *V.ix;
-        const int64_t need = rvc_ivf_coarse_ws_bytes(p.Tf, X.nlist);
-        if (need > V.ivf_ws_bytes) {
-            if (V.ivf_ws) {
-                MHIP(hipStreamSynchronize(s));
-                MHIP(hipFree(V.ivf_ws));
-                V.ivf_ws = nullptr;
-            }
-            MHIP(hipMalloc(&V.ivf_ws, need));
-            V.ivf_ws_bytes = need;
-        }
-        float* D = A + o_D;
-        int64_t* I = (int64_t*)(A + o_I);
-        MTRY(rvc_ivf_search(feats, p.Tf, p.C, p.Tf, 1, X.centT, X.nlist, X.nprobe, X.list_off, X.codes, X.ids, 8,
-                            V.ivf_ws, need, (int64_t*)(A + o_probes), D, I, (rvc_stream_t)s));
-        MTRY(rvc_ivf_blend(feats, p.Tf, p.C, p.Tf, 1, D, I, 8, X.big, X.ntotal, a->index_rate, A + o_blend, p.Tf,
-                           1, (rvc_stream_t)s));
-        fb = A + o_blend;
+    const rvc_stream_t sd = (rvc_stream_t)V.side;
+    if (f0m == RVC_F0_RMVPE) {
+        float* sal = A + o_sal;
+        MTRY(rvc_rmvpe_forward(c, xp, 1, p.Np, sal, sd));
+        MTRY(rvc_rmvpe_decode(sal, p.ld, p.F, 0.03, shift, postp, nullptr, coarse, pitchf, sd));
+    } else if (f0m == RVC_F0_CREPE) {
+        MTRY(rvc_crepe_f0(c, xp, p.Np, o ? o->crepe_dither : nullptr, a->seed, a->pitch_shift, postp, nullptr, coarse,
+                          pitchf, sd));
+    } else {
+        double* f0 = (double*)(A + o_pmf0);
+        MTRY(rvc_pm_f0(xp64, p.Np, V.pm_win, V.pm_win + 958, A + o_pmw, pmw, f0, sd));
+        MTRY(rvc_pm_post(f0, nf_pm, p.p_len, shift, postp, coarse, pitchf, sd));
     }
-    join.armed = false;
-    MHIP(hipStreamWaitEvent(s, V.ev_f0, 0));  // join: the upsample reads pitchf
-    float* phone = A + o_phone;
-    MTRY(rvc_phone_upsample(fb, feats, a->protect < 0.5f ? pitchf : nullptr, phone, p.C, p.Tf, p.T, a->protect,
-                            (rvc_stream_t)s));
-    // Synthesizer.infer (convert.py:381) with device noise at seed, then the trim and peak normalisation
-    float* wav = A + o_wav;
-    MTRY(synth_run_cf(c, phone, coarse, pitchf, p.T, a->sid, a->seed, wav, s));
-    MHIP(hipMemcpyAsync(out, wav + p.tp, p.out_len * 4, hipMemcpyDeviceToDevice, s));
-    return rvc_peak_normalize(out, p.out_len, A + o_ws, nullptr, (rvc_stream_t)s);
+    MHIP(hipEventRecord(V.ev_f0, V.side));
+    // per segment: features (convert.py:337-340), retrieval (:349-359), phone upsample + protect (:361-378),
+    // Synthesizer.infer with the segment's noise seed, the x_pad trim -- in order into out
+    int64_t Tf_max = 0, T_max = 0, L_max = 0;
+    for (const VcSeg& g : segs) {
+        Tf_max = g.Tf > Tf_max ? g.Tf : Tf_max;
+        T_max = g.T > T_max ? g.T : T_max;
+        L_max = g.L > L_max ? g.L : L_max;
+    }
+    const int nprobe = V.ix ? V.ix->nprobe : 1;
+    Plan ps;
+    const int64_t o_feats = ps.take(p.C * Tf_max), o_phone = ps.take(p.C * T_max), o_wav = ps.take(L_max),
+                  o_blend = ps.take(a->index_rate != 0.0 ? p.C * Tf_max : 0), o_D = ps.take(8 * Tf_max),
+                  o_I = ps.take(2 * 8 * Tf_max), o_probes = ps.take(2 * (int64_t)nprobe * Tf_max),
+                  o_r1 = ps.take(venv != 1.0 ? N / 8000 + 2 : 0), o_r2 = ps.take(venv != 1.0 ? total / 8000 + 2 : 0);
+    MTRY(ensure_arena(V.seg, ps.off, s));
+    float* B = V.seg.arena;
+    bool joined = false;
+    int64_t off = 0;
+    for (size_t k = 0; k < segs.size(); ++k) {
+        const VcSeg& g = segs[k];
+        float* feats = B + o_feats;
+        MTRY(contentvec_cf(c, xp + g.a, g.b - g.a, a->version == 1 ? 9 : 12, a->version == 1, feats, s));
+        const float* fb = feats;  // convert.py:347: the protect blend keeps the pre-retrieval features
+        if (a->index_rate != 0.0) {
+            const IvfIndex& X = *V.ix;
+            const int64_t need = rvc_ivf_coarse_ws_bytes(g.Tf, X.nlist);
+            MTRY(ensure_buf(&V.ivf_ws, &V.ivf_ws_bytes, need, s));
+            float* D = B + o_D;
+            int64_t* I = (int64_t*)(B + o_I);
+            MTRY(rvc_ivf_search(feats, g.Tf, p.C, g.Tf, 1, X.centT, X.nlist, X.nprobe, X.list_off, X.codes, X.ids, 8,
+                                V.ivf_ws, need, (int64_t*)(B + o_probes), D, I, (rvc_stream_t)s));
+            MTRY(rvc_ivf_blend(feats, g.Tf, p.C, g.Tf, 1, D, I, 8, X.big, X.ntotal, a->index_rate, B + o_blend, g.Tf,
+                               1, (rvc_stream_t)s));
+            fb = B + o_blend;
+        }
+        if (!joined) {  // the upsample reads pitchf
+            join.armed = false;
+            MHIP(hipStreamWaitEvent(s, V.ev_f0, 0));
+            joined = true;
+        }
+        float* phone = B + o_phone;
+        MTRY(rvc_phone_upsample(fb, feats, a->protect < 0.5f ? pitchf + g.fa : nullptr, phone, p.C, g.Tf, g.T,
+                                a->protect, (rvc_stream_t)s));
+        float* wav = B + o_wav;
+        MTRY(synth_run_cf(c, phone, coarse + g.fa, pitchf + g.fa, g.T, a->sid, a->seed + k, wav, s));
+        MHIP(hipMemcpyAsync(out + off, wav + p.tp, (g.L - 2 * p.tp) * 4, hipMemcpyDeviceToDevice, s));
+        off += g.L - 2 * p.tp;
+    }
+    if (venv != 1.0) {  // change_rms(audio, 16000, audio_opt, 16000, rate) (convert.py:449): hop 8000 for both
+        const int64_t n1 = rvc_rms_frames_len(N, 8000), n2 = rvc_rms_frames_len(total, 8000);
+        MCHECK(n1 > 0 && n1 <= N / 8000 + 2 && n2 > 0 && n2 <= total / 8000 + 2, "rvc_vc_convert: rms frames");
+        float *r1 = B + o_r1, *r2 = B + o_r2;
+        MTRY(rvc_rms_frames(xp64 + p.tpad, nullptr, N, 8000, r1, (rvc_stream_t)s));
+        MTRY(rvc_rms_frames(nullptr, out, total, 8000, r2, (rvc_stream_t)s));
+        MTRY(rvc_rms_mix(out, total, r1, n1, r2, n2, venv, (rvc_stream_t)s));
+    }
+    MTRY(rvc_peak_normalize(out, total, A + o_ws, nullptr, (rvc_stream_t)s));
+    if (out_len) *out_len = total;
+    return RVC_OK;
+}
+
+extern "C" int rvc_vc_convert(rvc_ctx* c, const float* audio, int64_t N, const rvc_vc_args* a, float* out,
+                              rvc_stream_t stream) {
+    const int64_t n = rvc_vc_out_len(c, N, a);
+    if (n <= 0) return RVC_EINVAL;  // the message is set
+    return rvc_vc_convert_ex(c, audio, N, a, nullptr, out, n, nullptr, stream);
 }
 
 extern "C" int rvc_load_index(rvc_ctx* c, const rvc_ivf_index* x) {

@@ -49,7 +49,7 @@ class ResblockArgs(ctypes.Structure):
     """rvc_resblock_args: one fused (convs1[i], convs2[i]) ResBlock pair (residuals.py:22-44)."""
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("w1x", c_void_p), ("b1", c_void_p), ("w2x", c_void_p),
                 ("b2", c_void_p), ("C", c_int64), ("L", c_int64), ("K", c_int), ("dil", c_int), ("nmf1", c_int),
-                ("nmf2", c_int), ("passes", c_int), ("accumulate", c_int), ("slope", c_float), ("_pad0", c_int)]
+                ("nmf2", c_int), ("passes", c_int), ("accumulate", c_int), ("slope", c_float), ("B", c_int)]
 
 
 class DenoiseArgs(ctypes.Structure):
@@ -85,6 +85,13 @@ class VcArgs(ctypes.Structure):
     """rvc_vc_args: one VC.pipeline segment (convert.py:388-458)."""
     _fields_ = [("sid", c_int64), ("pitch_shift", c_double), ("protect", c_float), ("version", c_int),
                 ("x_pad", c_int), ("x_max", c_int), ("tgt_sr", c_int), ("_pad0", c_int), ("index_rate", c_double), ("seed", c_uint64)]
+
+
+class VcOpts(ctypes.Structure):
+    """rvc_vc_opts: VC.pipeline's options beyond one RMVPE segment (f0 method, autotune, f0 file, volume envelope)."""
+    _fields_ = [("f0_method", c_int), ("f0_autotune", c_int), ("f0_autotune_strength", c_double),
+                ("f0_file", c_void_p), ("f0_file_rows", c_int64), ("volume_envelope", c_double),
+                ("crepe_dither", c_void_p)]
 
 
 class IvfIndex(ctypes.Structure):
@@ -182,7 +189,14 @@ SIGNATURES = {
     "rvc_vc_out_len": [c_void_p, c_int64, POINTER(VcArgs)],
     "rvc_load_index": [c_void_p, POINTER(IvfIndex)],
     "rvc_device_bytes_in_use": [],
+    "rvc_pm_windows": [c_void_p, c_void_p],
+    "rvc_f0_file_resample": [c_void_p, c_int64, c_void_p, c_int64],
+    "rvc_quiet_points_count": [c_int64, c_int, c_int64, c_int64],
+    "rvc_quiet_points_ws_bytes": [c_int64, c_int, c_int64, c_int64, c_int64],
+    "rvc_quiet_points": [c_void_p, c_int64, c_int, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p],
     "rvc_vc_convert": [c_void_p, c_void_p, c_int64, POINTER(VcArgs), c_void_p, c_void_p],
+    "rvc_vc_convert_ex": [c_void_p, c_void_p, c_int64, POINTER(VcArgs), c_void_p, c_void_p, c_int64,
+                          POINTER(c_int64), c_void_p],
     "rvc_crepe_f0": [c_void_p, c_void_p, c_int64, c_void_p, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p],
     "rvc_synth_infer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_uint64,
@@ -195,7 +209,8 @@ _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint,
              "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64,
              "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64,
-             "rvc_vc_out_len": c_int64, "rvc_device_bytes_in_use": c_int64}
+             "rvc_vc_out_len": c_int64, "rvc_device_bytes_in_use": c_int64,
+             "rvc_quiet_points_count": c_int64, "rvc_f0_file_resample": c_int64, "rvc_quiet_points_ws_bytes": c_int64}
 
 _lib = None
 

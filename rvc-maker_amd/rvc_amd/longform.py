@@ -107,7 +107,8 @@ def pipeline_sharded(vc, model, net_g, sid, audio, pitch, version, protect, dist
     N = audio.numel()
     long_input = N + vc.window > vc.t_max
     xp, xp64 = vc.filt(audio.contiguous(), vc.t_pad, want_f64=long_input and rank == 0)
-    opt_ts = [vc.segment_points(xp64[vc.t_pad: vc.t_pad + N].cpu().numpy())] if long_input and rank == 0 else [None]
+    opt_ts = [ops.quiet_points(xp64[vc.t_pad: vc.t_pad + N], vc.window, vc.t_center, vc.t_query, vc.t_max)] \
+        if long_input and rank == 0 else [None]
     if long_input:
         dist.broadcast_object_list(opt_ts, src=0)
     opt_ts = opt_ts[0] or []

@@ -330,14 +330,45 @@ class NativeVC(_Ctx):
         a.x_pad, a.x_max, a.tgt_sr, a.seed = x_pad, x_max, self.tgt_sr, int(seed)
         return a
 
-    def convert(self, audio, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0, index_rate=0.0):
-        """audio f32 [N] 16 kHz (device) -> waveform f32 at tgt_sr (device)."""
+    F0_METHODS = {"rmvpe": 0, "crepe": 1, "pm": 2}
+
+    def convert(self, audio, sid=0, pitch=0.0, protect=0.33, version="v2", seed=0, index_rate=0.0, f0_method="rmvpe",
+                f0_autotune=False, f0_autotune_strength=1.0, inp_f0=None, volume_envelope=1.0, crepe_dither=None):
+        """audio f32 [N] 16 kHz (device) -> waveform f32 at tgt_sr (device): rvc_vc_convert_ex, i.e. the whole
+        VC.pipeline (segmentation of inputs over 41 s, f0 method, autotune, f0 file rows ``inp_f0`` f32 [n][2] as
+        read_f0_file gives them, volume envelope); CREPE (``f0_method="crepe"``, loaded with load_crepe) takes its
+        dither from ``crepe_dither`` (device f32 [1 + padded N // 160]) or draws it on the device from seed."""
         audio = audio.to(self.device, torch.float32).reshape(-1).contiguous()
         a = self.args(sid, pitch, protect, version, seed, index_rate=index_rate)
-        n = int(self.lib.rvc_vc_out_len(self.ctx, audio.numel(), ctypes.byref(a)))
-        if n <= 0:
+        o = _lib.VcOpts()
+        o.f0_method = self.F0_METHODS[f0_method]
+        o.f0_autotune, o.f0_autotune_strength = int(bool(f0_autotune)), float(f0_autotune_strength)
+        keep = None
+        if inp_f0 is not None:
+            keep = np.ascontiguousarray(inp_f0, dtype=np.float32)
+            o.f0_file, o.f0_file_rows = ctypes.c_void_p(keep.ctypes.data), keep.shape[0]
+        o.volume_envelope = float(volume_envelope)
+        if crepe_dither is not None:
+            o.crepe_dither = ctypes.c_void_p(crepe_dither.data_ptr())
+        cap = int(self.lib.rvc_vc_out_len(self.ctx, audio.numel(), ctypes.byref(a)))
+        if cap <= 0:
             raise RuntimeError(f"rvc_vc_out_len: {self.lib.rvc_last_error().decode()}")
-        out = torch.empty(n, device=self.device)
-        check(self.lib.rvc_vc_convert(self.ctx, ctypes.c_void_p(audio.data_ptr()), audio.numel(), ctypes.byref(a),
-                                      ctypes.c_void_p(out.data_ptr()), self.stream()), "rvc_vc_convert")
-        return out
+        out = torch.empty(cap, device=self.device)
+        n = ctypes.c_int64(0)
+        check(self.lib.rvc_vc_convert_ex(self.ctx, ctypes.c_void_p(audio.data_ptr()), audio.numel(), ctypes.byref(a),
+                                         ctypes.byref(o), ctypes.c_void_p(out.data_ptr()), cap, ctypes.byref(n),
+                                         self.stream()), "rvc_vc_convert_ex")
+        del keep
+        return out[: n.value]
+
+    def load_crepe(self, sd: dict, log_trans=None, bn=None) -> None:
+        """A CREPE state dict (any capacity) for f0_method="crepe" (rvc_load_crepe; optional f64 log_trans and
+        [(alpha, beta)] x 6 folded BatchNorms, as NativeCrepe takes them)."""
+        W = {k: v for k, v in sd.items() if torch.as_tensor(v).is_floating_point()}
+        if log_trans is not None:
+            W["log_trans"] = torch.as_tensor(log_trans, dtype=torch.float64)
+        for i, (al, be) in enumerate(bn or []):
+            W[f"conv{i + 1}_BN.alpha"], W[f"conv{i + 1}_BN.beta"] = al.cpu(), be.cpu()
+        params, keep = _params(W)
+        check(self.lib.rvc_load_crepe(self.ctx, params, len(W)), "rvc_load_crepe")
+        del keep

@@ -329,16 +329,18 @@ def resblock_fusable(c1: "Conv", c2: "Conv", dil: int) -> bool:
 
 
 def resblock_pair(x, y, c1: "Conv", c2: "Conv", dil: int, slope: float, accumulate: bool = False):
-    """y (+)= x + c2(lrelu(c1(lrelu(x), dil)))  (residuals.py:22-44, one pair) in one launch; x [C][L]."""
-    C, L = x.shape
+    """y (+)= x + c2(lrelu(c1(lrelu(x), dil)))  (residuals.py:22-44, one pair) in one launch; x [C][L] or
+    [B][C][L] (B clips, each bit-identical to its own call)."""
+    B, C, L = _shape3(x)
     if y.shape != x.shape or not x.is_contiguous() or not y.is_contiguous() or x.data_ptr() == y.data_ptr():
-        raise ValueError("resblock_pair: x, y must be distinct contiguous [C][L] buffers")
+        raise ValueError("resblock_pair: x, y must be distinct contiguous [(B)][C][L] buffers")
     a = _lib.ResblockArgs()
     a.x, a.y = _p(x), _p(y)
     passes = rb_passes(c1.K)
     a.w1x, a.w2x = ctypes.c_void_p(c1.wx.data_ptr(passes)), ctypes.c_void_p(c2.wx.data_ptr(passes))
     a.b1, a.b2 = _p(c1.b), _p(c2.b)
     a.C, a.L, a.K, a.dil = C, L, c1.K, dil
+    a.B = B
     a.nmf1, a.nmf2 = c1.wx_nmf, c2.wx_nmf
     a.passes, a.accumulate, a.slope = passes, int(bool(accumulate)), slope
     check(_lib.load().rvc_resblock_pair(ctypes.byref(a), _stream()), "resblock_pair")
@@ -592,6 +594,26 @@ class FiltFilt:
                                            ctypes.c_void_p(out64.data_ptr()) if want_f64 else None, _stream()),
               "filtfilt_pad")
         return out, out64
+
+
+def quiet_points(x64, window, t_center, t_query, t_max):
+    """VC.pipeline's quiet-point segmentation (convert.py:404-412) on the device: the filtered f64 signal
+    x64 [n] (unpadded) -> host list of opt_ts (one small device->host copy; the segment plan needs it)."""
+    lib = _lib.load()
+    n = x64.numel()
+    cnt = lib.rvc_quiet_points_count(n, window, t_center, t_max)
+    if cnt < 0:
+        raise ValueError("quiet_points: bad arguments")
+    if cnt == 0:
+        return []
+    if x64.dtype != torch.float64 or not x64.is_cuda or not x64.is_contiguous():
+        raise TypeError("quiet_points: a contiguous CUDA f64 signal")
+    need = lib.rvc_quiet_points_ws_bytes(n, window, t_center, t_query, t_max)
+    ws = _workspace(x64.device, need, "quiet")
+    out = torch.empty(cnt, dtype=torch.int64, device=x64.device)
+    check(lib.rvc_quiet_points(ctypes.c_void_p(x64.data_ptr()), n, window, t_center, t_query, t_max, _p(ws), need,
+                               _p(out), _stream()), "quiet_points")
+    return out.cpu().tolist()
 
 
 IVF_FAISS, IVF_EXACT = 0, 1  # RVC_IVF_FAISS (faiss's own f32 arithmetic, the default) / RVC_IVF_EXACT (f64)

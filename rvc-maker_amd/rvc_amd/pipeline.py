@@ -73,7 +73,8 @@ class VC:
 
     # ------------------------------------------------------------------ host-side pieces
     def segment_points(self, audio: np.ndarray):
-        """convert.py:404-412."""
+        """convert.py:404-412 on the host (numpy), as the reference computes it; pipeline_device runs the same
+        search on the device (ops.quiet_points, tested equal)."""
         opt_ts = []
         audio_pad = np.pad(audio, (self.window // 2, self.window // 2), mode="reflect")
         if audio_pad.shape[0] > self.t_max:
@@ -162,6 +163,45 @@ class VC:
         z, _, _, gc = net_g.prior_cf(phone, pitch.contiguous(), sid, zn, seed)
         return {"z": z, "gc": gc, "pitchf": pitchf.contiguous(), "T": T}
 
+    def voice_conversion_batch_device(self, model, net_g, sid, items, version, protect, index=None, index_rate=0.0,
+                                      seeds=(), noise_segs=None):
+        """``voice_conversion_device`` over B clips of one length with the synthesizer batched: retrieval and
+        the phone upsample + protect per clip (convert.py:347-378), then TextEncoder, prior sample, flow^-1
+        and the NSF generator as B-clip launches (Synthesizer.infer, synthesizers.py:446-465).  items: [(xp,
+        coarse, pitchf, feats)] per clip; clip b draws its noise with seeds[b] (parity mode: noise_fn of
+        segment noise_segs[b], default 0).  -> waveforms [B][T*upp]."""
+        B = len(items)
+        phone = pitch = pf = None
+        for b, (xp, coarse, pitchf, feats) in enumerate(items):
+            p_len = xp.numel() // self.window
+            feats0 = feats  # convert.py:347: the protect blend uses the pre-retrieval features
+            if index is not None and index_rate != 0:
+                feats = index.retrieve_cf(feats, index_rate)
+            E, Tf = feats.shape
+            T = min(2 * Tf, p_len)  # convert.py:364-370
+            if 2 * Tf > p_len:
+                raise NotImplementedError("phone longer than p_len (x_mask padding) never occurs in VC.pipeline")
+            if phone is None:
+                phone = torch.empty(B, E, T, device=xp.device)
+                pitch = torch.empty(B, T, dtype=coarse.dtype, device=xp.device)
+                pf = torch.empty(B, T, dtype=pitchf.dtype, device=xp.device)
+            elif phone.shape[2] != T:
+                raise ValueError("voice_conversion_batch_device: clips of one length")
+            if coarse.numel() < T:
+                raise ValueError("pitch shorter than the phone sequence")
+            ops.phone_upsample(feats, feats0, pitchf[:T] if protect < 0.5 else None, phone[b], E, Tf, T,
+                               float(protect))
+            pitch[b].copy_(coarse[:T])
+            pf[b].copy_(pitchf[:T])
+        T = phone.shape[2]
+        zn = sn = None
+        if self.noise_fn:
+            segs = noise_segs or [0] * B
+            zn = torch.stack([self.noise_fn(g, "z", (1, net_g.inter, T)).reshape(net_g.inter, T) for g in segs])
+            sn = torch.stack([self.noise_fn(g, "sine", (1, T * net_g.upp, 1)).reshape(-1) for g in segs])
+        z, _, _, gc = net_g.prior_batch(phone, pitch, sid, zn, seeds)
+        return net_g.decode_batch(z, pf, gc, sn, seeds)
+
     def generate_device(self, net_g, prep, seg, seed):
         """The NSF generator on prior_device's z (synthesizers.py:461-465) -> waveform [T*upp]."""
         sn = self.noise_fn(seg, "sine", (1, prep["T"] * net_g.upp, 1)) if self.noise_fn else None
@@ -179,8 +219,9 @@ class VC:
         xp, xp64 = self.filt(audio.contiguous(), self.t_pad,
                              want_f64=long_input or volume_envelope != 1 or f0_method == "pm")
         opt_ts = []
-        if long_input:  # quiet-point search on the filtered f64 signal, host side as the reference
-            opt_ts = self.segment_points(xp64[self.t_pad: self.t_pad + N].cpu().numpy())
+        if long_input:  # quiet-point search on the filtered f64 signal (device; the plan reads the points back)
+            opt_ts = ops.quiet_points(xp64[self.t_pad: self.t_pad + N], self.window, self.t_center, self.t_query,
+                                      self.t_max)
         p_len = xp.numel() // self.window
         f0_opts = dict(f0_autotune=f0_autotune, f0_autotune_strength=f0_autotune_strength, inp_f0=inp_f0)
         src64 = xp64[self.t_pad: self.t_pad + N] if volume_envelope != 1 else None
@@ -191,10 +232,10 @@ class VC:
                               f0_method="rmvpe"):
         """``pipeline_device`` over B equal-length clips at once (the chunk loop of convert.py:506-507 for
         equal-length chunks, BASELINE configs[2]): RMVPE (U-Net, W_ih, the B BiGRU recurrences side by side)
-        and ContentVec run as B-batched launches on their two streams; the synthesizer -- whose generator
-        already fills the chip at one clip -- then runs per clip.  Clip b draws its noise with seed
+        and ContentVec run as B-batched launches on their two streams, then the synthesizer as B-clip launches
+        (``voice_conversion_batch_device``; RVC_AMD_SYNTH_BATCH=0: per clip).  Clip b draws its noise with seed
         ``self.seed + b``: it equals ``pipeline_device`` of that clip with ``seed = self.seed + b``, up to the
-        summation order of the batched GEMMs (split-K follows the batched grid).  Clips must fit one segment
+        summation order of the batched launches (split-K / split-KV follow the batched grid).  Clips must fit one segment
         (N + window <= t_max, 41 s)."""
         B = len(audios)
         audios = [a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(
@@ -228,6 +269,15 @@ class VC:
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=xpb.device)
         outs = []
+        if B > 1 and self.SYNTH_BATCH:
+            items = [(xpb[b], coarse[b], pitchf[b], feats[b]) for b in range(B)]
+            ob = self.voice_conversion_batch_device(model, net_g, sid, items, version, protect, index, index_rate,
+                                                    [self.seed + b for b in range(B)], list(range(B)))
+            for b in range(B):
+                out = ob[b, tp: ob.shape[1] - tp]
+                ops.peak_normalize(out, self._ws)
+                outs.append(out)
+            return outs
         for b in range(B):
             o = self.voice_conversion_device(model, net_g, sid, xpb[b], coarse[b, :p_len], pitchf[b, :p_len], version,
                                              protect, b, feats=feats[b], index=index, index_rate=index_rate)
@@ -245,12 +295,12 @@ class VC:
         ContentVec GEMMs) fill the CUs the generator's kernels leave between blocks and launches instead of
         running as a phase of their own.  ``batch`` > 1 runs the front end over groups of that many
         equal-length clips at once (``pipeline_device_batch``'s batched RMVPE and ContentVec), group g+1's
-        under group g's synthesizers.
+        under group g's synthesizer, which runs as B-clip launches (``voice_conversion_batch_device``).
 
         Clip k draws its noise with seed ``self.seed + k`` (as ``pipeline_device_batch``): at batch 1 its
         waveform is bit-identical to ``pipeline_device`` of that clip at ``seed = self.seed + k`` -- every
         launch is the same launch on the same data, only its stream differs (batched groups: up to the
-        batched GEMMs' split-K order, as ``pipeline_device_batch``).  Clips must fit one segment (N + window
+        batched launches' split-K / split-KV order, as ``pipeline_device_batch``).  Clips must fit one segment (N + window
         <= t_max, 41 s; longer inputs go through ``pipeline_device``'s host quiet-point search).  Returns the
         list of device waveforms, ordered on the caller's current stream.  ``events`` (a list) collects
         timing events (role, group, torch.cuda.Event) at each group's front / back start and end."""
@@ -334,9 +384,19 @@ class VC:
                 with torch.cuda.stream(back):
                     back.wait_event(done)
                     mark("back_start", g, back)
-                    for xp, coarse, pitchf, feats in items:
-                        for t in (xp, coarse, pitchf, feats):
+                    for it in items:
+                        for t in it:
                             t.record_stream(back)
+                    if len(items) > 1 and self.SYNTH_BATCH:
+                        seeds = [seed0 + len(outs) + b for b in range(len(items))]
+                        ob = self.voice_conversion_batch_device(model, net_g, sid, items, version, protect, index,
+                                                                index_rate, seeds)
+                        for b in range(len(items)):
+                            out = ob[b, tp: ob.shape[1] - tp]
+                            ops.peak_normalize(out, self._ws)
+                            outs.append(out)
+                        items = []
+                    for xp, coarse, pitchf, feats in items:
                         p_len = xp.numel() // self.window
                         self.seed = seed0 + len(outs)
                         o = self.voice_conversion_device(model, net_g, sid, xp, coarse[:p_len], pitchf[:p_len],
@@ -353,6 +413,8 @@ class VC:
             o.record_stream(caller)
         return outs
 
+    # batched groups of the clip stream run one B-clip synthesizer (RVC_AMD_SYNTH_BATCH=0: one per clip)
+    SYNTH_BATCH = os.environ.get("RVC_AMD_SYNTH_BATCH", "1") != "0"
     # clip-stream priorities (measured on one MI355X, 10 x 30 s clips: synthesizer stream high, front end
     # normal: 808 xRT; front end high: 781; per-call pipeline_device: 678)
     STREAM_PRIORITY = {"front": 0, "fside": 0, "back": -1}

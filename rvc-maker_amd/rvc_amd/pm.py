@@ -28,11 +28,14 @@ def _p64(t):
 
 class PitchPM:
     def __init__(self, device="cuda"):
-        i = np.arange(1, NW + 1, dtype=np.float64)
-        w = 0.5 - 0.5 * np.cos(i * 2 * np.pi / (NW + 1))  # Sound_to_Pitch_any's Hanning window
-        ac = np.array([float(np.dot(w[:NW - k], w[k:])) for k in range(BIX + 1)])
+        # Sound_to_Pitch_any's Hanning window and its normalised autocorrelation, from the library (the same
+        # host computation rvc_vc_convert_ex uses)
+        w = np.empty(NW, np.float64)
+        r = np.empty(BIX + 1, np.float64)
+        ops.check(_lib.load().rvc_pm_windows(ctypes.c_void_p(w.ctypes.data), ctypes.c_void_p(r.ctypes.data)),
+                  "pm_windows")
         self.window = torch.from_numpy(w).to(device)
-        self.window_r = torch.from_numpy(ac / ac[0]).to(device)
+        self.window_r = torch.from_numpy(r).to(device)
 
     def to_pitch_ac(self, x64: torch.Tensor) -> torch.Tensor:
         """x64: device f64 [n] at 16 kHz -> selected frequencies f64 [nframes] (0 = unvoiced)."""

@@ -323,18 +323,23 @@ class RMVPEAMD:
         ops.bigru_batched(gi, self.w_hh, self.b_hh, y, gran, self.err, B, Tp)
         return self.fc(y, out_act=ACT_SIGMOID), Tp
 
-    def f0_device_batch(self, xb: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, post=None):
-        """B equal-length signals [B][N] -> (coarse int64 [B][F], pitchf f32 [B][F]); same per-clip result as
-        ``f0_device`` up to the summation order of the batched GEMMs (split-K follows the batched grid)."""
+    def f0_device_batch(self, xb: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, post=None,
+                        want_f0=False, want_salience=False):
+        """B equal-length signals [B][N] -> (coarse int64 [B][F], pitchf f32 [B][F]) [+ raw f0 f64 [B][F]]
+        [+ salience [B][360][Tp]]; same per-clip result as ``f0_device`` up to the summation order of the batched
+        GEMMs (split-K follows the batched grid)."""
         with ops.precision(self.precision or ops.get_precision()):
             mel = self.mel_spectrogram_batch(xb)
             B, _, F = mel.shape
             sal, Tp = self.salience_batch(mel)
         coarse = torch.empty(B, F, dtype=torch.int64, device=xb.device)
         pitchf = torch.empty(B, F, device=xb.device)
+        f0 = torch.empty(B, F, dtype=torch.float64, device=xb.device) if want_f0 else None
         for b in range(B):
-            ops.rmvpe_decode(sal[b], Tp, F, thred, math.pow(2, pitch_shift / 12), None, coarse[b], pitchf[b], post)
-        return coarse, pitchf
+            ops.rmvpe_decode(sal[b], Tp, F, thred, math.pow(2, pitch_shift / 12), f0[b] if want_f0 else None,
+                             coarse[b], pitchf[b], post)
+        out = (coarse, pitchf) + ((f0,) if want_f0 else ()) + ((sal,) if want_salience else ())
+        return out
 
     def f0_device(self, audio: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, want_f0=False,
                   post=None):

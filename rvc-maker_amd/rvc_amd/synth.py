@@ -123,65 +123,72 @@ class SynthesizerAMD:
             self.res.append(blocks)
         self.conv_post = Conv(W["dec.conv_post.weight"], None, device=dev)
 
-    # ------------------------------------------------------------------ stages
-    def text_encoder(self, phone_cf, pitch, T):
-        """TextEncoder.forward (synthesizers.py:366-371) on phone [E][T] -> stats [2*inter][T]."""
-        H, dev = self.hidden, phone_cf.device
-        lin = self.emb_phone(phone_cf)
-        x = torch.empty(H, T, device=dev)
-        ops.textenc_embed(lin, self.emb_pitch if pitch is not None else None, pitch, x, 1, H, T, math.sqrt(H), 0.1)
-        tmp = torch.empty(H, T, device=dev)
-        o = torch.empty(H, T, device=dev)
-        ml = torch.empty(self.n_heads, 2, T, device=dev)
-        kc = self.kc
+    # ------------------------------------------------------------------ stages (B clips of one length T:
+    # every launch takes the clip batch; B = 1 issues exactly the single-clip launches)
+    def text_encoder(self, phone_cf, pitch, T, B=1):
+        """TextEncoder.forward (synthesizers.py:366-371) on phone [B][E][T] -> stats [B][2*inter][T]."""
+        H, dev, nh, kc = self.hidden, phone_cf.device, self.n_heads, self.kc
+        lin = self.emb_phone(phone_cf.reshape(B, -1, T))
+        x = torch.empty(B, H, T, device=dev)
+        ops.textenc_embed(lin, self.emb_pitch if pitch is not None else None, pitch, x, B, H, T, math.sqrt(H), 0.1)
+        tmp = torch.empty(B, H, T, device=dev)
+        o = torch.empty(B, H, T, device=dev)
+        ml = torch.empty(B, nh, 2, T, device=dev)
+        rk = torch.empty(B, nh, 21, T, device=dev)
         scale = 1.0 / math.sqrt(kc)
         for L in self.layers:
             qkv = L["qkv"](x)
-            rk = L["relk"](qkv, B=self.n_heads, Lin=T, x_bstride=kc * T, Lout=T, out_scale=scale)
-            ops.attention(qkv, qkv[H:], qkv[2 * H:], o, B=1, H=self.n_heads, D=kc, T=T, ldc=T, q_hs=kc * T,
-                          k_hs=kc * T, v_hs=kc * T, o_hs=kc * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10)
+            for b in range(B):  # Rk of clip b's heads: one K=1 conv over its nh query slices
+                L["relk"](qkv[b] if B > 1 else qkv, B=nh, Lin=T, x_bstride=kc * T, Lout=T, out_scale=scale,
+                          out=rk[b])
+            qb = qkv.view(B, 3 * H, T)
+            ops.attention(qb, qb[:, H:], qb[:, 2 * H:], o, B=B, H=nh, D=kc, T=T, ldc=T, q_hs=kc * T,
+                          k_hs=kc * T, v_hs=kc * T, o_hs=kc * T, q_bs=3 * H * T, k_bs=3 * H * T, v_bs=3 * H * T,
+                          o_bs=H * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10)
             y = L["o"](o, out=tmp)
-            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, 1, H, T)
+            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, H, T)
             h = L["ffn1"](x, pad=(self.ksz - 1) // 2, out_act=ACT_RELU)
             y = L["ffn2"](h, pad=(self.ksz - 1) // 2, out=tmp)
-            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, 1, H, T)
-        return self.proj(x)
+            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, B, H, T)
+        return self.proj(x).view(B, 2 * self.inter, T)
 
-    def flow_reverse(self, z_p, gc, T):
-        """ResidualCouplingBlock reverse (residuals.py:87-95, 127-137) + WaveNet (modules.py:35-51)."""
-        H, half, dev = self.hidden, self.inter // 2, z_p.device
+    def flow_reverse(self, z_p, gc, T, B=1):
+        """ResidualCouplingBlock reverse (residuals.py:87-95, 127-137) + WaveNet (modules.py:35-51);
+        z_p [B][inter][T]."""
+        H, I, half, dev = self.hidden, self.inter, self.inter // 2, z_p.device
         x = z_p
-        bufs = (torch.empty_like(z_p), torch.empty_like(z_p))
-        h = torch.empty(H, T, device=dev)
-        acts = torch.empty(H, T, device=dev)
-        out_acc = torch.empty(H, T, device=dev)
+        bufs = (torch.empty(B, I, T, device=dev), torch.empty(B, I, T, device=dev))
+        h = torch.empty(B, H, T, device=dev)
+        acts = torch.empty(B, H, T, device=dev)
+        out_acc = torch.empty(B, H, T, device=dev)
         for f in reversed(range(4)):
             F = self.flows[f]
             xf = bufs[0] if x is not bufs[0] else bufs[1]
-            ops.flip_channels(x, xf, 1, self.inter, T)
-            x0, x1 = xf[:half], xf[half:]
-            F["pre"](x0, out=h)
+            ops.flip_channels(x, xf, B, I, T)
+            # x0 = xf[:, :half], x1 = xf[:, half:]: batch stride I*T
+            F["pre"](xf, B=B, Lin=T, x_bstride=I * T, out=h)
             for l in range(3):
                 g_l = gc[f * 6 * H + l * 2 * H: f * 6 * H + (l + 1) * 2 * H]
                 xin = F["ins"][l](h, pad=2, bias2=g_l)
-                ops.gate(xin, acts, 1, H, T)
+                ops.gate(xin, acts, B, H, T)
                 if l < 2:
                     F["rs_a"][l](acts, out=h, res=h)
                     F["rs_b"][l](acts, out=out_acc, accumulate=(l > 0))
                 else:
                     F["rs_b"][l](acts, out=out_acc, accumulate=True)
-            F["post"](out_acc, out=x1, res=x1, out_scale=-1.0)
+            x1 = xf[:, half:]
+            F["post"](out_acc, out=x1, res=x1, y_bstride=I * T, res_bstride=I * T, out_scale=-1.0)
             x = xf
         return x
 
-    def generator(self, z, nsff0, gdec, T, sine_noise):
-        """GeneratorNSF.forward (synthesizers.py:144-161)."""
+    def generator(self, z, nsff0, gdec, T, sine_noise, B=1):
+        """GeneratorNSF.forward (synthesizers.py:144-161) on z [B][inter][T] -> [B][1][T*upp]."""
         dev = z.device
         L = T * self.upp
-        har = torch.empty(L, device=dev)
-        work = torch.empty(T, device=dev)
-        ops.sine_source(nsff0, sine_noise, har, work, 1, T, self.upp, float(self.sr), self.lin_w, self.lin_b)
-        x = self.conv_pre(z, pad=3, bias2=gdec)
+        har = torch.empty(B, L, device=dev)
+        work = torch.empty(B, T, device=dev)
+        ops.sine_source(nsff0, sine_noise, har, work, B, T, self.upp, float(self.sr), self.lin_w, self.lin_b)
+        x = self.conv_pre(z.reshape(B, self.inter, T), pad=3, bias2=gdec)
         scale = 1.0
         nk = len(self.rks)
         for i in range(len(self.ur)):
@@ -189,12 +196,13 @@ class SynthesizerAMD:
             y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale)
             Li = y.shape[-1]
             nc, s, pad = self.noise[i]
-            nc(har.view(1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True)
+            nc(har.view(B, 1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True)
             C = self.chans[i]
             t1 = None  # c1 output of the unfused pairs
-            xa = torch.empty(C, Li, device=dev)
-            xb = torch.empty(C, Li, device=dev)
-            xs = torch.empty(C, Li, device=dev)
+            xa = torch.empty(B, C, Li, device=dev)
+            xb = torch.empty(B, C, Li, device=dev)
+            xs = torch.empty(B, C, Li, device=dev)
+            y = y.view(B, C, Li)
             for j, (kk, pairs) in enumerate(self.res[i]):
                 cur = y
                 for m, (d, c1, c2) in enumerate(pairs):
@@ -205,7 +213,7 @@ class SynthesizerAMD:
                         cur = nxt
                         continue
                     if t1 is None:
-                        t1 = torch.empty(C, Li, device=dev)
+                        t1 = torch.empty(B, C, Li, device=dev)
                     c1(cur, pad=(kk * d - d) // 2, dil=d, out=t1, in_act=ACT_LRELU, in_slope=LRELU_SLOPE)
                     if m == len(pairs) - 1:
                         c2(t1, pad=(kk - 1) // 2, out=xs, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
@@ -224,30 +232,54 @@ class SynthesizerAMD:
         g = self.emb_g[sid].view(self.gin, 1)
         return self.cond(g).view(-1)
 
+    def prior_batch(self, phone_cf, pitch, sid: int, z_noise=None, seeds=(0,)):
+        """Synthesizer.infer up to the generator (synthesizers.py:446-460) over B clips of one length:
+        phone [B][E][T], pitch int64 [B][T] -> (z, z_p, stats) [B][.][T] and gc.  Clip b draws its prior
+        noise with seeds[b] (exactly the draw of a single-clip call with that seed)."""
+        B, E, T = phone_cf.shape
+        dev = phone_cf.device
+        if E != self.emb_dim:
+            raise ValueError(f"phone dim {E} != model's {self.emb_dim}")
+        if z_noise is None and len(seeds) != B:
+            raise ValueError("prior_batch: one seed per clip")
+        gc = self.speaker_cond(sid)
+        stats = self.text_encoder(phone_cf, pitch, T, B)
+        if z_noise is None:
+            z_noise = torch.empty(B, self.inter, T, device=dev)
+            for b in range(B):
+                ops.randn(z_noise[b], seeds[b], 0)
+        z_p = torch.empty(B, self.inter, T, device=dev)
+        ops.prior_sample(stats, z_noise.reshape(B, self.inter, T), z_p, B, self.inter, T, 0.66666)
+        z = self.flow_reverse(z_p, gc, T, B)
+        return z, z_p, stats, gc
+
+    def decode_batch(self, z, nsff0, gc, sine_noise=None, seeds=(0,)):
+        """The NSF generator on z [B][inter][T] (synthesizers.py:461-465) -> o [B][T*upp]; clip b's sine
+        noise from seeds[b]."""
+        B, _, T = z.shape
+        L = T * self.upp
+        if sine_noise is None:
+            if len(seeds) != B:
+                raise ValueError("decode_batch: one seed per clip")
+            sine_noise = torch.empty(B, L, device=z.device)
+            for b in range(B):
+                ops.randn(sine_noise[b], seeds[b], 1 << 40)
+        o = self.generator(z, nsff0.reshape(B, T).float().contiguous(), gc[4 * 6 * self.hidden:], T,
+                           sine_noise.reshape(B, L), B)
+        return o.view(B, L)
+
     def prior_cf(self, phone_cf, pitch, sid: int, z_noise=None, seed: int = 0):
         """Synthesizer.infer up to the generator (synthesizers.py:446-460): TextEncoder, prior sample, flow^-1.
         phone [E][T], pitch int64 [T] -> (z, z_p, stats, gc)."""
         E, T = phone_cf.shape
-        dev = phone_cf.device
-        if E != self.emb_dim:
-            raise ValueError(f"phone dim {E} != model's {self.emb_dim}")
-        gc = self.speaker_cond(sid)
-        stats = self.text_encoder(phone_cf, pitch, T)
-        if z_noise is None:
-            z_noise = ops.randn(torch.empty(self.inter, T, device=dev), seed, 0)
-        z_p = torch.empty(self.inter, T, device=dev)
-        ops.prior_sample(stats, z_noise.reshape(self.inter, T), z_p, 1, self.inter, T, 0.66666)
-        z = self.flow_reverse(z_p, gc, T)
-        return z, z_p, stats, gc
+        z, z_p, stats, gc = self.prior_batch(phone_cf.view(1, E, T), pitch, sid,
+                                             None if z_noise is None else z_noise.reshape(1, self.inter, T), (seed,))
+        return z[0], z_p[0], stats[0], gc
 
     def decode_cf(self, z, nsff0, gc, sine_noise=None, seed: int = 0):
         """The NSF generator on z [inter][T] (synthesizers.py:461-465) -> o [T*upp]."""
         T = z.shape[-1]
-        if sine_noise is None:
-            sine_noise = ops.randn(torch.empty(T * self.upp, device=z.device), seed, 1 << 40)
-        o = self.generator(z, nsff0.reshape(T).float().contiguous(), gc[4 * 6 * self.hidden:], T,
-                           sine_noise.reshape(T * self.upp))
-        return o.view(-1)
+        return self.decode_batch(z.reshape(1, self.inter, T), nsff0, gc, sine_noise, (seed,)).view(-1)
 
     def infer_cf(self, phone_cf, pitch, nsff0, sid: int, z_noise=None, sine_noise=None, seed: int = 0):
         """Channels-first core: phone [E][T], pitch int64 [T], nsff0 f32 [T] -> (o [T*upp], z, z_p, stats)."""

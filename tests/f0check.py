@@ -7,8 +7,11 @@ synthetic random-init weights a few frames per clip have their top two bins (or 
 closer together than that.  Those frames' decisions are not determined at f32 precision.
 
 The yardstick is the reference itself: ``tests/golden/ref_spread_cfg2.npz`` (``make_golden.py spread``)
-ran the reference's VC.pipeline on the headline clip at 8 torch thread counts plus once with its RMVPE in
-float64, and holds every run's salience at the f64 run's top-2 bins per frame.  From it:
+ran the reference's VC.pipeline on the headline clip at 8 torch thread counts, on the input with 1-ulp
+perturbations of its filtered signal (3 runs: the size of the difference between two filtfilt summation
+orders), plus once with its RMVPE in float64, and holds every run's salience at the f64 run's top-2 bins per
+frame.  One of the perturbed runs itself takes a different decision than f64 (frame 326, exact margin 1.7e-5)
+and its waveform differs from the others by 1e-2 RMS.  From it:
 
   * DECISION_NOISE_MAX   the largest error of a decision quantity (top1 - top2, top1 - 0.03) any reference
                          f32 run made against f64 over the whole clip;
@@ -39,10 +42,17 @@ def reference_noise() -> dict:
     s64 = st[-1]
     d64, v64 = s64[0] - s64[1], s64[0] - 0.03
     err = [np.maximum(np.abs((r[0] - r[1]) - d64), np.abs((r[0] - 0.03) - v64)) for r in st[:-1]]
+    # each f32 run's decisions different from the f64 run's (a 1-ulp input perturbation flips one frame)
+    ref_flips = [np.flatnonzero((z["argmax"][i] != z["argmax"][-1]) | (z["voiced"][i] != z["voiced"][-1]))
+                 for i in range(len(st) - 1)]
+    same = [i for i, f in enumerate(ref_flips) if not len(f)] + [len(st) - 1]
     return dict(decision_noise_max=float(np.max(err)),
                 decision_noise_rms=float(max(np.sqrt(np.mean(e ** 2)) for e in err)),
                 decision_noise_frame=np.max(err, 0), sal_err_max=float(z["sal_max"][:-1, -1].max()),
-                wav_spread=float(z["wav_rms"].max()), margin64=z["margin64"], names=[str(n) for n in z["names"]])
+                # waveform spread among the runs that take every f64 decision, and over all runs
+                wav_spread=float(z["wav_rms"][np.ix_(same, same)].max()), wav_spread_all=float(z["wav_rms"].max()),
+                reference_flips={str(z["names"][i]): f.tolist() for i, f in enumerate(ref_flips) if len(f)},
+                margin64=z["margin64"], names=[str(n) for n in z["names"]])
 
 
 def oracle_salience(sd: dict, audio: np.ndarray, dtype=torch.float64) -> np.ndarray:
@@ -87,12 +97,14 @@ def device_salience(vc, audio: np.ndarray):
     return sal[:, :F].t().cpu().numpy().astype(np.float64), f0.cpu().numpy()
 
 
-def check(vc, sd: dict, audio: np.ndarray, factor: float = NOISE_FACTOR, max_flip_frac: float = 1e-3):
+def check(vc, sd: dict, audio: np.ndarray, factor: float = NOISE_FACTOR, max_flip_frac: float = 1e-3,
+          device=None):
     """Device RMVPE on one clip vs the exact model, within ``factor`` of the reference's own f32 noise.
-    Returns (device raw f0, exact-model raw f0, report)."""
+    ``device`` = (salience [F][360], raw f0 [F]) the caller computed (e.g. by the batched path), else the
+    per-clip device path's.  Returns (device raw f0, exact-model raw f0, report)."""
     from oracle import rmvpe as orm
     ref = reference_noise()
-    sdv, f0_dev = device_salience(vc, audio)
+    sdv, f0_dev = device if device is not None else device_salience(vc, audio)
     s64 = oracle_salience(sd, audio, torch.float64)
     s32 = oracle_salience(sd, audio, torch.float32)
     F = s64.shape[0]

@@ -495,7 +495,7 @@ def gen_ref_spread(seconds=30.0, seed=201, threads=(8, 7, 6, 5, 4, 3, 2, 1)):
         return h
     RR.RMVPE.mel2hidden = m2h
 
-    def run(f0_override=None):
+    def run(f0_override=None, x=None):
         vc = conv.VC(48000, conv.config)
         f0s = []
         g0 = vc.get_f0_rmvpe
@@ -506,7 +506,8 @@ def gen_ref_spread(seconds=30.0, seed=201, threads=(8, 7, 6, 5, 4, 3, 2, 1)):
             return f
         vc.get_f0_rmvpe = gf
         with torch.no_grad(), InjectNoise(5):
-            out = vc.pipeline(model=hub, net_g=net_g, sid=0, audio=audio.copy(), pitch=0, f0_method="rmvpe",
+            out = vc.pipeline(model=hub, net_g=net_g, sid=0, audio=(audio if x is None else x).copy(), pitch=0,
+                              f0_method="rmvpe",
                               file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3, volume_envelope=1,
                               version="v2", protect=0.33, hop_length=64, f0_autotune=False, f0_autotune_strength=1,
                               suffix=".pth", embed_suffix=".pt", f0_file=None, f0_onnx=False, pbar=Pbar())
@@ -523,6 +524,21 @@ def gen_ref_spread(seconds=30.0, seed=201, threads=(8, 7, 6, 5, 4, 3, 2, 1)):
         f0s.append(f)
         sals.append(sal_rec[0])
         print(names[-1], o.shape, float(np.sqrt(np.mean(o.astype(np.float64) ** 2))), flush=True)
+    # the same input within its own f32 precision: every sample moved by one f32 ulp (toward +inf or -inf,
+    # seeded) -- as numerically equivalent as the thread counts, and the size of a filtfilt evaluated in a
+    # different (e.g. chunked) order (3e-8 of full scale)
+    torch.set_num_threads(max(threads))
+    for u in range(3):
+        rng = np.random.default_rng(70 + u)
+        x = np.nextafter(audio.astype(np.float32), np.where(rng.random(len(audio)) < 0.5, np.inf, -np.inf)
+                         .astype(np.float32)).astype(audio.dtype)
+        sal_rec.clear()
+        o, f = run(x=x)
+        names.append(f"f32_input_ulp{u}")
+        outs.append(o)
+        f0s.append(f)
+        sals.append(sal_rec[0])
+        print(names[-1], flush=True)
     # the reference's RMVPE in float64 on the same filtered, reflect-padded signal (convert.py:403,416,436)
     torch.set_num_threads(max(threads))
     r = RR.RMVPE(rpath, is_half=False, device="cpu")

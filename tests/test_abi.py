@@ -116,3 +116,27 @@ def test_struct_layouts_match_c_compiler(tmp_path):
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f[0]).offset for f in cls._fields_]
     assert got == want
+
+
+def test_f0_file_resample_matches_reference_numpy():
+    """rvc_f0_file_resample (the f0-file values rvc_vc_convert_ex writes) vs the reference's own numpy steps
+    (convert.py:316-318, restated in rvc_amd.pipeline.f0_override): bit-identical, including rows starting after
+    0 s (np.interp's left value), exact grid hits and rounding of the frame count."""
+    import numpy as np
+    from rvc_amd.pipeline import f0_override
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    cases = [np.array([[0.0, 200.0], [0.4, 260.5], [0.9, 150.0], [1.6, 0.0], [2.0, 310.0]], np.float32),
+             np.array([[0.25, 100.0]], np.float32),
+             np.array([[0.013, 80.0], [0.505, 400.0], [3.3333, 123.456]], np.float32)]
+    for _ in range(20):
+        n = int(rng.integers(2, 40))
+        t = np.sort(rng.uniform(0, 8, n)).astype(np.float32)
+        cases.append(np.stack([t, rng.uniform(0, 900, n).astype(np.float32)], 1))
+    for rows in cases:
+        want, off = f0_override(rows, 1)
+        out = np.zeros(max(len(want), 1), np.float64)
+        n = lib.rvc_f0_file_resample(ctypes.c_void_p(rows.ctypes.data), rows.shape[0], ctypes.c_void_p(out.ctypes.data),
+                                     out.size)
+        assert n == len(want) and off == 100
+        np.testing.assert_array_equal(out[:n], np.asarray(want, np.float64))

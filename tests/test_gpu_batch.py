@@ -61,17 +61,31 @@ def test_rmvpe_batched_matches_per_clip(models):
     mel_b = rm.mel_spectrogram_batch(xp)
     sal_b, Tp = rm.salience_batch(mel_b)
     coarse_b, pitchf_b = rm.f0_device_batch(xp)
+    import f0check
+    _, _, f0_b, _ = rm.f0_device_batch(xp, want_f0=True, want_salience=True)
     for b in range(3):
         mel = rm.mel_spectrogram(xp[b])
-        # log-mel: the batched DFT GEMM sums in another split-K order; log(max(., 1e-5)) magnifies the
-        # relative rounding of the near-cancelling bins
-        assert (mel_b[b] - mel).abs().max().item() <= 2e-3
+        # the |STFT| is per frame (f64 FFT) in both; the mel GEMM may sum in another split-K order
+        assert (mel_b[b] - mel).abs().max().item() <= 1e-4
         sal, Tp1 = rm.salience(mel)
         assert Tp1 == Tp
         assert (sal_b[b] - sal).abs().max().item() <= 2e-3
         coarse, pitchf, _ = rm.f0_device(xp[b])
-        same = (coarse_b[b] == coarse).float().mean().item()
-        assert same >= 0.995, same
+        # the f0-decision rule of tests/f0check.py for the batched path: its salience within the reference's own
+        # f32 noise of the exact (f64) model, and a decision different from the exact model's -- hence from the
+        # per-clip path's, also checked -- only where the exact margin is below the reference's decision noise
+        F = mel.shape[-1]
+        audio = xs[b].cpu().numpy()
+        sd_b = sal_b[b, :, :F].t().cpu().numpy().astype(np.float64)
+        sd_1 = sal[:, :F].t().cpu().numpy().astype(np.float64)
+        _, _, rep_b = f0check.check(None, synthetic.rmvpe_state_dict(72), audio,
+                                    device=(sd_b, f0_b[b].cpu().numpy()))
+        _, _, rep_1 = f0check.check(None, synthetic.rmvpe_state_dict(72), audio, device=(sd_1, None))
+        differ = np.flatnonzero((coarse_b[b] != coarse).cpu().numpy())
+        allowed = set(rep_b["flips_vs_exact"]) | set(rep_1["flips_vs_exact"])
+        for t in differ:  # the coarse quantiser of an equal decision may still round a 1e-6 pitch change
+            if t not in allowed:
+                assert abs(pitchf_b[b, t].item() - pitchf[t].item()) <= 1e-3 * max(1.0, pitchf[t].item()), t
     rm.check_error()
 
 
@@ -124,3 +138,47 @@ def test_batched_stream_bit_identical_to_batch(models):
     for k in range(5):
         assert torch.equal(outs[k], ref[k]), (k, (outs[k] - ref[k]).abs().max().item())
     vc.check_errors()
+
+
+@pytest.mark.parametrize("C,K,dil", [(32, 3, 5), (64, 7, 3), (64, 11, 1)])
+def test_resblock_pair_batched_bit_identical(models, C, K, dil):
+    """The fused ResBlock pair over [B][C][L]: each clip bit-identical to its own launch (per-tile scales and
+    summation order do not depend on the batch)."""
+    g = torch.Generator().manual_seed(C + K)
+    c1 = ops.Conv(torch.randn(C, C, K, generator=g) * 0.1, torch.randn(C, generator=g) * 0.1, device=DEV)
+    c2 = ops.Conv(torch.randn(C, C, K, generator=g) * 0.1, torch.randn(C, generator=g) * 0.1, device=DEV)
+    if not ops.resblock_fusable(c1, c2, dil):
+        pytest.skip("fused ResBlock off")
+    B, L = 3, 5000
+    x = torch.randn(B, C, L, generator=g).to(DEV)
+    y0 = torch.randn(B, C, L, generator=g).to(DEV)
+    for acc in (False, True):
+        y = y0.clone()
+        ops.resblock_pair(x, y, c1, c2, dil, 0.1, accumulate=acc)
+        for b in range(B):
+            yb = y0[b].clone()
+            ops.resblock_pair(x[b].contiguous(), yb, c1, c2, dil, 0.1, accumulate=acc)
+            assert torch.equal(y[b], yb), (acc, b, (y[b] - yb).abs().max().item())
+
+
+def test_synth_batched_matches_per_clip(models):
+    """SynthesizerAMD.prior_batch + decode_batch (TextEncoder, prior, flow^-1, NSF generator as B-clip
+    launches) against infer_cf per clip at the same seeds: equal up to the batched launches' split-K /
+    split-KV order."""
+    net_g = models[2]
+    B, T = 3, 400
+    g = torch.Generator().manual_seed(5)
+    phone = (torch.randn(B, net_g.emb_dim, T, generator=g)).to(DEV)
+    pitch = torch.randint(1, 255, (B, T), generator=g).to(DEV)
+    nsff0 = (100 + 200 * torch.rand(B, T, generator=g)).to(DEV)
+    nsff0[:, 50:80] = 0  # unvoiced run
+    seeds = [11, 12, 13]
+    z, _, stats, gc = net_g.prior_batch(phone, pitch, 0, None, seeds)
+    o = net_g.decode_batch(z, nsff0, gc, None, seeds)
+    for b in range(B):
+        o1, z1, _, st1 = net_g.infer_cf(phone[b].contiguous(), pitch[b].contiguous(), nsff0[b].contiguous(), 0,
+                                        seed=seeds[b])
+        assert (stats[b] - st1).abs().max().item() <= 1e-5 * max(1.0, st1.abs().max().item())
+        assert (z[b] - z1).abs().max().item() <= 1e-5 * max(1.0, z1.abs().max().item())
+        rel = ((o[b] - o1).double().pow(2).mean().sqrt() / o1.double().pow(2).mean().sqrt()).item()
+        assert rel <= 1e-5, (b, rel)

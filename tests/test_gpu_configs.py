@@ -125,9 +125,11 @@ def test_cfg2_headline_30s_48k_fp32_vs_oracle():
     # independent: the oracle on the exact model's f0 decisions (f64 RMVPE), and fully independent (f32 oracle)
     err_exact = _rms(out, _oracle(m, audio, noise, f0_track=f0_exact))
     err_ind = _rms(out, _oracle(m, audio, noise))
-    spread = f0check.reference_noise()["wav_spread"]
+    rn = f0check.reference_noise()
+    spread = rn["wav_spread"]
     _record("cfg2_30s_fp32", rms_on_device_f0=err, rms_vs_exact_f0=err_exact, rms_vs_oracle_f32=err_ind,
-            reference_wav_spread=spread, ref_rms=_rms(ref, 0 * ref), **rep)
+            reference_wav_spread=spread, reference_wav_spread_all_runs=rn["wav_spread_all"],
+            reference_flips=rn["reference_flips"], ref_rms=_rms(ref, 0 * ref), **rep)
     assert err < 1e-4, err
     if not rep["flips_vs_exact"]:  # every decision equals the exact model's: the whole waveform is bounded
         assert err_exact < max(1e-4, spread), err_exact
@@ -195,17 +197,18 @@ def _graph_noise(vc, net_g, T, upp, seed):
     return z.cpu().view(1, net_g.inter, T), sine.cpu().view(1, T * upp, 1)
 
 
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
-def test_cfg5_crepe_full_40k_graph_vs_oracle(precision):
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("precision,secs", [("bf16x3", 4.0), ("bf16", 4.0), ("bf16x3", 30.0)])
+def test_cfg5_crepe_full_40k_graph_vs_oracle(precision, secs):
     """configs[4]: 40k v2 + crepe-full, a ClipGraph captured at the config's arithmetic and replayed over
-    chunks; each replay against the oracle fed the replay's own device draws."""
+    chunks; each replay against the oracle fed the replay's own device draws.  30 s is the chunk bench.py's
+    cfg-5 line replays (its split-K / split-KV choices depend on the length)."""
     from rvc_amd.graph import ClipGraph
-    sr, seed, cap, secs = 40000, 221, "full", 4.0
+    sr, seed, cap = 40000, 221, "full"
     vc, hub, net_g = _device_models(sr, "v2", seed, crepe_cap=cap)
     from rvc_amd.crepe import CrepeAMD  # noqa: F401
     csd = synthetic.crepe_state_dict(seed + 5, cap)
-    chunks = [torch.from_numpy(synthetic.synthetic_audio(secs, seed=1200 + c)).to(DEV) for c in range(2)]
+    chunks = [torch.from_numpy(synthetic.synthetic_audio(secs, seed=1200 + c)).to(DEV) for c in range(2 if secs < 10 else 1)]
     with ops.precision(precision):
         g = ClipGraph(vc, hub, net_g, 0, chunks[0].numel(), f0_method=f"crepe-{cap}")
     m = _oracle_models(sr, "v2", seed, crepe=True)
@@ -226,8 +229,49 @@ def test_cfg5_crepe_full_40k_graph_vs_oracle(precision):
         errs.append(_rms(out, ref))
         scales.append(_rms(ref, 0 * ref))
     rel = [e / s for e, s in zip(errs, scales)]
-    _record(f"cfg5_crepe_full_40k_graph_{precision}", rms=errs, ref_rms=scales, rel=rel)
+    _record(f"cfg5_crepe_full_40k_graph_{precision}_{secs:g}s", rms=errs, ref_rms=scales, rel=rel)
     if precision == "bf16x3":
         assert max(errs) < 1e-4, errs
     else:
         assert max(rel) < BF16_REL_RMS, rel
+
+
+@pytest.mark.timeout(1500)
+def test_cfg3_batched_stream_bf16x3_vs_oracle(cfg3):
+    """configs[2] in the form bench.py measures it: 8 x 10 s chunks through VC.pipeline_device_stream(batch=8)
+    (RMVPE + ContentVec batched over the 8 chunks, the chunks' synthesizers on the back stream), IVF-Flat
+    retrieval at index_rate 0.75, bf16x3 arithmetic, device noise.  Each chunk against the oracle fed the same
+    noise draws: f0 decisions from the batched RMVPE vs the exact model (tests/f0check.py), the waveform within
+    1e-4 RMS on the device's decisions and -- when they equal the exact model's -- on the exact model's."""
+    vc, hub, net_g, dindex, idx, _, _, m = cfg3
+    chunks = [torch.from_numpy(synthetic.synthetic_audio(10.0, seed=1300 + c)).to(DEV) for c in range(8)]
+    seed0 = vc.seed = 500
+    vc.noise_fn = None  # device draws (the fixture's other tests leave their injected noise set)
+    with ops.precision("bf16x3"):
+        outs = vc.pipeline_device_stream(hub, net_g, 0, chunks, 0, "v2", 0.33, dindex, 0.75, batch=8)
+        xpb = torch.stack([vc.filt(a.contiguous(), vc.t_pad)[0] for a in chunks])
+        _, _, f0b, salb = vc.rmvpe.f0_device_batch(xpb, 0.03, 0.0, want_f0=True, want_salience=True)
+    torch.cuda.synchronize()
+    vc.seed = 0
+    vc.check_errors()
+    F = f0b.shape[1]
+    errs, exact, reps = [], [], []
+    for c, a in enumerate(chunks):
+        a_np = a.cpu().numpy()
+        T = (outs[c].numel() + 2 * vc.t_pad_tgt) // net_g.upp  # the chunk's synth frames
+        z, sine = _graph_noise(vc, net_g, T, net_g.upp, seed0 + c)
+        noise = {(0, "z"): z, (0, "sine"): sine}
+        nz = lambda s, k, sh: noise[(s, k)].reshape(sh)  # noqa: E731
+        sd = salb[c, :, :F].t().cpu().numpy().astype(np.float64)
+        f0, f0_exact, rep = f0check.check(vc, synthetic.rmvpe_state_dict(211 + 2), a_np,
+                                          device=(sd, f0b[c].cpu().numpy()))
+        out = outs[c].cpu().numpy()
+        ref = _oracle(m, a_np, nz, index=idx, index_rate=0.75, f0_track=f0)
+        assert out.shape == ref.shape, (out.shape, ref.shape, T)
+        errs.append(_rms(out, ref))
+        reps.append(rep)
+        if not rep["flips_vs_exact"]:
+            exact.append(_rms(out, _oracle(m, a_np, nz, index=idx, index_rate=0.75, f0_track=f0_exact)))
+    _record("cfg3_batch8_stream_bf16x3", rms_on_device_f0=errs, rms_vs_exact_f0=exact, f0=reps)
+    assert max(errs) < 1e-4, errs
+    assert all(e < 1e-4 for e in exact), exact

@@ -337,3 +337,104 @@ def test_load_index_validates_and_replaces():
     torch.cuda.synchronize()
     grown = lib.rvc_device_bytes_in_use() - base
     assert grown < 16 << 20, grown  # one index is ~124 MB (codes + big): a leak would grow by 6x that
+
+
+def _native_and_python(sr=48000, version="v2", seed=81, crepe_cap=None):
+    from rvc_amd import melbasis
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.native import NativeVC
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD, fold_weight_norm
+    hub_ck, rm_sd, cpt = synthetic.make_contentvec_ckpt(seed), synthetic.rmvpe_state_dict(seed + 1), \
+        synthetic.make_synth_ckpt(sr, version, seed=seed + 2)
+    hub, net_g = ContentVecAMD(hub_ck, DEV), SynthesizerAMD(cpt, DEV)
+    crepe = None
+    if crepe_cap:
+        from rvc_amd.crepe import CrepeAMD
+        crepe = {crepe_cap: CrepeAMD(synthetic.crepe_state_dict(seed + 3, crepe_cap), crepe_cap, DEV)}
+    vc = VC(sr, Config(DEV), rmvpe=RMVPEAMD(rm_sd, DEV), crepe=crepe)
+    hw = dict(hub_ck["model"])
+    p = "encoder.pos_conv.0.weight"
+    hw[p] = torch._weight_norm(hw.pop(p + "_v").float(), hw.pop(p + "_g").float(), 2)
+    nat = NativeVC(hub_ck, rm_sd, cpt, DEV, synth_weights=fold_weight_norm(cpt["weight"]), hub_weights=hw,
+                   window=torch.hann_window(1024), mel_basis=melbasis.mel_filterbank(16000, 1024, 128, 30, 8000))
+    if crepe_cap:
+        c = crepe[crepe_cap]
+        nat.load_crepe(synthetic.crepe_state_dict(seed + 3, crepe_cap), log_trans=c.log_trans.cpu(), bn=c.bns)
+    return vc, hub, net_g, nat
+
+
+def test_native_vc_convert_long_input_equals_pipeline_device():
+    """rvc_vc_convert_ex on a 45 s input: the quiet-point segmentation on the device, f0 over the whole input,
+    two segments with their own noise seeds, stitched -- bit-identical to VC.pipeline_device."""
+    vc, hub, net_g, nat = _native_and_python()
+    audio = torch.from_numpy(synthetic.synthetic_audio(45.0, seed=86)).float().to(DEV)
+    ref = vc.pipeline_device(hub, net_g, 0, audio, 1.0, "v2", 0.33)
+    got = nat.convert(audio, 0, 1.0, 0.33, "v2", seed=0)
+    torch.cuda.synchronize()
+    vc.check_errors()
+    assert got.shape == ref.shape and torch.equal(got, ref), rms(got, ref)
+
+
+@pytest.mark.parametrize("f0_method", ["rmvpe", "pm", "crepe"])
+def test_native_vc_convert_options_equal_pipeline_device(f0_method):
+    """rvc_vc_convert_ex with get_f0's autotune and f0-file override and the volume envelope (convert.py:311-318,
+    449), per f0 method: bit-identical to VC.pipeline_device with the same options."""
+    vc, hub, net_g, nat = _native_and_python(40000, "v2", 91, crepe_cap="tiny" if f0_method == "crepe" else None)
+    audio = torch.from_numpy(synthetic.synthetic_audio(4.6, seed=92)).float().to(DEV)
+    inp_f0 = np.array([[0.0, 210.0], [0.37, 260.5], [1.21, 0.0], [2.9, 320.25]], np.float32)
+    kw = dict(f0_autotune=True, f0_autotune_strength=0.7, inp_f0=inp_f0, volume_envelope=0.45)
+    dither = None
+    method = f0_method
+    if f0_method == "crepe":
+        method = "crepe-tiny"
+        T = 1 + (audio.numel() + 2 * vc.t_pad) // 160
+        d = torch.from_numpy(np.random.default_rng(5).triangular(-20.0, 0.0, 20.0, T).astype(np.float32))
+        vc.crepe["tiny"].dither_fn = lambda n: d.numpy().astype(np.float64)
+        dither = d.to(DEV)
+    ref = vc.pipeline_device(hub, net_g, 0, audio, -2.0, "v2", 0.33, f0_method=method, **kw)
+    got = nat.convert(audio, 0, -2.0, 0.33, "v2", seed=0, f0_method=f0_method, crepe_dither=dither, **kw)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and torch.equal(got, ref), rms(got, ref)
+    plain = nat.convert(audio, 0, -2.0, 0.33, "v2", seed=0, f0_method=f0_method, crepe_dither=dither)
+    assert not torch.equal(plain, got)
+
+
+def test_c_host_runs_a_long_input(tmp_path):
+    """examples/c_host/vc_demo on a 45 s input (two segments at a device-found quiet point) from safetensors exports
+    of the checkpoints with the host's folds (weight norm, pos_conv) and RMVPE's window / mel basis, as the Python
+    models make them: bit-identical to VC.pipeline_device."""
+    import os
+    import subprocess
+    from rvc_amd import melbasis
+    from rvc_amd.native import export_safetensors, export_synth_safetensors
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD, fold_weight_norm
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "c_host", "vc_demo")
+    hub_ck, rm_sd, cpt = synthetic.make_contentvec_ckpt(95), synthetic.rmvpe_state_dict(96), \
+        synthetic.make_synth_ckpt(48000, "v2", seed=97)
+    hw = dict(hub_ck["model"])
+    p = "encoder.pos_conv.0.weight"
+    hw[p] = torch._weight_norm(hw.pop(p + "_v").float(), hw.pop(p + "_g").float(), 2)
+    export_safetensors(hw, str(tmp_path / "hub.safetensors"), rvc_contentvec_cfg=[768, 12, 16, 0])
+    rw = dict(rm_sd, window=torch.hann_window(1024),
+              mel_basis=torch.from_numpy(melbasis.mel_filterbank(16000, 1024, 128, 30, 8000)))
+    export_safetensors(rw, str(tmp_path / "rmvpe.safetensors"))
+    export_synth_safetensors(dict(cpt, weight=fold_weight_norm(cpt["weight"])), str(tmp_path / "model.safetensors"))
+    audio = synthetic.synthetic_audio(45.0, seed=98).astype(np.float32)
+    audio.tofile(tmp_path / "audio.f32")
+    r = subprocess.run([exe, str(tmp_path / "hub.safetensors"), str(tmp_path / "rmvpe.safetensors"),
+                        str(tmp_path / "model.safetensors"), str(tmp_path / "audio.f32"), str(tmp_path / "out.f32"),
+                        "0", "0.33", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(tmp_path / "out.f32", dtype=np.float32)
+    vc = VC(48000, Config(DEV), rmvpe=RMVPEAMD(rm_sd, DEV))
+    vc.seed = 3
+    ref = vc.pipeline_device(ContentVecAMD(hub_ck, DEV), SynthesizerAMD(cpt, DEV), 0,
+                             torch.from_numpy(audio).to(DEV), 0.0, "v2", 0.33).cpu().numpy()
+    vc.check_errors()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert np.array_equal(got, ref), (float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2))), r.stdout)

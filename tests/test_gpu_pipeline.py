@@ -162,3 +162,20 @@ def test_f0_post_autotune_override(golden, dtype):
         return
     np.testing.assert_array_equal(coarse.cpu().numpy(), ref_c)
     np.testing.assert_array_equal(pitchf.cpu().numpy(), ref_f0.astype(np.float32))
+
+
+@pytest.mark.parametrize("seconds", [41.5, 95.0, 200.0])
+def test_quiet_points_device_equals_reference_search(seconds):
+    """ops.quiet_points (pipeline.hip) vs the reference's numpy search (VC.segment_points, convert.py:404-412)
+    on a filtered f64 signal with digital-silence runs (exact |sum| = 0 ties: the first index wins) and a
+    non-silent stretch: identical quiet points."""
+    from rvc_amd import ops
+    from rvc_amd.pipeline import VC, Config
+    vc = VC(48000, Config(DEV))
+    x = synthetic.synthetic_audio(seconds, seed=3).astype(np.float64)
+    x[int(50.0 * 16000): int(52.5 * 16000)] = 0.0  # a silence run inside the second search window
+    x64 = vc.filt(torch.from_numpy(x.astype(np.float32)).to(DEV), 0, want_f64=True)[1]
+    want = vc.segment_points(x64.cpu().numpy())
+    got = ops.quiet_points(x64, vc.window, vc.t_center, vc.t_query, vc.t_max)
+    assert got == [int(t) for t in want], (got, want)
+    assert len(got) == (len(x) - 1) // vc.t_center

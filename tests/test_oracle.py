@@ -175,7 +175,11 @@ def test_rmvpe_f64_matches_reference_f64_and_spread_fixture():
     # the reference's f64 run builds its Hann window in f64, the oracle upcasts torch's f32 window (RMVPE.py:166)
     assert np.abs(s64[fi, top2[0]] - st[-1, 0]).max() < 1e-6
     assert np.abs(s64[fi, top2[1]] - st[-1, 1]).max() < 1e-6
-    # the reference's f32 runs: decision errors of 1e-4 order, no decision different from f64 on this clip
+    # the reference's f32 runs: decision errors of 1e-4 order; a decision different from f64 only where the
+    # exact margin is below that noise (one input-ulp run flips frame 326), waveforms within 1e-4 of each other
+    # among the runs that take every f64 decision
     assert 1e-5 < ref["decision_noise_max"] < 1e-3 and ref["decision_noise_rms"] < 2e-5
-    assert not (z["argmax"][:-1] != z["argmax"][-1]).any() and not (z["voiced"][:-1] != z["voiced"][-1]).any()
+    for name, fl in ref["reference_flips"].items():
+        assert name.startswith("f32_") and all(ref["margin64"][fl] < ref["decision_noise_max"]), (name, fl)
     assert ref["wav_spread"] < 1e-4
+    assert ref["wav_spread_all"] < 5e-2
