@@ -90,9 +90,10 @@ class ConvProbe:
             e0.record(s)
             out = self.orig_rb(x, y, c1, c2, dil, slope, accumulate=accumulate)
             e1.record(s)
-            C, L = x.shape
-            flops = 2 * 2.0 * C * C * c1.K * L
-            nbytes = 4.0 * (C * L * (2 + bool(accumulate)) + 2 * C * C * c1.K)  # x, y (+ y read), both weights
+            B = x.shape[0] if x.dim() == 3 else 1  # the synthesizer passes [B][C][L] since it batches clips
+            C, L = x.shape[-2], x.shape[-1]
+            flops = 2 * 2.0 * B * C * C * c1.K * L
+            nbytes = 4.0 * (B * C * L * (2 + bool(accumulate)) + 2 * C * C * c1.K)  # x, y (+ y read), both weights
             self.rec.append((e0, e1, flops, 1, nbytes, self.ops.rb_passes(c1.K)))
             return out
         self.ops.conv1d = wrapped
@@ -211,7 +212,9 @@ def cpu_baseline(seconds=30.0):
     return {"value": round(len(out) / 48000 / dt, 4), "unit": "audio-s/s", "cores": torch.get_num_threads(),
             "host_cpus": os.cpu_count(), "kind": "port",
             "sample": f"{seconds:g} s clip, 48k v2, RMVPE, fp32, torch-CPU oracle (oracle/), wall {dt:.2f} s, "
-                      f"{torch.get_num_threads()} torch threads",
+                      f"{torch.get_num_threads()} torch threads (OMP_NUM_THREADS="
+                      f"{os.environ.get('OMP_NUM_THREADS', 'unset')}: the host's CPU share for this GPU; "
+                      f"os.cpu_count() = {os.cpu_count()} counts every GPU's share)",
             "oracle_over_reference_time": cal.get("oracle_over_reference_time") if cal else None,
             "calibration": (f"oracle / reference wall time on one {cal['seconds']:g} s clip in the build container "
                             f"({cal['threads']} threads): {cal['oracle_s']:.2f} s / {cal['reference_s']:.2f} s "
