@@ -46,6 +46,8 @@ struct ConvParams {
     const uint4* wx;  // split-bf16 packed weights (x6 engine) or null
     int wx_nmf, wx_nch, wx_passes;
     int rot;  // x6: rotate each block's (chunk, tap) order so that the CUs of an XCD spread over the weight image
+    int xcd;  // x6: XCD-aware tile order (each XCD takes a contiguous run of tiles: row tiles share weights in its L2)
+    int ld4;  // x6: the 4-deep input prefetch ring (short-tap convs, where one chunk is only K k-steps of MFMAs)
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
 };
 
@@ -405,7 +407,12 @@ constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2
 // hH and the two sums are added once at the end: the f32 accumulator of the large terms is rounded once per
 // 32 products instead of six times, the corrections' roundings are 2^-8 smaller (RMVPE, whose f0 is a
 // per-frame decision: scripts/conv_prec.py).
-template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
+// LD: the loaders' register ring of staged chunks.  Chunk c + LD - 1's loads are issued while chunk c computes,
+// so a load has LD - 1 chunk-times to land.  LD = 2 covers convs with >= 5 taps; at K = 1 (ContentVec's and
+// the TextEncoder's linears) a chunk is one k-step (48 MFMAs per wave, ~0.6 us) -- shorter than an HBM miss
+// under load -- and LD = 4 keeps 3 chunks in flight (96 more VGPRs in the loader waves, which the compute
+// waves' budget already pays for).
+template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false, int LD = 2>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
     constexpr int NCW = WM * WN;  // compute waves; 4 loader waves follow them
@@ -417,15 +424,30 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     constexpr int BN = 16 * FN * WN;
     extern __shared__ uint4 xs[];  // [2 buffers][span][NPL planes][4 x 16 B]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int zb = blockIdx.z;
+    // XCD-aware tile order (cdna_hip_programming.md T1, the bijective form): blocks are dealt round-robin over
+    // the 8 XCDs, so block b serves tile t(b), which gives each XCD a contiguous run of the row-major tile
+    // order -- whole rows of column tiles, which read the same weight fragments, share that XCD's L2 instead
+    // of each XCD fetching every row's weights.  Speed only: every tile computes the same sums either way.
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (p.xcd) {
+        const int nx = gridDim.x, ny = gridDim.y;
+        const int nwg = nx * ny * (int)gridDim.z;
+        const int orig = bx + nx * (by + ny * bz);
+        const int q = nwg >> 3, r = nwg & 7, xc = orig & 7;
+        const int t = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + (orig >> 3);
+        bx = t % nx;
+        by = (t / nx) % ny;
+        bz = t / (nx * ny);
+    }
+    int zb = bz;
     const int split = zb % p.ksplit;
     zb /= p.ksplit;
     const int phase = zb % p.nphase;
     const int b = zb / p.nphase;
     const int Cog = (int)p.Co;
     const int Cig = (int)p.Ci;
-    const int m0g = blockIdx.y * BM;
-    const int64_t n0 = (int64_t)blockIdx.x * BN;
+    const int m0g = by * BM;
+    const int64_t n0 = (int64_t)bx * BN;
     const int K = p.K, span = p.span;
     const int nch = p.wx_nch, nmf = p.wx_nmf;
     const int ch_beg = split * p.chunks_per_split;
@@ -435,9 +457,13 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     float* tmax = reinterpret_cast<float*>(xs + 2 * bufsz);  // F16: the 4 loader waves' tile |max|
     // Blocks co-resident on one XCD (ids = x mod 8) walk the k-steps from different starting
     // (chunk, tap): in lockstep they would all read the same few weight lines, i.e. the same L2 channels.
-    const int rseed = p.rot ? (int)(blockIdx.x >> 3) : 0;
+    const int rseed = p.rot ? (bx >> 3) : 0;
     const int rt = rseed % K, rc = (rseed / K) % max(nck, 1);
-    auto pchunk = [&](int i) __attribute__((always_inline)) { return ch_beg + (min(i, nck - 1) + rc) % nck; };
+    // logical chunk i (clamped to the last) -> physical chunk; rc < nck, so one conditional subtract, no division
+    auto pchunk = [&](int i) __attribute__((always_inline)) {
+        const int c = min(i, nck - 1) + rc;
+        return ch_beg + (c >= nck ? c - nck : c);
+    };
 
     if (wave >= NCW) {
         // ---------------- loader waves: chunk c+1 split into LDS while chunk c computes
@@ -456,7 +482,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             const int q = base + ipos[it];
             iok |= (unsigned)(idx < 4 * span && q >= 0 && q < lin) << it;
         }
-        float xr[2][X6_NI][8];
+        float xr[LD][X6_NI][8];
         auto xload = [&](int ch, float (&r)[X6_NI][8]) __attribute__((always_inline)) {
             // unconditional (clamped) loads so that the vmcnt bookkeeping is static
 #pragma unroll
@@ -512,6 +538,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                     for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(r[it][e]));
                 return m;
             };
+            static_assert(LD == 2, "split-fp16 keeps the 2-deep ring");
             float am = 0.f;
             for (int i = 2; i < nck; i += 2) {
                 xload(pchunk(i), xr[0]);
@@ -525,20 +552,60 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             __syncthreads();  // tile max published
             sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
         } else {
-            xload(pchunk(0), xr[0]);
-            xload(pchunk(1), xr[1]);
+#pragma unroll
+            for (int d = 0; d < LD; ++d) xload(pchunk(d), xr[d]);
         }
         xstore(pchunk(0), xr[0], xs);
         __syncthreads();
-        // iteration i (chunk ch_beg + i computing): regs slot (i+1)&1 holds chunk i+1; slot i&1 is free
-        auto iter = [&](int i, float (&nxt)[X6_NI][8], float (&fre)[X6_NI][8]) __attribute__((always_inline)) {
-            xload(pchunk(i + 2), fre);
-            if (i + 1 < nck) xstore(pchunk(i + 1), nxt, xs + ((i + 1) & 1) * bufsz);
-            __syncthreads();
-        };
-        for (int i = 0; i < nck; i += 2) {
-            iter(i, xr[1], xr[0]);
-            if (i + 1 < nck) iter(i + 1, xr[0], xr[1]);
+        // iteration i (chunk ch_beg + i computing): ring slot i % LD held chunk i (staged last iteration), so it
+        // takes chunk i + LD's loads; chunk i + 1 goes from slot (i + 1) % LD to the other LDS buffer.  Unrolled
+        // by LD so that every slot index is a compile-time constant.
+        if constexpr (LD == 2) {
+            auto iter = [&](int i, float (&nxt)[X6_NI][8], float (&fre)[X6_NI][8]) __attribute__((always_inline)) {
+                xload(pchunk(i + 2), fre);
+                if (i + 1 < nck) xstore(pchunk(i + 1), nxt, xs + ((i + 1) & 1) * bufsz);
+                __syncthreads();
+            };
+            for (int i = 0; i < nck; i += 2) {
+                iter(i, xr[1], xr[0]);
+                if (i + 1 < nck) iter(i + 1, xr[0], xr[1]);
+            }
+        } else {
+            // K = 1: the weights are a GEMM's A panel (ContentVec's 3072 x 768 image is 14 MB, beyond an XCD's
+            // L2), and the compute waves' PD = 2 k-step prefetch is two short chunks -- less than an L2 miss
+            // under load.  So the loaders also touch one dword per 128-B line of chunk i + LD + 1's weight
+            // fragments (the block's rows, every plane: BM / 16 x 3 KB), bringing them into L2 three chunks
+            // before the compute waves load them.  The dword is folded into a sink when its ring slot is reused
+            // so that it is a real load the compiler counts, never an unused one it drops.
+            const bool pf_on = K == 1;
+            constexpr int PF_LINES = (BM / 16) * 3 * 64 / 8;  // 128-B lines of one (tap, chunk) row panel
+            const uint32_t* wimg = reinterpret_cast<const uint32_t*>(p.wx + (int64_t)phase * K * nch * nmf * 3 * 64);
+            const int pf_line = ltid < PF_LINES ? ltid : PF_LINES - 1;
+            uint32_t pf[LD];
+            uint32_t sink = 0;
+#pragma unroll
+            for (int d = 0; d < LD; ++d) pf[d] = 0;
+            auto pfetch = [&](int c) __attribute__((always_inline)) {
+                const int64_t frag0 = (int64_t)pchunk(c) * nmf + m0g / 16;  // K = 1: tap 0
+                return wimg[(frag0 * 3 * 64 + (int64_t)pf_line * 8) * 4];
+            };
+            for (int i = 0; i < nck; i += LD) {
+#pragma unroll
+                for (int u = 0; u < LD; ++u) {
+                    if (i + u < nck) {
+                        xload(pchunk(i + u + LD), xr[u]);
+                        if (pf_on) {
+                            sink ^= pf[u];
+                            pf[u] = pfetch(i + u + LD + 1);
+                        }
+                        if (i + u + 1 < nck) xstore(pchunk(i + u + 1), xr[(u + 1) % LD], xs + ((i + u + 1) & 1) * bufsz);
+                        __syncthreads();
+                    }
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < LD; ++d) sink ^= pf[d];
+            if (p.dbg == -1 && sink == 0x7fc00001u) p.y[0] = 0.f;  // never true: keeps the prefetch loads live
         }
         return;
     }
@@ -548,17 +615,12 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     const int s_beg = ch_beg * K, s_end = ch_end * K;
     const uint4* wxp = p.wx + (int64_t)phase * K * nch * nmf * 3 * 64;
     const int mf0 = m0g / 16 + wm * FM;
-    // logical k-step s (chunk-major from s_beg) -> physical (chunk, tap)
-    auto kstep = [&](int s, int& ch, int& t) __attribute__((always_inline)) {
-        const int i = (s - s_beg) / K, tl = s - s_beg - i * K;
-        ch = pchunk(i);
-        t = tl + rt < K ? tl + rt : tl + rt - K;
-    };
-    auto aload = [&](int s, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
+    // weight fragments of logical k-step (chunk index i, tap index tl) -- chunk-major from s_beg
+    auto aload = [&](int i, int tl, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
         // wave-uniform fragment base (scalar registers) + one per-lane offset: saddr loads, no
         // per-fragment 64-bit address registers
-        int ch, t;
-        kstep(s, ch, t);
+        const int ch = pchunk(i);
+        const int t = tl + rt < K ? tl + rt : tl + rt - K;
         const int frag0 = __builtin_amdgcn_readfirstlane((t * nch + ch) * nmf + mf0);
         const uint4* src = wxp + (int64_t)frag0 * 3 * 64;
 #pragma unroll
@@ -626,6 +688,12 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     // (the L2 latency must hide behind PD steps of MFMAs: 1 step of 6 passes, 2 of 3, 4 of 1).  The
     // sched_barrier pins each prefetch ahead of the MFMAs it must overlap (hipcc otherwise sinks the
     // independent loads below them and every k-step pays the full L2 round trip).
+    // Every prefetch is issued unconditionally, past the last k-step too (pchunk clamps the chunk, the tap
+    // stays in range: a valid fragment that is never used), and the k-step decode is a pair of counters
+    // stepped once per k-step.  A prefetch under "if (s + PD < s_end)" made hipcc's vmcnt bookkeeping merge
+    // the with- and without-load paths, and it then waited with vmcnt(0) -- on the prefetch just issued --
+    // before each k-step's first MFMAs: the ring bought nothing and every k-step paid an L2 round trip.
+    // The per-step divisions it replaces were ~80 scalar instructions per k-step.
     // depth: as many k-steps as fit a 24-uint4 (96-VGPR) ring, at most 4
     // (8 compute waves = 3 waves per SIMD: an 18-uint4 ring, at most 2 deep)
     // (a 256-column tile, FN = 8, keeps its 64 accumulators by giving the ring 12 uint4)
@@ -634,27 +702,32 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > PD_MAX ? PD_MAX : PD_FIT);
     constexpr int NB = PD + 1;
     uint4 abuf[NB][NPL][FM];
+    int li = 0, lt = 0;  // the next prefetch's logical (chunk index, tap index)
 #pragma unroll
-    for (int i = 0; i < PD; ++i)
-        if (s_beg + i < s_end) aload(s_beg + i, abuf[i]);
+    for (int i = 0; i < PD; ++i) {
+        aload(li, lt, abuf[i]);
+        if (++lt == K) { lt = 0; ++li; }
+    }
     float tile_rs = 1.f;
     if constexpr (F16) {
         __syncthreads();  // tile max published by the loaders
         tile_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
     }
     __syncthreads();  // chunk 0 staged
-    for (int s0 = s_beg; s0 < s_end; s0 += NB) {
+    const int nsteps = s_end - s_beg;
+    int ci = 0, ct = 0;  // the computing k-step's logical (chunk index, tap index)
+    for (int s0 = 0; s0 < nsteps; s0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
-            const int s = s0 + u;
-            if (s < s_end) {
-                const int i = (s - s_beg) / K, tl = s - s_beg - i * K;
-                const int t = tl + rt < K ? tl + rt : tl + rt - K;
-                if (s + PD < s_end) aload(s + PD, abuf[(u + PD) % NB]);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(t, xs + (i & 1) * bufsz, abuf[u]);
-                if (tl == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
+            aload(li, lt, abuf[(u + PD) % NB]);
+            if (++lt == K) { lt = 0; ++li; }
+            __builtin_amdgcn_sched_barrier(0);
+            if (s0 + u < nsteps) {
+                const int t = ct + rt < K ? ct + rt : ct + rt - K;
+                compute(t, xs + (ci & 1) * bufsz, abuf[u]);
+                if (ct == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
             }
+            if (++ct == K) { ct = 0; ++ci; }
         }
     }
     if constexpr (SA) {
@@ -716,8 +789,16 @@ template <int FM, int FN, int WM, int WN, int NP, bool F16 = false, bool SA = fa
 void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     // loader items per thread sized to the staged span (unused items would still issue loads)
     const dim3 blk(64 * (WM * WN + 4));
-    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
+    if (4 * p.span <= 256 * 3) {
+        // the 4-deep ring: 6-pass split-bf16 on one-block-per-CU tiles (the loaders' 96 extra VGPRs fit there)
+        if constexpr (NP == 6 && !F16 && !SA && x6_min_blocks<FM, FN, WM * WN, NP>() == 1) {
+            if (p.ld4) {
+                hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA, 4>), grid, blk, lds, s, p);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA>), grid, blk, lds, s, p);
+    } else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -759,6 +840,11 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     // waveform bar -- off, so the engine keeps the summation order the parity suite validated
     static const int rot = getenv("RVC_X6_ROT") ? atoi(getenv("RVC_X6_ROT")) : 0;
     p.rot = rot;
+    static const int xcd = getenv("RVC_X6_XCD") ? atoi(getenv("RVC_X6_XCD")) : 1;
+    p.xcd = xcd;
+    // the 4-deep input ring for convs of at most this many taps (RVC_X6_LD4_K; 0 = off)
+    static const int ld4_k = getenv("RVC_X6_LD4_K") ? atoi(getenv("RVC_X6_LD4_K")) : 3;
+    p.ld4 = a->K <= ld4_k;
 }
 
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip

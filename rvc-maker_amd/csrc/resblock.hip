@@ -211,11 +211,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     const int SPH = NCH * K;      // k-steps per phase
     const int SPT = 2 * SPH;      // per tile
     const int S_end = my_n * SPT;
-    auto aload = [&](int S, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
-        const int sl = S % SPT;
-        const bool two = sl >= SPH;
-        const int s2 = two ? sl - SPH : sl;
-        const int ch = s2 / K, t = s2 - ch * K;
+    // weight fragments of one k-step: conv two (c2) or c1, 32-channel chunk ch, tap t
+    auto aload = [&](bool two, int ch, int t, uint4 (&a)[NPL][FM]) __attribute__((always_inline)) {
         const uint4* img = two ? p.w2x : p.w1x;
         const int nmf = two ? p.nmf2 : p.nmf1;
         const int frag = __builtin_amdgcn_readfirstlane((t * NCH + ch) * nmf + rg * FM);
@@ -256,12 +253,32 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #ifndef RB_PD3
 #define RB_PD3 3
 #endif
-    constexpr int PD = NPL == 3 ? RB_PD3 : (NPL == 2 ? 2 : 4);
+#ifndef RB_PD2
+#define RB_PD2 2
+#endif
+    constexpr int PD = NPL == 3 ? RB_PD3 : (NPL == 2 ? RB_PD2 : 4);
     constexpr int NB = PD + 1;            // ring slots: k-step S uses slot S % NB (compile-time below)
     uint4 abuf[NB][NPL][FM];
+    // k-step decode by counters stepped once per k-step (tap, chunk, conv), for the prefetch (PD ahead) and the
+    // computing step.  Every prefetch is issued, past the block's last k-step too (the counters wrap inside
+    // the images, so the address stays valid): under "if (S + PD < S_end)" hipcc merged the with- and
+    // without-load paths and waited vmcnt(0) on the prefetch it had just issued before each k-step's MFMAs;
+    // the per-step divisions it replaces were ~80 scalar instructions per 12 MFMAs.
+    bool l_two = false;
+    int l_ch = 0, l_t = 0;
+    auto lstep = [&]() __attribute__((always_inline)) {
+        if (++l_t == K) {
+            l_t = 0;
+            if (++l_ch == NCH) { l_ch = 0; l_two = !l_two; }
+        }
+    };
 #pragma unroll
-    for (int i = 0; i < PD; ++i)
-        if (i < S_end) aload(i, abuf[i]);
+    for (int i = 0; i < PD; ++i) {
+        aload(l_two, l_ch, l_t, abuf[i]);
+        lstep();
+    }
+    bool two = false;  // the computing k-step: conv, chunk, tap, and its tile
+    int ch = 0, t = 0, k = 0;
     float yold[FM][FN][4];
     int n0 = 0;
     float* yb = p.y;  // the current tile's clip
@@ -277,9 +294,12 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
             const int S = S0 + u;
+            aload(l_two, l_ch, l_t, abuf[(u + PD) % NB]);
+            lstep();
+            __builtin_amdgcn_sched_barrier(0);
             if (S < S_end) {
-                const int k = S / SPT, ss = S - k * SPT;
-                if (ss == 0) {  // ---- tile start: X of tile k staged
+                const bool last_ch = ch == NCH - 1 && t == K - 1;  // the conv's last k-step
+                if (!two && ch == 0 && t == 0) {  // ---- tile start: X of tile k staged
                     const int g = (int)blockIdx.x + k * (int)gridDim.x;
                     const int cb = g / ntc;
                     n0 = (g - cb * ntc) * N;
@@ -290,14 +310,9 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #pragma unroll
                         for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
                 }
-                const bool two = ss >= SPH;
-                const int s2 = two ? ss - SPH : ss;
-                const int ch = s2 / K, t = s2 - ch * K;
-                if (S + PD < S_end) aload(S + PD, abuf[(u + PD) % NB]);
-                __builtin_amdgcn_sched_barrier(0);
                 if (!two) compute(Xs + ch * (Wx * NPL * 4), t * d, NF1, abuf[u]);  // c1 over X, tap stride d
                 else compute(Ts + ch * (TW * NPL * 4), t, NF2, abuf[u]);        // c2 over T
-                if (ss == SPH - 1) {
+                if (!two && last_ch) {
                     // ---- c1 epilogue: + bias, lrelu, zero outside [0, L) (c2's padding) -> T (split planes)
                     float tsc = 1.f;
                     if constexpr (F16) {
@@ -383,7 +398,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                             }
                     }
                 }
-                if (ss == SPT - 1) {
+                if (two && last_ch) {
                     // ---- c2 epilogue: + bias, + residual (from R) (+ accumulate) -> y
 #pragma unroll
                     for (int i = 0; i < FM; ++i) {
@@ -403,6 +418,14 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                             }
                         }
                     }
+                }
+            }
+            if (++t == K) {  // step the computing k-step: tap, chunk, conv, tile
+                t = 0;
+                if (++ch == NCH) {
+                    ch = 0;
+                    if (two) ++k;
+                    two = !two;
                 }
             }
         }

@@ -14,13 +14,15 @@ sys.path.insert(0, os.path.join(REPO, "rvc-maker_amd"))
 SHAPES = [(3072, 768, 1599), (768, 3072, 1599), (2304, 768, 1599), (768, 768, 1599)]  # Co, Ci, N
 
 
-def run(prec, reps):
+def run(prec, reps, only=""):
     import torch
     from rvc_amd import ops
     ops.set_precision(prec)
     g = torch.Generator().manual_seed(0)
     tot = 0.0
-    for Co, Ci, N in SHAPES:
+    for i, (Co, Ci, N) in enumerate(SHAPES):
+        if only and str(i) not in only.split(","):
+            continue
         w = torch.randn(Co, Ci, 1, generator=g) / Ci ** 0.5
         b = torch.randn(Co, generator=g)
         conv = ops.Conv(w, b, device="cuda")
@@ -39,7 +41,7 @@ def run(prec, reps):
         tot += us
         ref = (w[:, :, 0].double() @ x.cpu().double()) + b.double()[:, None]
         err = float(((y.cpu().double() - ref).abs().max() / ref.abs().max()))
-        print(f"  {prec:7s} splitk={os.environ.get('RVC_SPLITK_TILES', '512'):4s} {Co:5d}x{Ci:5d}x{N}: "
+        print(f"  {prec:7s} {Co:5d}x{Ci:5d}x{N}: "
               f"{us:7.1f} us  {2 * Co * Ci * N / us / 1e6:6.1f} TF/s  max rel err {err:.2e}", flush=True)
     print(f"  total {tot:.1f} us", flush=True)
 
@@ -48,13 +50,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--child", default="")
+    ap.add_argument("--precisions", default="fp32,f16x3")
+    ap.add_argument("--only", default="", help="comma list of shape indices")
+    ap.add_argument("--envs", default="RVC_SPLITK_TILES=512;RVC_SPLITK_TILES=256;RVC_SPLITK_TILES=0",
+                    help="';'-separated environment settings, each a ','-separated list of NAME=VALUE")
     args = ap.parse_args()
     if args.child:
-        return run(args.child, args.reps)
-    for sk in ("512", "256", "0"):
-        for prec in ("fp32", "f16x3"):
-            env = dict(os.environ, RVC_SPLITK_TILES=sk)
-            rc = subprocess.call([sys.executable, __file__, "--child", prec, "--reps", str(args.reps)], env=env)
+        return run(args.child, args.reps, args.only)
+    for setting in args.envs.split(";"):
+        env = dict(os.environ, **dict(kv.split("=", 1) for kv in setting.split(",") if kv))
+        for prec in args.precisions.split(","):
+            print(f"[{setting}]", flush=True)
+            rc = subprocess.call([sys.executable, __file__, "--child", prec, "--reps", str(args.reps), "--only",
+                                  args.only], env=env)
             if rc:
                 return rc
     return 0
