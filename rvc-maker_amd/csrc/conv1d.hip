@@ -47,7 +47,6 @@ struct ConvParams {
     int wx_nmf, wx_nch, wx_passes;
     int rot;  // x6: rotate each block's (chunk, tap) order so that the CUs of an XCD spread over the weight image
     int xcd;  // x6: XCD-aware tile order (each XCD takes a contiguous run of tiles: row tiles share weights in its L2)
-    int ld4;  // x6: the 4-deep input prefetch ring (short-tap convs, where one chunk is only K k-steps of MFMAs)
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
 };
 
@@ -407,12 +406,10 @@ constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2
 // hH and the two sums are added once at the end: the f32 accumulator of the large terms is rounded once per
 // 32 products instead of six times, the corrections' roundings are 2^-8 smaller (RMVPE, whose f0 is a
 // per-frame decision: scripts/conv_prec.py).
-// LD: the loaders' register ring of staged chunks.  Chunk c + LD - 1's loads are issued while chunk c computes,
-// so a load has LD - 1 chunk-times to land.  LD = 2 covers convs with >= 5 taps; at K = 1 (ContentVec's and
-// the TextEncoder's linears) a chunk is one k-step (48 MFMAs per wave, ~0.6 us) -- shorter than an HBM miss
-// under load -- and LD = 4 keeps 3 chunks in flight (96 more VGPRs in the loader waves, which the compute
-// waves' budget already pays for).
-template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false, int LD = 2>
+// LD: the loaders' register ring of staged chunks (chunk c + 1's loads are issued while chunk c computes).  A
+// 4-deep ring (with an L2 prefetch of the K = 1 weight panels by the loaders) measured no faster on ContentVec's
+// K = 1 GEMMs and slower end to end: not kept.
+template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
     constexpr int NCW = WM * WN;  // compute waves; 4 loader waves follow them
@@ -424,6 +421,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     constexpr int BN = 16 * FN * WN;
     extern __shared__ uint4 xs[];  // [2 buffers][span][NPL planes][4 x 16 B]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int LD = 2;  // the loaders' chunk ring
     // XCD-aware tile order (cdna_hip_programming.md T1, the bijective form): blocks are dealt round-robin over
     // the 8 XCDs, so block b serves tile t(b), which gives each XCD a contiguous run of the row-major tile
     // order -- whole rows of column tiles, which read the same weight fragments, share that XCD's L2 instead
@@ -482,18 +480,43 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             const int q = base + ipos[it];
             iok |= (unsigned)(idx < 4 * span && q >= 0 && q < lin) << it;
         }
+      auto loader = [&](auto fast_c, auto lrelu_c) __attribute__((always_inline)) {
+        // FASTL: every chunk holds 32 real channels (Ci % 32 == 0), no input scale, and the pre-activation is
+        // fixed at compile time (LRELU: leaky ReLU, else none) -- the loads take a wave-uniform row base plus
+        // one 32-bit per-lane offset (no per-element 64-bit address arithmetic or channel clamp) and the split
+        // converts pairs (v_cvt_pk_bf16_f32); the general form handles everything else.  At K = 1 the loaders'
+        // split is the per-chunk cost (one k-step of MFMAs per chunk), ~20 vector instructions per element in
+        // the general form against ~7 here; the results are the same bits.
+        constexpr bool FASTL = decltype(fast_c)::value;
+        constexpr bool LRELU = decltype(lrelu_c)::value;
+        uint32_t ioff[X6_NI];  // FASTL: element offset of (row 8 ig8, clamped position) within a chunk's rows
+#pragma unroll
+        for (int it = 0; it < X6_NI; ++it) {
+            const int q = base + ipos[it];
+            const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
+            ioff[it] = (uint32_t)(ig8[it] * 8 * lin + qc);
+        }
         float xr[LD][X6_NI][8];
         auto xload = [&](int ch, float (&r)[X6_NI][8]) __attribute__((always_inline)) {
             // unconditional (clamped) loads so that the vmcnt bookkeeping is static
-#pragma unroll
-            for (int it = 0; it < X6_NI; ++it) {
-                const int q = base + ipos[it];
-                const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
+            if constexpr (FASTL) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    int c = ch * 32 + ig8[it] * 8 + e;
-                    c = c < Cig ? c : Cig - 1;
-                    r[it][e] = (kAblations && (p.dbg & 4)) ? 0.f : xb[(int64_t)c * lin + qc];
+                    const float* xrow = xb + (int64_t)(ch * 32 + e) * lin;  // wave-uniform
+#pragma unroll
+                    for (int it = 0; it < X6_NI; ++it) r[it][e] = (kAblations && (p.dbg & 4)) ? 0.f : xrow[ioff[it]];
+                }
+            } else {
+#pragma unroll
+                for (int it = 0; it < X6_NI; ++it) {
+                    const int q = base + ipos[it];
+                    const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        int c = ch * 32 + ig8[it] * 8 + e;
+                        c = c < Cig ? c : Cig - 1;
+                        r[it][e] = (kAblations && (p.dbg & 4)) ? 0.f : xb[(int64_t)c * lin + qc];
+                    }
                 }
             }
         };
@@ -503,21 +526,31 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             for (int it = 0; it < X6_NI; ++it) {
                 if (ltid + 256 * it < 4 * span) {
                     uint32_t hw[4], mw[4], lw[4];
+                    if constexpr (FASTL && !F16) {
+                        const bool ok = (iok >> it) & 1u;
+#pragma unroll
+                        for (int e2 = 0; e2 < 4; ++e2) {
+                            float v0 = r[it][2 * e2], v1 = r[it][2 * e2 + 1];
+                            if constexpr (LRELU) {
+                                v0 = v0 >= 0.f ? v0 : v0 * p.in_slope;
+                                v1 = v1 >= 0.f ? v1 : v1 * p.in_slope;
+                            }
+                            split3_pk(ok ? v0 : 0.f, ok ? v1 : 0.f, hw[e2], mw[e2], lw[e2]);
+                        }
+                    } else
 #pragma unroll
                     for (int e2 = 0; e2 < 4; ++e2) {
-                        uint32_t h2[2], m2[2], l2[2];
+                        float v2[2];
 #pragma unroll
                         for (int u = 0; u < 2; ++u) {
                             const int e = 2 * e2 + u;
                             const bool ok = ((iok >> it) & 1u) && ch * 32 + ig8[it] * 8 + e < Cig;
                             float v = r[it][e] * p.in_scale;
                             if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
-                            if constexpr (F16) split2h(ok ? v * sc : 0.f, h2[u], m2[u]);
-                            else split3(ok ? v : 0.f, h2[u], m2[u], l2[u]);
+                            v2[u] = ok ? (F16 ? v * sc : v) : 0.f;
                         }
-                        hw[e2] = h2[0] | (h2[1] << 16);
-                        mw[e2] = m2[0] | (m2[1] << 16);
-                        lw[e2] = l2[0] | (l2[1] << 16);
+                        if constexpr (F16) split2h_pk(v2[0], v2[1], hw[e2], mw[e2]);
+                        else split3_pk(v2[0], v2[1], hw[e2], mw[e2], lw[e2]);
                     }
                     const int pos = ipos[it];
                     dst[x_slot<NPL>(pos, 0, ig8[it])] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
@@ -559,54 +592,29 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         __syncthreads();
         // iteration i (chunk ch_beg + i computing): ring slot i % LD held chunk i (staged last iteration), so it
         // takes chunk i + LD's loads; chunk i + 1 goes from slot (i + 1) % LD to the other LDS buffer.  Unrolled
-        // by LD so that every slot index is a compile-time constant.
-        if constexpr (LD == 2) {
-            auto iter = [&](int i, float (&nxt)[X6_NI][8], float (&fre)[X6_NI][8]) __attribute__((always_inline)) {
-                xload(pchunk(i + 2), fre);
-                if (i + 1 < nck) xstore(pchunk(i + 1), nxt, xs + ((i + 1) & 1) * bufsz);
-                __syncthreads();
-            };
-            for (int i = 0; i < nck; i += 2) {
-                iter(i, xr[1], xr[0]);
-                if (i + 1 < nck) iter(i + 1, xr[0], xr[1]);
+        // by LD so that every slot index is a compile-time constant.  Every iteration issues its loads
+        // unconditionally (pchunk clamps past the last chunk), so that every path through the loop issues the
+        // same loads: with the loads under "if (i + 1 < nck)" hipcc's vmcnt bookkeeping could not follow the
+        // ring across the loop's back-edge and waited vmcnt(0) at the loop head -- on the chunk just requested.
+        // The stores and the barrier stay guarded (no loads inside).
+        for (int i = 0; i < nck; i += LD) {
+#pragma unroll
+            for (int u = 0; u < LD; ++u) {
+                xload(pchunk(i + u + LD), xr[u]);
+                if (i + u + 1 < nck) xstore(pchunk(i + u + 1), xr[(u + 1) % LD], xs + ((i + u + 1) & 1) * bufsz);
+                if (i + u < nck) __syncthreads();
             }
-        } else {
-            // K = 1: the weights are a GEMM's A panel (ContentVec's 3072 x 768 image is 14 MB, beyond an XCD's
-            // L2), and the compute waves' PD = 2 k-step prefetch is two short chunks -- less than an L2 miss
-            // under load.  So the loaders also touch one dword per 128-B line of chunk i + LD + 1's weight
-            // fragments (the block's rows, every plane: BM / 16 x 3 KB), bringing them into L2 three chunks
-            // before the compute waves load them.  The dword is folded into a sink when its ring slot is reused
-            // so that it is a real load the compiler counts, never an unused one it drops.
-            const bool pf_on = K == 1;
-            constexpr int PF_LINES = (BM / 16) * 3 * 64 / 8;  // 128-B lines of one (tap, chunk) row panel
-            const uint32_t* wimg = reinterpret_cast<const uint32_t*>(p.wx + (int64_t)phase * K * nch * nmf * 3 * 64);
-            const int pf_line = ltid < PF_LINES ? ltid : PF_LINES - 1;
-            uint32_t pf[LD];
-            uint32_t sink = 0;
-#pragma unroll
-            for (int d = 0; d < LD; ++d) pf[d] = 0;
-            auto pfetch = [&](int c) __attribute__((always_inline)) {
-                const int64_t frag0 = (int64_t)pchunk(c) * nmf + m0g / 16;  // K = 1: tap 0
-                return wimg[(frag0 * 3 * 64 + (int64_t)pf_line * 8) * 4];
-            };
-            for (int i = 0; i < nck; i += LD) {
-#pragma unroll
-                for (int u = 0; u < LD; ++u) {
-                    if (i + u < nck) {
-                        xload(pchunk(i + u + LD), xr[u]);
-                        if (pf_on) {
-                            sink ^= pf[u];
-                            pf[u] = pfetch(i + u + LD + 1);
-                        }
-                        if (i + u + 1 < nck) xstore(pchunk(i + u + 1), xr[(u + 1) % LD], xs + ((i + u + 1) & 1) * bufsz);
-                        __syncthreads();
-                    }
-                }
-            }
-#pragma unroll
-            for (int d = 0; d < LD; ++d) sink ^= pf[d];
-            if (p.dbg == -1 && sink == 0x7fc00001u) p.y[0] = 0.f;  // never true: keeps the prefetch loads live
         }
+      };
+        // the loader body, once per form (a wave-uniform choice made once per block)
+        if constexpr (!F16) {
+            if ((Cig & 31) == 0 && p.in_scale == 1.f && (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
+                if (p.in_act == RVC_ACT_LRELU) loader(std::true_type{}, std::true_type{});
+                else loader(std::true_type{}, std::false_type{});
+                return;
+            }
+        }
+        loader(std::false_type{}, std::false_type{});
         return;
     }
 
@@ -789,16 +797,8 @@ template <int FM, int FN, int WM, int WN, int NP, bool F16 = false, bool SA = fa
 void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     // loader items per thread sized to the staged span (unused items would still issue loads)
     const dim3 blk(64 * (WM * WN + 4));
-    if (4 * p.span <= 256 * 3) {
-        // the 4-deep ring: 6-pass split-bf16 on one-block-per-CU tiles (the loaders' 96 extra VGPRs fit there)
-        if constexpr (NP == 6 && !F16 && !SA && x6_min_blocks<FM, FN, WM * WN, NP>() == 1) {
-            if (p.ld4) {
-                hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA, 4>), grid, blk, lds, s, p);
-                return;
-            }
-        }
-        hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA>), grid, blk, lds, s, p);
-    } else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
+    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -842,9 +842,6 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.rot = rot;
     static const int xcd = getenv("RVC_X6_XCD") ? atoi(getenv("RVC_X6_XCD")) : 1;
     p.xcd = xcd;
-    // the 4-deep input ring for convs of at most this many taps (RVC_X6_LD4_K; 0 = off)
-    static const int ld4_k = getenv("RVC_X6_LD4_K") ? atoi(getenv("RVC_X6_LD4_K")) : 3;
-    p.ld4 = a->K <= ld4_k;
 }
 
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip

@@ -150,16 +150,14 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                     uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
                     for (int e2 = 0; e2 < 4; ++e2) {
-                        uint32_t h2[2], m2[2], l2[2];
+                        float v2[2];
 #pragma unroll
                         for (int u = 0; u < 2; ++u) {
                             const float v = ok ? xr[it][2 * e2 + u] : 0.f;
-                            if constexpr (F16) split2h((v >= 0.f ? v : v * p.slope) * sc, h2[u], m2[u]);
-                            else split3(v >= 0.f ? v : v * p.slope, h2[u], m2[u], l2[u]);
+                            v2[u] = F16 ? (v >= 0.f ? v : v * p.slope) * sc : (v >= 0.f ? v : v * p.slope);
                         }
-                        hw[e2] = h2[0] | (h2[1] << 16);
-                        mw[e2] = m2[0] | (m2[1] << 16);
-                        lw[e2] = l2[0] | (l2[1] << 16);
+                        if constexpr (F16) split2h_pk(v2[0], v2[1], hw[e2], mw[e2]);
+                        else split3_pk(v2[0], v2[1], hw[e2], mw[e2], lw[e2]);
                     }
                     uint4* dst = Xs + ch * Wx * NPL * 4;
                     dst[x_slot<NPL>(pos, 0, g8)] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
@@ -193,7 +191,9 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             __syncthreads();  // S0(k): X(k) staged; R free
             rstore();         // R(k) from the registers still holding tile k
             const bool more = k + 1 < my_n;
-            if (more) xload(blockIdx.x + (k + 1) * gridDim.x);
+            // unconditional (the last tile reloads itself): every path issues the same loads, which keeps
+            // hipcc's vmcnt bookkeeping exact across the loop (a guarded load made it wait vmcnt(0))
+            xload(blockIdx.x + (more ? k + 1 : k) * gridDim.x);
             if constexpr (F16) {
                 __syncthreads();  // B_T(k): the compute waves' T max (c1 epilogue)
                 if (more) publish_max((k + 1) & 1);
@@ -361,20 +361,19 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                             uint32_t hw[2], mw[2], lw[2];
 #pragma unroll
                             for (int r2 = 0; r2 < 2; ++r2) {
-                                uint32_t h2[2], m2[2], l2[2];
+                                float v2[2];
 #pragma unroll
                                 for (int e = 0; e < 2; ++e) {
                                     if constexpr (F16) {
-                                        split2h(acc[i][j][2 * r2 + e] * tsc, h2[e], m2[e]);
+                                        v2[e] = acc[i][j][2 * r2 + e] * tsc;
                                     } else {
                                         float v = acc[i][j][2 * r2 + e] + p.b1[m0 + 2 * r2 + e];
                                         v = v >= 0.f ? v : v * p.slope;
-                                        split3(ok ? v : 0.f, h2[e], m2[e], l2[e]);
+                                        v2[e] = ok ? v : 0.f;
                                     }
                                 }
-                                hw[r2] = h2[0] | (h2[1] << 16);
-                                mw[r2] = m2[0] | (m2[1] << 16);
-                                lw[r2] = l2[0] | (l2[1] << 16);
+                                if constexpr (F16) split2h_pk(v2[0], v2[1], hw[r2], mw[r2]);
+                                else split3_pk(v2[0], v2[1], hw[r2], mw[r2], lw[r2]);
                             }
                             reinterpret_cast<uint2*>(tb + x_slot<NPL>(it, 0, tg8))[thalf] = make_uint2(hw[0], hw[1]);
                             if constexpr (NPL >= 2)

@@ -50,6 +50,34 @@ RVC_DEV void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
     l = __builtin_bit_cast(uint16_t, bl);
 }
 
+// split3 of two values at once: v_cvt_pk_bf16_f32 rounds a pair (round to nearest even, as the scalar
+// conversion), the residuals come from the packed halves; h / m / l are the pairs' packed words (element 0 in the
+// low half), bit for bit what two split3 calls packed give.
+typedef float rvc_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 rvc_bf2 __attribute__((ext_vector_type(2)));
+RVC_DEV uint32_t pk_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((rvc_f2){a, b}, rvc_bf2));
+}
+RVC_DEV void split3_pk(float v0, float v1, uint32_t& h, uint32_t& m, uint32_t& l) {
+    h = pk_bf16(v0, v1);
+    const float r0 = v0 - __uint_as_float(h << 16), r1 = v1 - __uint_as_float(h & 0xffff0000u);
+    m = pk_bf16(r0, r1);
+    const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xffff0000u);
+    l = pk_bf16(s0, s1);
+}
+
+// split2h of two values at once (v_cvt_pk_f16_f32 rounds a pair to nearest even, as the scalar conversion): h / l
+// are the packed words, element 0 in the low half -- bit for bit two split2h calls packed.
+typedef _Float16 rvc_h2 __attribute__((ext_vector_type(2)));
+RVC_DEV uint32_t pk_f16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((rvc_f2){a, b}, rvc_h2));
+}
+RVC_DEV void split2h_pk(float v0, float v1, uint32_t& h, uint32_t& l) {
+    h = pk_f16(v0, v1);
+    const rvc_h2 hh = __builtin_bit_cast(rvc_h2, h);
+    l = pk_f16(v0 - (float)hh.x, v1 - (float)hh.y);
+}
+
 // NP = MFMA passes per product: 6 (f32-accurate, above), 3 (hH + hM + mH: 16-bit-mantissa products,
 // ~2^-16 relative) or 1 (hH: plain bf16 operands, f32 accumulation).  Only the NPL = 3 / 2 / 1 planes a
 // pass set reads are staged and loaded.  LDS rows are [pos][NPL planes][4 x 16 B]; the 16-B group is
