@@ -75,13 +75,23 @@ class ConvProbe:
         self.rec = []
 
     def __enter__(self):
+        import ctypes
+        from rvc_amd import _lib
+        lib = _lib.load()
+
         def wrapped(*a, **k):
+            # e0 before the call; em is recorded by the library right after the conv kernel, before its split-K
+            # reduce (rvc_conv1d_set_probe_event), so e0 -> em brackets the conv kernel alone
             s = torch.cuda.current_stream()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, em = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            em.record(s)  # creates the event's handle (the library records it again after the kernel)
             e0.record(s)
-            out = self.orig(*a, **k)
-            e1.record(s)
-            self.rec.append((e0, e1, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE, self._bytes(a, k, out),
+            lib.rvc_conv1d_set_probe_event(ctypes.c_void_p(em.cuda_event))
+            try:
+                out = self.orig(*a, **k)
+            finally:
+                lib.rvc_conv1d_set_probe_event(None)
+            self.rec.append((e0, em, self.ops.LAST_CONV_FLOPS, self.ops.LAST_CONV_ENGINE, self._bytes(a, k, out),
                              self.ops.LAST_CONV_PASSES))
             return out
         def wrapped_rb(x, y, c1, c2, dil, slope, accumulate=False):
@@ -144,6 +154,56 @@ class ConvProbe:
     def algorithmic_bytes(self, engine=None):
         rec = [r for r in self.rec if engine is None or r[3] == engine]
         return float(sum(r[4] for r in rec)) / max(len(rec), 1)
+
+
+def _pass_set(name):
+    """The pass set of a split-operand kernel from its template arguments (conv_x6_kernel<FM, FN, WM, WN, NI, NP,
+    F16, SA>, resblock_x6_kernel<C, NP, F16>), in ConvProbe's keys: 16 = split-fp16, 7 = split accumulators."""
+    args = [t.strip() for t in name.split("<", 1)[1].split(">", 1)[0].split(",")]
+    if name.startswith("conv_x6_kernel"):
+        np_, f16, sa = int(args[5]), args[6] == "true", args[7] == "true"
+    else:
+        np_, f16, sa = int(args[1]), args[2] == "true", False
+    return 16 if f16 else (7 if sa else np_)
+
+
+def profiler_kernel_times(fn):
+    """{pass set: (launches, device ms)} of the split-operand kernels one call of ``fn`` launches, from
+    torch.profiler's device records; None when the profiler is unavailable (or rocprofv3 already traces)."""
+    if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
+        return None
+    try:
+        from torch.profiler import ProfilerActivity, profile
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            fn()
+            torch.cuda.synchronize()
+        out = {}
+        for e in prof.events():
+            name = e.name.replace("(anonymous namespace)::", "").replace("void ", "")
+            if not (name.startswith("conv_x6_kernel<") or name.startswith("resblock_x6_kernel<")):
+                continue
+            g = out.setdefault(_pass_set(name), [0, 0.0])
+            g[0] += 1
+            g[1] += e.time_range.elapsed_us() * 1e-3
+        return out or None
+    except Exception as exc:  # noqa: BLE001 -- a missing tracer leaves the event timing in place
+        print(f"bench.py: torch.profiler unavailable ({exc}); roofline from HIP events", file=sys.stderr)
+        return None
+
+
+def park_gpu(seconds):
+    """Occupy the current stream for about ``seconds`` with torch's spin kernel (calibrated once)."""
+    global _SLEEP_RATE
+    if _SLEEP_RATE is None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(1 << 22)
+        e1.record()
+        torch.cuda.synchronize()
+        _SLEEP_RATE = (1 << 22) / max(e0.elapsed_time(e1) * 1e-3, 1e-6)  # cycles per second
+    torch.cuda._sleep(int(_SLEEP_RATE * seconds))
+_SLEEP_RATE = None
 
 
 def pmc_traffic(kernel_family="x6"):
@@ -300,8 +360,8 @@ def main():
 
     if args.graph:
         args.stream = False  # the graph replays are their own chunk loop
-    if args.batch > 1 and (args.graph or len(clips) % args.batch):
-        raise SystemExit("bench.py: --batch needs eager mode and --chunks a multiple of it")
+    if args.batch > 1 and (args.graph or (not args.stream and len(clips) % args.batch)):
+        raise SystemExit("bench.py: --batch needs eager mode, and --chunks a multiple of it without the clip stream")
 
     def step():
         outs = []
@@ -381,10 +441,31 @@ def main():
     roof = None
     if rank == 0 and not args.no_roofline:
         with ConvProbe() as probe:  # one eager pass (a graph replay launches no host-side conv calls)
+            # park the GPU first so that the host queues the pass's launches ahead of it: each event pair then
+            # brackets its kernel, not the host's issue gap before it (short launches would otherwise count
+            # the ~20 us of Python per call)
+            park_gpu(0.08)
             vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
         n, ms, flops = probe.summary(engine=1)  # dominant family: the split-operand conv engine
         n32, ms32, fl32 = probe.summary(engine=0)
         groups, peak = probe.by_passes()
+        timing = "HIP events around each launch (bench.py ConvProbe)"
+        # the same pass again under torch.profiler, whose kernel records are the device's own start / end stamps
+        # (what rocprofv3's kernel trace reads): the events above add a few us of their own to every launch
+        prof = profiler_kernel_times(lambda: vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index,
+                                                                args.index_rate, args.f0))
+        if prof and sum(v[0] for v in prof.values()) == n:
+            ev_ms = {p: g[1] for p, g in groups.items()}
+            for p, g in groups.items():
+                if p in prof:
+                    g[1] = prof[p][1]
+            if all(p in prof for p in groups):
+                ms = sum(g[1] for g in groups.values())
+                timing = ("device kernel stamps (torch.profiler over a second pass; HIP-event time of the "
+                          f"instrumented pass {sum(ev_ms.values()):.3f} ms)")
+            else:
+                for p in groups:
+                    groups[p][1] = ev_ms[p]
         achieved = flops / (ms * 1e-3) / 1e12
         traffic, tsrc = (pmc_traffic("x6") if (args.sr, args.f0, args.precision, args.index_rate, args.seconds)
                          == (48000, "rmvpe", "fp32", 0.0, 30.0) else (None, None))
@@ -407,7 +488,7 @@ def main():
                                                        "tflops": round(g[2] / max(g[1], 1e-9) / 1e9, 2),
                                                        "peak": round(pass_peak(p), 1)}
                                 for p, g in sorted(groups.items())},
-                "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4),
+                "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4), "timing": timing,
                 "algorithmic_gflop_per_step": round(flops / 1e9, 1), "kernel_ms_per_step": round(ms, 3),
                 "f32_engine": {"launches": n32, "kernel_ms": round(ms32, 3), "gflop": round(fl32 / 1e9, 1),
                                "tflops": round(fl32 / max(ms32, 1e-9) / 1e9, 2), "peak": PEAK_F32_MFMA_TFLOPS}}

@@ -106,6 +106,10 @@ int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a);
 /* Which engine a call would run on: 0 = f32 MFMA, 1 = split-bf16 (x6); -1 on bad args. */
 int rvc_conv1d_engine(const rvc_conv1d_args* a);
 int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
+/* Profiling hook (this host thread): while set to a hipEvent_t, each rvc_conv1d call records it on its stream
+ * right after the conv kernel, before any split-K reduce, so that a caller's events can bracket the conv
+ * kernel alone (bench.py's roofline probe).  NULL (the default) turns it off. */
+void rvc_conv1d_set_probe_event(void* hip_event);
 /* Pack KM weights [nphase][Ci*K][Co] (one group) for the split-bf16 engine: out must hold
  * rvc_conv1d_x6_bytes(nphase, Ci, K, Co) bytes; *nmf_out receives wx_nmf. */
 int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co);

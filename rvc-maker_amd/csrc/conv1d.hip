@@ -1129,6 +1129,10 @@ extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {
     return (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
 }
 
+static thread_local hipEvent_t g_probe_event = nullptr;
+
+extern "C" void rvc_conv1d_set_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
+
 extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
     ConvParams p;
     Cfg cfg;
@@ -1162,6 +1166,7 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     else if (cfg.FN == 4) e = launch<2, 4, 2, 2>(p, grid, lds, s);
     else e = launch<2, 2, 2, 2>(p, grid, lds, s);
     RVC_HIP(e);
+    if (g_probe_event) RVC_HIP(hipEventRecord(g_probe_event, s));
     if (p.ksplit > 1) {
         hipLaunchKernelGGL(conv_splitk_reduce, dim3(cdiv(p.ncols, 256), (unsigned)p.Co, (unsigned)(p.B * p.nphase)),
                            dim3(256), 0, s, p);

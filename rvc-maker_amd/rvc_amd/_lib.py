@@ -107,6 +107,7 @@ SIGNATURES = {
     "rvc_version": [],
     "rvc_conv1d": [POINTER(Conv1dArgs), c_void_p, c_int64, c_void_p],
     "rvc_conv1d_workspace_bytes": [POINTER(Conv1dArgs)],
+    "rvc_conv1d_set_probe_event": [c_void_p],
     "rvc_conv1d_engine": [POINTER(Conv1dArgs)],
     "rvc_conv1d_x6_bytes": [c_int64, c_int64, c_int, c_int64],
     "rvc_conv1d_pack_x6": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
@@ -207,7 +208,7 @@ _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,
              "rvc_rms_frames_len": c_int64, "rvc_denoise_work_bytes": c_int64, "rvc_resblock_lds_bytes": c_int64, "rvc_bigru_set_spin_limit": ctypes.c_uint,
-             "rvc_ctx_destroy": None, "rvc_synth_out_len": c_int64,
+             "rvc_ctx_destroy": None, "rvc_conv1d_set_probe_event": None, "rvc_synth_out_len": c_int64,
              "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64,
              "rvc_vc_out_len": c_int64, "rvc_device_bytes_in_use": c_int64,
              "rvc_quiet_points_count": c_int64, "rvc_f0_file_resample": c_int64, "rvc_quiet_points_ws_bytes": c_int64}
