@@ -110,6 +110,14 @@ int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_
  * right after the conv kernel, before any split-K reduce, so that a caller's events can bracket the conv
  * kernel alone (bench.py's roofline probe).  NULL (the default) turns it off. */
 void rvc_conv1d_set_probe_event(void* hip_event);
+/* Split-K policy (this host thread): the library splits a conv's k range over blocks while its tile grid is
+ * below `target` tiles (default 512 = 2 per CU, or RVC_SPLITK_TILES); 0 = never split, -1 = back to the
+ * default.  Returns the previous setting.  Results depend on it at f32 rounding level (the split changes the
+ * summation order). */
+int rvc_conv1d_set_splitk_target(int target);
+/* A stream restricted to the CUs set in mask (nwords 32-bit words, bit i = CU i), and its release. */
+int rvc_stream_create_cu_mask(const uint32_t* mask, int nwords, rvc_stream_t* out);
+int rvc_stream_destroy(rvc_stream_t stream);
 /* Pack KM weights [nphase][Ci*K][Co] (one group) for the split-bf16 engine: out must hold
  * rvc_conv1d_x6_bytes(nphase, Ci, K, Co) bytes; *nmf_out receives wx_nmf. */
 int64_t rvc_conv1d_x6_bytes(int64_t nphase, int64_t Ci, int K, int64_t Co);

@@ -845,9 +845,13 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
 }
 
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
+// per-thread override of the split-K target grid (rvc_conv1d_set_splitk_target; -1 = the process default)
+static thread_local int g_splitk_target = -1;
+
 void split_k(ConvParams& p, int64_t tiles, int nch) {
     // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU
-    static const int target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
+    static const int env_target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
+    const int target = g_splitk_target >= 0 ? g_splitk_target : env_target;
     int ks = 1;
     if (tiles < target && nch >= 4) {
         ks = (int)((target + tiles - 1) / tiles);
@@ -1127,6 +1131,12 @@ extern "C" int64_t rvc_conv1d_workspace_bytes(const rvc_conv1d_args* a) {
     if (plan(a, p, cfg, grid, lds) != RVC_OK) return -1;
     if (p.ksplit <= 1) return 0;
     return (int64_t)p.ksplit * p.B * p.nphase * p.Co * p.ncols * 4;
+}
+
+extern "C" int rvc_conv1d_set_splitk_target(int target) {
+    const int prev = g_splitk_target;
+    g_splitk_target = target < 0 ? -1 : target;
+    return prev;
 }
 
 static thread_local hipEvent_t g_probe_event = nullptr;

@@ -94,6 +94,23 @@ def set_precision(name: str) -> str:
     return prev
 
 
+class splitk_target:
+    """Context manager: the conv engine's split-K target grid for the launches issued inside (tiles below which a
+    conv's k range is split over blocks; 0 = never split, None = leave the current setting)."""
+
+    def __init__(self, target):
+        self.target = target
+
+    def __enter__(self):
+        if self.target is not None:
+            self.prev = _lib.load().rvc_conv1d_set_splitk_target(int(self.target))
+        return self
+
+    def __exit__(self, *a):
+        if self.target is not None:
+            _lib.load().rvc_conv1d_set_splitk_target(self.prev)
+
+
 class precision:
     """Context manager: ``with ops.precision("bf16"): ...``."""
 

@@ -431,27 +431,68 @@ class VC:
         (RVC_AMD_{FRONT,FSIDE,BACK}_PRIORITY override)."""
         prio = int(os.environ.get(f"RVC_AMD_{role.upper()}_PRIORITY", str(self.STREAM_PRIORITY[role])))
         slot = self.STREAM_SLOT[role] if pipe == 0 else 2 * pipe + (role == "front")
-        return self._pooled_stream(device, prio, slot)
+        return self._pooled_stream(device, prio, slot, self.BACK_CU_MASK if role == "back" else "none")
 
-    def _pooled_stream(self, device, prio, slot):
+    def _pooled_stream(self, device, prio, slot, mask="none"):
         """Streams are pooled by (priority, slot) and shared between roles that never run at once (the
         per-call side stream is the clip stream's back stream, ClipGraph's normal-priority fork its fside
         stream).  The device has GPU_MAX_HW_QUEUES = 4 hardware queues per process: with the default stream,
         these three fill them, and a fifth stream would share a queue -- serialising, for example, RMVPE
         behind ContentVec (measured: a per-call pass 30 % slower once a fifth stream existed)."""
-        key = f"{device}/{prio}/{slot}"
+        key = f"{device}/{prio}/{slot}" + (f"/{mask}" if mask != "none" else "")
         if getattr(self, "_streams", None) is None:
             self._streams = {}
         if key not in self._streams:
-            self._streams[key] = torch.cuda.Stream(device=device, priority=prio)
+            self._streams[key] = (self._masked_stream(device, mask) if mask != "none" else
+                                  torch.cuda.Stream(device=device, priority=prio))
         return self._streams[key]
+
+    # The synthesizer (back) stream leaves 32 CUs -- every CU whose mask index is 7 mod 8, i.e. 4 on each XCD --
+    # to the front end (RVC_BACK_CU_MASK: "mod:m:r", "top:n" or "none").  Without it RMVPE's BiGRU, whose 32
+    # workgroups must all be resident to advance (blocks are dealt round-robin over the XCDs: 4 per XCD), waits
+    # for CUs the generator's kernels hold, partly resident and spinning: the clip stream ran 890-1000 xRT from
+    # run to run on one box.  Measured (one box each, 2 runs per setting, interleaved): 4 CUs per XCD left free
+    # 986-990 against 899-1003 unmasked; 8 per XCD 986-989; 2 per XCD 765-768 and 1 per XCD 660 (too few
+    # for the recurrence's workgroups); 32 contiguous mask bits (one XCD's worth) 798-801.  The masked stream is
+    # its own pooled stream, apart from the per-call side stream (sharing it put the per-call RMVPE on 224 CUs
+    # at default priority: 805 -> 650 xRT per call).
+    BACK_CU_MASK = os.environ.get("RVC_BACK_CU_MASK", "mod:8:7")
+
+    @staticmethod
+    def _masked_stream(device, spec):
+        """A stream restricted to part of the chip (BACK_CU_MASK): "top:n" leaves out the last n CUs of the
+        mask, "mod:m:r" every CU whose index is r mod m (rvc_stream_create_cu_mask)."""
+        import ctypes
+        ncu = torch.cuda.get_device_properties(device).multi_processor_count
+        kind, *arg = spec.split(":")
+        keep = [True] * ncu
+        for i in range(ncu):
+            if kind == "top":
+                keep[i] = i < ncu - int(arg[0])
+            elif kind == "mod":
+                keep[i] = i % int(arg[0]) != int(arg[1])
+            else:
+                raise ValueError(f"RVC_BACK_CU_MASK: unknown form {spec!r}")
+        words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
+        for i in range(ncu):
+            if keep[i]:
+                words[i // 32] |= 1 << (i % 32)
+        out = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            ops.check(ops._lib.load().rvc_stream_create_cu_mask(words, len(words), ctypes.byref(out)),
+                      "stream_create_cu_mask")
+        return torch.cuda.ExternalStream(out.value, device=device)
 
     def _side_stream(self, device):
         # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a high-priority
         # stream so that its launches are dispatched ahead of the ContentVec ones: +1.5 % eager (603 ->
         # 612 xRT).  A captured graph runs 17 % slower with it, so ClipGraph sets side_priority = 0.
+        # With the masked synthesizer stream (BACK_CU_MASK) the high-priority side stream would be a fifth stream
+        # on the process's 4 hardware queues, sharing one (per call 805 -> 550 xRT): it is then the clip stream's
+        # fside stream (normal priority), which is idle whenever a per-call pass runs.
+        dflt = "-1" if self.BACK_CU_MASK == "none" else "0"
         prio = self.side_priority if getattr(self, "side_priority", None) is not None \
-            else int(os.environ.get("RVC_AMD_SIDE_PRIORITY", "-1"))
+            else int(os.environ.get("RVC_AMD_SIDE_PRIORITY", dflt))
         return self._pooled_stream(device, prio, self.STREAM_SLOT["side"])
 
     def _pipeline_on_device(self, model, net_g, sid, xp, opt_ts, p_len, pitch, version, protect, index=None,

@@ -29,10 +29,14 @@ N_MELS, N_CLASS, NFFT, HOP = 128, 360, 1024, 160
 EPS = 1e-5
 
 
+# split-K target grid of RMVPE's convs (RVC_RMVPE_SPLITK; unset = the engine's default)
+RMVPE_SPLITK = int(os.environ["RVC_RMVPE_SPLITK"]) if os.environ.get("RVC_RMVPE_SPLITK") else None
+
+
 def _at_precision(fn):
-    """Run a RMVPEAMD stage at the model's own arithmetic (self.precision), whoever calls it."""
+    """Run a RMVPEAMD stage at the model's own arithmetic (self.precision) and split-K policy, whoever calls it."""
     def wrapped(self, *a, **k):
-        with ops.precision(self.precision or ops.get_precision()):
+        with ops.precision(self.precision or ops.get_precision()), ops.splitk_target(RMVPE_SPLITK):
             return fn(self, *a, **k)
     wrapped.__name__, wrapped.__doc__ = fn.__name__, fn.__doc__
     return wrapped
