@@ -481,7 +481,28 @@ class VC:
         with torch.cuda.device(device):
             ops.check(ops._lib.load().rvc_stream_create_cu_mask(words, len(words), ctypes.byref(out)),
                       "stream_create_cu_mask")
+        VC._release_at_exit(device, out.value)
         return torch.cuda.ExternalStream(out.value, device=device)
+
+    _masked = []
+
+    @staticmethod
+    def _release_at_exit(device, handle):
+        """Destroy the library-created streams when the process exits (after their work has finished): left to
+        process teardown, rocprofv3's kernel trace crashed in its finalisation."""
+        if not VC._masked:
+            import atexit
+
+            def release():
+                for dev, h in VC._masked:
+                    try:
+                        torch.cuda.synchronize(dev)
+                        ops._lib.load().rvc_stream_destroy(h)
+                    except Exception:  # noqa: BLE001 -- best effort at exit
+                        pass
+                VC._masked.clear()
+            atexit.register(release)
+        VC._masked.append((device, handle))
 
     def _side_stream(self, device):
         # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a high-priority
