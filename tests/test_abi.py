@@ -140,3 +140,17 @@ def test_f0_file_resample_matches_reference_numpy():
                                      out.size)
         assert n == len(want) and off == 100
         np.testing.assert_array_equal(out[:n], np.asarray(want, np.float64))
+
+
+def test_bench_pass_set_parser():
+    """bench.py reads each split-operand kernel's pass set from its template arguments (torch.profiler names)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench._pass_set("conv_x6_kernel<2, 8, 4, 2, 6, 3, true, false>") == 16
+    assert bench._pass_set("conv_x6_kernel<2, 4, 4, 2, 3, 6, false, true>") == 7
+    assert bench._pass_set("conv_x6_kernel<2, 4, 4, 2, 3, 6, false, false>") == 6
+    assert bench._pass_set("conv_x6_kernel<2, 2, 1, 4, 3, 1, false, false>") == 1
+    assert bench._pass_set("resblock_x6_kernel<64, 6, false>") == 6
+    assert bench._pass_set("resblock_x6_kernel<32, 3, true>") == 16
