@@ -255,6 +255,53 @@ unsigned rvc_bigru_set_spin_limit(unsigned limit);
 /* bigru_batched: B independent sequences (gi + b*gi_bs, y + b*y_bs); gran_ws: 8192 B * min(B, 16) scratch. */
 int rvc_bigru_batched(const float* gi, int64_t gi_bs, const float* whh, const float* bhh, float* y, int64_t y_bs,
                       void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream);
+
+/* ------------------------------------------------------------------ RMVPE in f64 (rmvpe64.hip)
+ * RMVPE's f0 is a per-frame decision (argmax over 360 bins, 0.03 voicing threshold, RMVPE.py:217-252) and
+ * some frames' top two bins lie closer than any f32 evaluation of the network resolves, so the f0 model runs
+ * in f64 end to end (rvc_rmvpe_forward): the same steps as the f32 entry points above, on f64
+ * buffers, with the salience rounded to f32 once.
+ *
+ * conv64: y[b][m][t] = act(sum_{c,k} w[c*K + k][m] x[b][c][t - pad + off(k)] + bias[m]) (+ res[b][m][t]),
+ *   off(k) = toff[k] (ntoff == K) or k; x positions outside [0, Lin) read 0.  w is KM [Ci*K][Co] f64.
+ *   wrap > 0: 2-D mode on zero-bordered images flattened to Lout = rows x wrap -- border cells are stored as 0.
+ *   y is f64, or f32 (rounded once) when y_f32.  out_act: RVC_ACT_* with out_slope (LOGCLAMP's clamp).
+ *   Stride 1, no groups.  Replaces torch.nn.Conv2d (3x3 pad 1 / 1x1) and nn.Linear in E2E / MelSpectrogram
+ *   (RMVPE.py:11-44, 78-107, 141-144, 162-181), batch b in [0, B) with strides (0 = dense). */
+typedef struct rvc_conv64_args {
+    const double* x;
+    const double* w;
+    const double* bias;
+    const double* res;
+    void* y;
+    int64_t B, Ci, Co, Lin, Lout;
+    int64_t x_bstride, y_bstride, res_bstride;
+    int K, pad, out_act, y_f32;
+    double out_slope;
+    int ntoff, wrap;
+    int toff[16];
+} rvc_conv64_args;
+/* split-K workspace (bytes; 0 = none, -1 = bad args), as rvc_conv1d_workspace_bytes */
+int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a);
+int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
+/* stft_mag64: rvc_stft_mag with the f64 magnitudes unrounded */
+int rvc_stft_mag64(const float* x, const float* win, double* mag, int64_t B, int64_t N, int64_t F, int nfft, int hop,
+                   int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream);
+/* f64 forms of rvc_mel_image / avgpool2 / interleave4 / img_to_seq over B images (batch strides, 0 = dense
+ * unused when B == 1); mel_image64 writes only the interior (the caller keeps the border zero). */
+int rvc_mel_image64(const double* mel, double* img, int64_t B, int64_t M, int64_t F, int64_t Tp, double scale,
+                    double shift, int64_t mel_bstride, int64_t img_bstride, rvc_stream_t stream);
+int rvc_avgpool2_64(const double* in, double* out, int64_t B, int64_t C, int64_t H, int64_t W, int64_t in_bstride,
+                    int64_t out_bstride, rvc_stream_t stream);
+int rvc_interleave4_64(const double* phases, double* out, int64_t B, int64_t C, int64_t H, int64_t W,
+                       int64_t ph_bstride, int64_t out_bstride, rvc_stream_t stream);
+int rvc_img_to_seq64(const double* img, double* x, int64_t B, int64_t C, int64_t H, int64_t W, int64_t img_bstride,
+                     int64_t x_bstride, rvc_stream_t stream);
+/* bigru64_batched: rvc_bigru_batched in f64 (gi [2][768][T], whh [2][768][256], bhh [2][768], y [512][T] per
+ * sequence); gran_ws: RVC_BIGRU64_GRAN_BYTES * min(B, 16) scratch (zeroed by the call); err as rvc_bigru. */
+#define RVC_BIGRU64_GRAN_BYTES 16384
+int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double* whh, const double* bhh, double* y,
+                        int64_t y_bs, void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream);
 /* Optional steps of VC.get_f0 between the raw f0 and the mel quantiser (convert.py:311-318), in
  * the reference's order: autotune (Autotune.autotune_f0, convert.py:168-179: f += (nearest of the 54
  * reference notes - f) * strength, first note on ties, unvoiced frames included) on the raw f0, then
@@ -397,7 +444,10 @@ int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T,
  *   rvc_ctx_create / destroy   one context per HIP device (not re-entrant; calls are stream-ordered).
  *   rvc_ctx_set_precision      the conv engine's arithmetic: RVC_PREC_FP32 (default: 6-pass split-bf16
  *                              mixed with split-fp16 where measured faster), _FP32X6, _FP32SA, _F16X3,
- *                              _BF16X3, _BF16.  RMVPE always runs at _FP32SA (rvc_rmvpe_forward).
+ *                              _BF16X3, _BF16.  RMVPE has its own setting (below).
+ *   rvc_ctx_set_rmvpe_precision RMVPE's arithmetic, read by the next rvc_load_rmvpe: RVC_PREC_FP64 (default: the
+ *                              whole network in f64, rmvpe64.hip -- the f0 decisions of the exact model) or a
+ *                              conv precision above for the f32 form (_FP32SA: round 3's split-accumulator convs).
  *   rvc_load_synth             params = the .pth "weight" dict (train.py:729-742) as named HOST arrays,
  *                              f32 or f16; weight-norm pairs (x.weight_g / x.weight_v) are folded at load
  *                              (torch._weight_norm, dim 0), already-folded x.weight is taken as is.
@@ -411,7 +461,7 @@ typedef struct rvc_ctx rvc_ctx;
 
 enum { RVC_DT_F32 = 0, RVC_DT_F16 = 1, RVC_DT_F64 = 2 };
 enum { RVC_PREC_FP32 = 0, RVC_PREC_BF16 = 1, RVC_PREC_BF16X3 = 3, RVC_PREC_FP32X6 = 6, RVC_PREC_FP32SA = 7,
-       RVC_PREC_F16X3 = 16 };
+       RVC_PREC_F16X3 = 16, RVC_PREC_FP64 = 64 };
 
 typedef struct rvc_param {
     const char* name;  /* state-dict key, e.g. "dec.ups.0.weight_v" */
@@ -436,6 +486,7 @@ typedef struct rvc_synth_cfg { /* the checkpoint's "config" list (train.py:729-7
 int rvc_ctx_create(int hip_device, rvc_ctx** out);
 void rvc_ctx_destroy(rvc_ctx* ctx);
 int rvc_ctx_set_precision(rvc_ctx* ctx, int prec);
+int rvc_ctx_set_rmvpe_precision(rvc_ctx* ctx, int prec);
 int rvc_load_synth(rvc_ctx* ctx, const rvc_param* params, int n, const rvc_synth_cfg* cfg);
 int64_t rvc_synth_out_len(const rvc_ctx* ctx, int64_t T);
 int rvc_synth_infer(rvc_ctx* ctx, const float* phone, const int64_t* pitch, const float* pitchf, int64_t B, int64_t T,

@@ -46,6 +46,7 @@ struct VcState;
 struct rvc_ctx {
     int device = 0;
     int prec = RVC_PREC_FP32;
+    int rm_prec = RVC_PREC_FP64;  // RMVPE's arithmetic (rvc_ctx_set_rmvpe_precision), read by rvc_load_rmvpe
     bool x6 = true, f16mix = true, fused_rb = true;  // RVC_AMD_X6 / RVC_AMD_F16MIX / RVC_AMD_FUSED_RB as ops.py
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
@@ -303,8 +304,6 @@ inline int ensure_ws(ModelBase& m, int64_t need, hipStream_t s) {
     }
     const int64_t bytes = need + (4 << 20);
     MHIP(hipMalloc(&m.ws, bytes));
-    // the conv engine's split-K arrival counters start at zero -- ordered on s, before the launch that uses it
-    MHIP(hipMemsetAsync(m.ws, 0, bytes, s));
     m.ws_bytes = bytes;
     return RVC_OK;
 }

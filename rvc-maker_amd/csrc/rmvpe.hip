@@ -57,7 +57,8 @@ extern "C" int rvc_spec_mag(const float* spec, float* mag, int64_t K, int64_t F,
 // stored STFT_FPB consecutive frames at a time.
 constexpr int STFT_NMAX = 1024, STFT_FPB = 8;
 
-__global__ __launch_bounds__(256) void stft_mag_kernel(const float* x, const float* win, float* mag, int64_t N,
+template <typename TO>
+__global__ __launch_bounds__(256) void stft_mag_kernel(const float* x, const float* win, TO* mag, int64_t N,
                                                        int64_t F, int nfft, int logn, int hop, int64_t x_bs,
                                                        int64_t m_bs) {
     __shared__ double2 a[STFT_FPB][STFT_NMAX];
@@ -100,29 +101,41 @@ __global__ __launch_bounds__(256) void stft_mag_kernel(const float* x, const flo
         __syncthreads();
     }
     const int K = nfft / 2 + 1;
-    float* mb = mag + b * m_bs;
+    TO* mb = mag + b * m_bs;
     for (int i = threadIdx.x; i < K * STFT_FPB; i += blockDim.x) {
         const int k = i / STFT_FPB, q = i - k * STFT_FPB;
         const int64_t f = f0 + q;
         if (f < F) {
             const double2 v = a[q][k];
-            mb[(int64_t)k * F + f] = (float)sqrt(v.x * v.x + v.y * v.y);
+            mb[(int64_t)k * F + f] = (TO)sqrt(v.x * v.x + v.y * v.y);
         }
     }
 }
 
-extern "C" int rvc_stft_mag(const float* x, const float* win, float* mag, int64_t B, int64_t N, int64_t F,
-                            int nfft, int hop, int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream) {
+template <typename TO>
+static int stft_mag_launch(const float* x, const float* win, TO* mag, int64_t B, int64_t N, int64_t F, int nfft, int hop,
+                           int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream) {
     int logn = 0;
     while ((1 << logn) < nfft) ++logn;
     RVC_CHECK_ARG(x && win && mag && B > 0 && N > nfft / 2 && F > 0 && hop > 0, "stft_mag: bad args");
     RVC_CHECK_ARG((1 << logn) == nfft && nfft >= 2 && nfft <= STFT_NMAX, "stft_mag: nfft must be a power of 2 <= 1024");
     RVC_CHECK_ARG((F - 1) * hop <= 2 * (N - 1), "stft_mag: F too large for reflect padding");
     RVC_CHECK_ARG(B == 1 || (x_bstride >= N && mag_bstride >= (int64_t)(nfft / 2 + 1) * F), "stft_mag: bad batch strides");
-    hipLaunchKernelGGL(stft_mag_kernel, dim3(cdiv(F, STFT_FPB), (unsigned)B), dim3(256), 0, (hipStream_t)stream, x,
+    hipLaunchKernelGGL(stft_mag_kernel<TO>, dim3(cdiv(F, STFT_FPB), (unsigned)B), dim3(256), 0, (hipStream_t)stream, x,
                        win, mag, N, F, nfft, logn, hop, x_bstride, mag_bstride);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
+}
+
+extern "C" int rvc_stft_mag(const float* x, const float* win, float* mag, int64_t B, int64_t N, int64_t F,
+                            int nfft, int hop, int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream) {
+    return stft_mag_launch<float>(x, win, mag, B, N, F, nfft, hop, x_bstride, mag_bstride, stream);
+}
+
+// the same magnitudes unrounded (the f64 RMVPE, rmvpe64.hip)
+extern "C" int rvc_stft_mag64(const float* x, const float* win, double* mag, int64_t B, int64_t N, int64_t F,
+                              int nfft, int hop, int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream) {
+    return stft_mag_launch<double>(x, win, mag, B, N, F, nfft, hop, x_bstride, mag_bstride, stream);
 }
 
 // ---------------------------------------------------------------- U-Net input image

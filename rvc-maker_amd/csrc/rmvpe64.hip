@@ -1,0 +1,613 @@
+// RMVPE in f64 (main/library/predictors/RMVPE.py): the f0 is a per-frame decision -- argmax over 360 salience
+// bins and a 0.03 voicing threshold (RMVPE.py:217-252) -- and on real inputs a few frames per clip have their
+// top two bins closer than any f32 evaluation of the network resolves (3.2e-6 apart on the headline clip, while
+// f32 evaluations -- the reference's own at other thread counts among them -- err by up to 1.7e-4).  So the
+// whole network runs in f64 here: mel (f64 STFT, f64 mel GEMM + log), the U-Net convs on the f64 matrix cores
+// (v_mfma_f64_16x16x4_f64), pooling / transposed-conv phases / image->sequence in f64, W_ih, the BiGRU
+// recurrence and the classifier in f64; only the salience is rounded to f32, once, for the decode (which is
+// what the reference decodes: RMVPE.py:217).  Against the exact model the salience then errs by ~1e-13 and the
+// only remaining difference is the f32 input rounding the reference itself applies (RMVPE.py:224: <= 1.4e-7 on
+// the decision quantities of the headline clip).
+//
+// conv64_kernel: implicit GEMM Y[m][n] = sum_k W[k][m] X(k, n) over k = (input channel, tap), for the 3x3 /
+// 1x1 convs on zero-bordered images ([C][H+2][W+2] flattened; tap offsets, border cells stored as 0) and the
+// K = 1 GEMMs (mel basis, W_ih, fc).  A block is 4 waves; per 16-deep k chunk the weights [16][BM] and the
+// input rows the chunk touches (with their tap halo) are staged into a double-buffered LDS tile, the next
+// chunk's global loads in flight across the current chunk's MFMAs, one barrier per chunk.  An f64 MFMA is 64
+// cycles, so the staging work per chunk is small beside the 4 x FM x FN MFMAs it feeds.
+#include "rvc_common.h"
+#include <stdlib.h>
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+// v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4], B[l>>4][l&15]; C/D: col = l&15, row = (l>>4) + 4 r
+RVC_DEV doublex4 mfma64(double a, double b, doublex4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+
+RVC_DEV double act64(double v, int act, double slope) {
+    switch (act) {
+        case RVC_ACT_LRELU: return v >= 0.0 ? v : v * slope;
+        case RVC_ACT_RELU: return v > 0.0 ? v : 0.0;
+        case RVC_ACT_TANH: return tanh(v);
+        case RVC_ACT_GELU: return 0.5 * v * (1.0 + erf(v * 0.70710678118654752440));
+        case RVC_ACT_SIGMOID: return 1.0 / (1.0 + exp(-v));
+        case RVC_ACT_LOGCLAMP: return log(fmax(v, slope));
+        default: return v;
+    }
+}
+
+constexpr int KC = 16;  // flattened k per chunk (4 MFMA k-steps)
+
+// staged input doubles per thread (rows * span <= 256 * NB): 12 for the 512-column tile (3 channel rows of a
+// 3x3 conv's 774-wide span), 8 otherwise (a K = 1 chunk's 16 rows of 128)
+template <int BN>
+constexpr int nb64() { return BN >= 512 ? 12 : 8; }
+
+struct C64 {
+    const double* x;
+    const double* w;
+    const double* bias;
+    const double* res;
+    double* y;
+    float* yf;
+    double* ws;  // split-K partials [ksplit][B][Co][Lout]
+    int64_t B, Ci, Co, Lin, Lout;
+    int64_t x_bs, y_bs, res_bs;
+    int K, pad, out_act, wrap;
+    double out_slope;
+    int ntoff;
+    int toff[16];
+    int span, span_s, rows_max, ksplit, cps;  // cps = chunks per split
+};
+
+RVC_DEV int tap64(const C64& p, int t) { return p.ntoff ? p.toff[t] : t; }
+
+// output position n -> n, -1 (beyond Lout) or -(n + 2) for a border cell of a 2-D image (stored as 0)
+RVC_DEV int opos64(const C64& p, int n) {
+    if (n >= (int)p.Lout) return -1;
+    if (p.wrap) {
+        const int row = n / p.wrap, col = n - row * p.wrap;
+        if (col == 0 || col == p.wrap - 1 || row == 0 || row == (int)p.Lout / p.wrap - 1) return -(n + 2);
+    }
+    return n;
+}
+
+RVC_DEV void store64(const C64& p, double acc, int b, int m, int t) {
+    if (t == -1) return;
+    const int64_t o = (int64_t)m * p.Lout + (t >= 0 ? t : -t - 2);
+    double v = 0.0;
+    if (t >= 0) {
+        v = acc;
+        if (p.bias) v += p.bias[m];
+        v = act64(v, p.out_act, p.out_slope);
+        if (p.res) v += p.res[b * p.res_bs + o];
+    }
+    if (p.yf) p.yf[b * p.y_bs + o] = (float)v;
+    else p.y[b * p.y_bs + o] = v;
+}
+
+template <int FM, int FN, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
+    constexpr int BM = 16 * FM * WM;
+    constexpr int BN = 16 * FN * WN;
+    constexpr int NB64 = nb64<BN>();
+    constexpr int WS = BM + 4;            // weight tile row pitch (doubles)
+    constexpr int NA = KC * BM / 256;     // weight doubles staged per thread
+    static_assert(WM * WN == 4 && NA >= 1 && (KC * BM) % 256 == 0, "tile");
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int xs_n = p.rows_max * p.span_s;
+    double* Wsb = sm;                       // [2][KC][WS]
+    double* Xsb = sm + 2 * KC * WS;         // [2][xs_n]
+    int* koffb = (int*)(Xsb + 2 * xs_n);    // [2][KC]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int split = blockIdx.z % p.ksplit, b = blockIdx.z / p.ksplit;
+    const int m0 = blockIdx.y * BM;
+    const int n0 = blockIdx.x * BN;
+    const int Co = (int)p.Co, Ci = (int)p.Ci, K = p.K;
+    const double* xb = p.x + b * p.x_bs;
+    const int kmax = Ci * K;
+    const int nch = (kmax + KC - 1) / KC;
+    const int ch_beg = split * p.cps;
+    const int ch_end = min(nch, ch_beg + p.cps);
+    const int base = n0 - p.pad;
+    const int lin = (int)p.Lin;
+
+    // per-thread staging slots of the rows x span input tile (the same for every chunk)
+    int bslot[NB64];
+    unsigned bok = 0;
+#pragma unroll
+    for (int i = 0; i < NB64; ++i) {
+        const int idx = tid + 256 * i;
+        const int r = idx / p.span, j = idx - r * p.span;
+        bslot[i] = (r << 16) | j;
+        bok |= (unsigned)(base + j >= 0 && base + j < lin) << i;
+    }
+    double ra[NA], rb[NB64];
+    // raw loads only (clamped addresses): the values are first used by sstore, after the chunk's MFMAs
+    auto gload = [&](int ch) {
+        const int k0 = ch * KC;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int idx = tid + 256 * i;
+            const int kk = idx / BM, m = idx % BM;
+            const bool ok = k0 + kk < kmax && m0 + m < Co;
+            ra[i] = p.w[ok ? (int64_t)(k0 + kk) * Co + m0 + m : 0];
+        }
+        const int c_lo = k0 / K;
+        const int rows = min((k0 + KC - 1) / K, Ci - 1) - c_lo + 1;
+        const int n = rows * p.span;
+        const int rbase = c_lo * lin + base;
+#pragma unroll
+        for (int g = 0; g < NB64; g += 4) {
+            if (g * 256 < n) {
+#pragma unroll
+                for (int i = g; i < g + 4; ++i) {
+                    const int r = bslot[i] >> 16, j = bslot[i] & 0xffff;
+                    const bool ok = r < rows && ((bok >> i) & 1u);
+                    rb[i] = xb[ok ? rbase + r * lin + j : 0];
+                }
+            }
+        }
+    };
+    auto sstore = [&](int ch, int buf) {
+        const int k0 = ch * KC;
+        double* Ws = Wsb + buf * KC * WS;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int idx = tid + 256 * i;
+            const int kk = idx / BM, m = idx % BM;
+            const bool ok = k0 + kk < kmax && m0 + m < Co;
+            Ws[kk * WS + m] = ok ? ra[i] : 0.0;
+        }
+        const int c_lo = k0 / K;
+        const int rows = min((k0 + KC - 1) / K, Ci - 1) - c_lo + 1;
+        const int n = rows * p.span;
+        double* Xs = Xsb + buf * xs_n;
+#pragma unroll
+        for (int g = 0; g < NB64; g += 4) {
+            if (g * 256 < n) {
+#pragma unroll
+                for (int i = g; i < g + 4; ++i) {
+                    const int r = bslot[i] >> 16, j = bslot[i] & 0xffff;
+                    const bool ok = r < rows && ((bok >> i) & 1u);
+                    if (tid + 256 * i < n) Xs[r * p.span_s + j] = ok ? rb[i] : 0.0;
+                }
+            }
+        }
+        if (tid < KC) {
+            const int kk = k0 + tid;
+            const int c = kk / K, t = kk - c * K;
+            koffb[buf * KC + tid] = kk < kmax ? (c - c_lo) * p.span_s + tap64(p, t) : 0;
+        }
+    };
+
+    doublex4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+
+    const int lk = lane >> 4, ln = lane & 15;
+    if (ch_beg < ch_end) {
+        gload(ch_beg);
+        sstore(ch_beg, 0);
+    }
+    __syncthreads();
+    for (int ch = ch_beg; ch < ch_end; ++ch) {
+        const int cur = (ch - ch_beg) & 1;
+        const bool more = ch + 1 < ch_end;
+        if (more) gload(ch + 1);
+        const double* Ws = Wsb + cur * KC * WS + wm * 16 * FM + ln;
+        const double* Xs = Xsb + cur * xs_n + wn * 16 * FN + ln;
+        const int* ko = koffb + cur * KC;
+#pragma unroll
+        for (int ks = 0; ks < KC / 4; ++ks) {
+            const int kk = ks * 4 + lk;
+            double a[FM], bv[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) a[i] = Ws[kk * WS + i * 16];
+            const double* xr = Xs + ko[kk];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) bv[j] = xr[j * 16];
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j] = mfma64(a[i], bv[j], acc[i][j]);
+        }
+        if (more) sstore(ch + 1, cur ^ 1);
+        __syncthreads();
+    }
+
+    if (p.ksplit > 1) {
+        double* wsb = p.ws + ((int64_t)split * p.B + b) * p.Co * p.Lout;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * 16 * FM + i * 16 + lk + 4 * r;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int n = n0 + wn * 16 * FN + j * 16 + ln;
+                    if (m < Co && n < (int)p.Lout) wsb[(int64_t)m * p.Lout + n] = acc[i][j][r];
+                }
+            }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int t = opos64(p, n0 + wn * 16 * FN + j * 16 + ln);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * 16 * FM + i * 16 + lk + 4 * r;
+                if (m < Co) store64(p, acc[i][j][r], b, m, t);
+            }
+    }
+}
+
+// split-K: the partials summed in split order, then the epilogue
+__global__ void conv64_splitk_reduce(C64 p) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = blockIdx.y, b = blockIdx.z;
+    if (n >= (int)p.Lout) return;
+    const int64_t sstride = p.B * p.Co * p.Lout;
+    const double* src = p.ws + ((int64_t)b * p.Co + m) * p.Lout + n;
+    double s = 0.0;
+    for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
+    store64(p, s, b, m, opos64(p, n));
+}
+
+struct Cfg64 {
+    int FM, FN, WM, WN;
+};
+
+int plan64(const rvc_conv64_args* a, C64& p, Cfg64& cfg, dim3& grid, size_t& lds) {
+    RVC_CHECK_ARG(a && a->x && a->w && a->y, "conv64: null pointer");
+    RVC_CHECK_ARG(a->B > 0 && a->Ci > 0 && a->Co > 0 && a->K > 0 && a->Lin > 0 && a->Lout > 0,
+                  "conv64: bad sizes B=%lld Ci=%lld Co=%lld K=%d Lin=%lld Lout=%lld", (long long)a->B,
+                  (long long)a->Ci, (long long)a->Co, a->K, (long long)a->Lin, (long long)a->Lout);
+    RVC_CHECK_ARG(a->Co * a->Lout < (1ll << 31) && a->Ci * a->Lin < (1ll << 31) && a->Lin + a->pad < (1ll << 30) &&
+                      a->pad >= 0 && a->Ci * a->K < (1ll << 30),
+                  "conv64: per-batch tensor exceeds 2^31 elements (use the batch dimension)");
+    RVC_CHECK_ARG(a->ntoff == 0 || (a->ntoff == a->K && a->K <= 16), "conv64: toff needs ntoff == K <= 16");
+    RVC_CHECK_ARG(a->wrap == 0 || (a->wrap >= 3 && a->Lout % a->wrap == 0), "conv64: Lout must be rows x wrap");
+    int maxoff = a->ntoff ? 0 : a->K - 1;
+    for (int i = 0; i < a->ntoff; ++i) {
+        RVC_CHECK_ARG(a->toff[i] >= 0, "conv64: negative tap offset");
+        maxoff = a->toff[i] > maxoff ? a->toff[i] : maxoff;
+    }
+    p.x = a->x; p.w = a->w; p.bias = a->bias; p.res = a->res;
+    p.y = a->y_f32 ? nullptr : (double*)a->y;
+    p.yf = a->y_f32 ? (float*)a->y : nullptr;
+    p.ws = nullptr;
+    p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout;
+    p.x_bs = a->x_bstride ? a->x_bstride : a->Ci * a->Lin;
+    p.y_bs = a->y_bstride ? a->y_bstride : a->Co * a->Lout;
+    p.res_bs = a->res_bstride ? a->res_bstride : a->Co * a->Lout;
+    p.K = a->K; p.pad = a->pad; p.out_act = a->out_act; p.wrap = a->wrap; p.out_slope = a->out_slope;
+    p.ntoff = a->ntoff;
+    for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff && i < a->ntoff ? a->toff[i] : 0;
+
+    if (a->Co <= 16) cfg = {1, 8, 1, 4};       // 16 x 512
+    else if (a->Co <= 32) cfg = {2, 4, 1, 4};  // 32 x 256
+    else if (a->Co <= 64) cfg = {2, 4, 2, 2};  // 64 x 128
+    else cfg = {4, 4, 2, 2};                   // 128 x 128
+    int rows_max = (KC % a->K == 0) ? KC / a->K : (KC - 1) / a->K + 2;
+    if (rows_max > a->Ci) rows_max = (int)a->Ci;
+    int BN = 16 * cfg.FN * cfg.WN;
+    // a wide tile whose staged rows x span exceed its per-thread budget (K = 1 / 2-tap convs over many rows)
+    // takes the 64 x 128 tile instead
+    if ((int64_t)rows_max * (BN + maxoff) > 256 * (BN >= 512 ? 12 : 8)) {
+        cfg = {2, 4, 2, 2};
+        BN = 128;
+    }
+    const int BM = 16 * cfg.FM * cfg.WM;
+    p.span = BN + maxoff;
+    p.span_s = p.span + 1;
+    p.rows_max = rows_max;
+    RVC_CHECK_ARG((int64_t)rows_max * p.span <= 256 * 8 && p.span < 65536 || (BN >= 512 && rows_max * p.span <= 256 * 12),
+                  "conv64: staged tile too large (rows %d x span %d)", rows_max, p.span);
+    const int mt = (int)((a->Co + BM - 1) / BM);
+    const int64_t tiles = (int64_t)mt * cdiv(a->Lout, BN) * a->B;
+    const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
+    // split-K while the grid underfills the chip (2 blocks per CU): the partials go to a workspace and are
+    // summed in split order by conv64_splitk_reduce
+    static const int target = getenv("RVC_C64_SPLITK_TILES") ? atoi(getenv("RVC_C64_SPLITK_TILES")) : 512;
+    int ks = 1;
+    if (tiles < target && nch >= 4) {
+        ks = (int)((target + tiles - 1) / tiles);
+        if (ks > 16) ks = 16;
+        if (ks > nch / 2) ks = nch / 2;
+        if (ks < 1) ks = 1;
+    }
+    p.cps = (nch + ks - 1) / ks;
+    p.ksplit = (nch + p.cps - 1) / p.cps;
+    const int WS = BM + 4;
+    lds = (size_t)(2 * KC * WS + 2 * rows_max * p.span_s) * 8 + 2 * KC * 4;
+    RVC_CHECK_ARG(lds <= 160 * 1024, "conv64: LDS %zu too large", lds);
+    grid = dim3(cdiv(a->Lout, BN), (unsigned)mt, (unsigned)(a->B * p.ksplit));
+    RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv64: grid too large");
+    return RVC_OK;
+}
+
+template <int FM, int FN, int WM, int WN>
+void launch64(const C64& p, dim3 grid, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((conv64_kernel<FM, FN, WM, WN>), grid, dim3(256), lds, s, p);
+}
+
+// ---------------------------------------------------------------- f64 image / sequence glue (rmvpe.hip's f32 forms)
+__global__ void mel_image64_kernel(const double* mel, double* img, int M, int64_t F, int64_t Tp, double scale,
+                                   double shift, int64_t mel_bs, int64_t img_bs) {
+    const int64_t t = blockIdx.x;
+    const int m = threadIdx.x;
+    mel += blockIdx.y * mel_bs;
+    img += blockIdx.y * img_bs;
+    if (t >= Tp || m >= M) return;
+    const int64_t s = t < F ? t : 2 * (F - 1) - t;
+    img[(t + 1) * (M + 2) + m + 1] = mel[(int64_t)m * F + s] * scale + shift;
+}
+
+// AvgPool2d(2): ((a + b) + c) + d, / 4
+__global__ void avgpool2_64_kernel(const double* in, double* out, int C, int H, int W, int64_t in_bs, int64_t out_bs) {
+    const int Ho = H / 2, Wo = W / 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    in += blockIdx.y * in_bs;
+    out += blockIdx.y * out_bs;
+    if (i >= (int64_t)C * Ho * Wo) return;
+    const int x = (int)(i % Wo);
+    const int64_t r = i / Wo;
+    const int y = (int)(r % Ho), c = (int)(r / Ho);
+    const double* ib = in + (int64_t)c * (H + 2) * (W + 2);
+    const int64_t a0 = (int64_t)(2 * y + 1) * (W + 2) + 2 * x + 1;
+    double s = ib[a0];
+    s += ib[a0 + 1];
+    s += ib[a0 + W + 2];
+    s += ib[a0 + W + 3];
+    out[(int64_t)c * (Ho + 2) * (Wo + 2) + (int64_t)(y + 1) * (Wo + 2) + x + 1] = s / 4.0;
+}
+
+__global__ void interleave4_64_kernel(const double* ph, double* out, int C, int H, int W, int64_t ph_bs,
+                                      int64_t out_bs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int Ho = 2 * H, Wo = 2 * W;
+    ph += blockIdx.y * ph_bs;
+    out += blockIdx.y * out_bs;
+    if (i >= (int64_t)C * Ho * Wo) return;
+    const int xo = (int)(i % Wo);
+    const int64_t r = i / Wo;
+    const int yo = (int)(r % Ho), c = (int)(r / Ho);
+    const int py = yo & 1, px = xo & 1, y = yo >> 1, x = xo >> 1;
+    const int64_t plane = (int64_t)(H + 2) * (W + 2);
+    out[(int64_t)c * (Ho + 2) * (Wo + 2) + (int64_t)(yo + 1) * (Wo + 2) + xo + 1] =
+        ph[((int64_t)(py * 2 + px) * C + c) * plane + (int64_t)(y + 1) * (W + 2) + x + 1];
+}
+
+__global__ void img_to_seq64_kernel(const double* img, double* x, int C, int64_t H, int W, int64_t img_bs,
+                                    int64_t x_bs) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int cf = blockIdx.y;
+    img += blockIdx.z * img_bs;
+    x += blockIdx.z * x_bs;
+    if (t >= H) return;
+    const int c = cf / W, f = cf - c * W;
+    x[(int64_t)cf * H + t] = img[(int64_t)c * (H + 2) * (W + 2) + (t + 1) * (W + 2) + f + 1];
+}
+
+// ---------------------------------------------------------------- f64 bidirectional GRU recurrence
+// rmvpe.hip's bigru_kernel in f64: 16 workgroups per direction, 16 hidden units each, W_hh rows in registers
+// (48 doubles per thread); h is exchanged every step as two 8-byte {tag, 32-bit half} granules per unit
+// (lo, hi), double-buffered by step parity; a reader takes a unit's value once both halves carry the step's
+// tag.  Every spin is bounded; a timeout sets *err and the kernel drains.
+constexpr int G_H = 256;
+constexpr int G_WG = 16;
+
+__global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const double* whh, const double* bhh,
+                                                      double* y, unsigned long long* gran, int* err, int64_t T,
+                                                      unsigned spin_limit, int64_t gi_bs, int64_t y_bs) {
+    gi += (int64_t)blockIdx.y * gi_bs;
+    y += (int64_t)blockIdx.y * y_bs;
+    gran += (int64_t)blockIdx.y * 2 * 2 * G_H * 2;
+    const int d = blockIdx.x / G_WG;
+    const int j = blockIdx.x % G_WG;
+    const int tid = threadIdx.x;
+    const int ul = tid >> 4, s = tid & 15;
+    const int u = j * 16 + ul;
+    __shared__ double hs[2][G_H];
+    __shared__ int abort_flag;
+    if (tid == 0) abort_flag = 0;
+    const double* W = whh + (int64_t)d * 3 * G_H * G_H;
+    double wr[16], wz[16], wn[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        wr[i] = W[(int64_t)u * G_H + 16 * s + i];
+        wz[i] = W[(int64_t)(G_H + u) * G_H + 16 * s + i];
+        wn[i] = W[(int64_t)(2 * G_H + u) * G_H + 16 * s + i];
+    }
+    const double bhr = bhh[d * 3 * G_H + u], bhz = bhh[d * 3 * G_H + G_H + u], bhn = bhh[d * 3 * G_H + 2 * G_H + u];
+    const double* G = gi + (int64_t)d * 3 * G_H * T;
+    unsigned long long* GR = gran + (int64_t)d * 2 * G_H * 2;  // [parity][unit][lo, hi]
+    double hprev = 0.0;
+    double gxr = 0.0, gxz = 0.0, gxn = 0.0;
+    if (s == 0) {
+        const int64_t tau0 = d ? T - 1 : 0;
+        gxr = G[(int64_t)u * T + tau0];
+        gxz = G[(int64_t)(G_H + u) * T + tau0];
+        gxn = G[(int64_t)(2 * G_H + u) * T + tau0];
+    }
+    hs[0][tid] = 0.0;
+    __syncthreads();
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t tau = d ? T - 1 - t : t;
+        const int cur = (int)(t & 1);
+        if (t > 0) {
+            unsigned long long* g = GR + ((t - 1) & 1) * G_H * 2 + 2 * tid;
+            unsigned long long v0 = 0, v1 = 0;
+            bool ok0 = false, ok1 = false;
+            unsigned spins = 0;
+            for (;;) {
+                if (!ok0) {
+                    v0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok0 = (uint32_t)(v0 >> 32) == (uint32_t)t;
+                }
+                if (!ok1) {
+                    v1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok1 = (uint32_t)(v1 >> 32) == (uint32_t)t;
+                }
+                if (ok0 && ok1) break;
+                if (++spins > spin_limit) {
+                    atomicExch(err, 1);
+                    abort_flag = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            hs[cur][tid] = __hiloint2double((int)(uint32_t)v1, (int)(uint32_t)v0);
+            __syncthreads();
+            if (abort_flag) break;
+        }
+        double nxr = 0.0, nxz = 0.0, nxn = 0.0;
+        if (s == 0 && t + 1 < T) {
+            const int64_t tn = d ? T - 2 - t : t + 1;
+            nxr = G[(int64_t)u * T + tn];
+            nxz = G[(int64_t)(G_H + u) * T + tn];
+            nxn = G[(int64_t)(2 * G_H + u) * T + tn];
+        }
+        double pr = 0.0, pz = 0.0, pn = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const double h = hs[cur][16 * s + i];
+            pr += wr[i] * h;
+            pz += wz[i] * h;
+            pn += wn[i] * h;
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            pr += __shfl_xor(pr, o, 64);
+            pz += __shfl_xor(pz, o, 64);
+            pn += __shfl_xor(pn, o, 64);
+        }
+        if (s == 0) {
+            const double r = 1.0 / (1.0 + exp(-(gxr + (pr + bhr))));
+            const double z = 1.0 / (1.0 + exp(-(gxz + (pz + bhz))));
+            const double n = tanh(gxn + r * (pn + bhn));
+            const double h = (hprev - n) * z + n;
+            hprev = h;
+            const unsigned long long tag = (unsigned long long)(uint32_t)(t + 1) << 32;
+            unsigned long long* o = GR + (t & 1) * G_H * 2 + 2 * u;
+            __hip_atomic_store(o, tag | (uint32_t)__double2loint(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 1, tag | (uint32_t)__double2hiint(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            y[(int64_t)(d * G_H + u) * T + tau] = h;
+        }
+        gxr = nxr;
+        gxz = nxz;
+        gxn = nxn;
+    }
+}
+
+constexpr int G_B_MAX = 16;  // sequences per launch (32 co-resident workgroups each)
+
+}  // namespace
+
+extern "C" int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a) {
+    C64 p;
+    Cfg64 cfg;
+    dim3 grid;
+    size_t lds;
+    if (plan64(a, p, cfg, grid, lds) != RVC_OK) return -1;
+    return p.ksplit > 1 ? (int64_t)p.ksplit * p.B * p.Co * p.Lout * 8 : 0;
+}
+
+extern "C" int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
+    C64 p;
+    Cfg64 cfg;
+    dim3 grid;
+    size_t lds;
+    const int rc = plan64(a, p, cfg, grid, lds);
+    if (rc != RVC_OK) return rc;
+    if (p.ksplit > 1) {
+        const int64_t need = (int64_t)p.ksplit * p.B * p.Co * p.Lout * 8;
+        RVC_CHECK_ARG(ws && ws_bytes >= need, "conv64: split-K needs %lld B of workspace (got %lld)", (long long)need,
+                      (long long)ws_bytes);
+        p.ws = (double*)ws;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (cfg.FM == 1) launch64<1, 8, 1, 4>(p, grid, lds, s);
+    else if (cfg.WM == 1) launch64<2, 4, 1, 4>(p, grid, lds, s);
+    else if (cfg.FM == 2) launch64<2, 4, 2, 2>(p, grid, lds, s);
+    else launch64<4, 4, 2, 2>(p, grid, lds, s);
+    RVC_HIP(hipGetLastError());
+    if (p.ksplit > 1) {
+        hipLaunchKernelGGL(conv64_splitk_reduce, dim3(cdiv(p.Lout, 256), (unsigned)p.Co, (unsigned)p.B), dim3(256), 0,
+                           s, p);
+        RVC_HIP(hipGetLastError());
+    }
+    return RVC_OK;
+}
+
+extern "C" int rvc_mel_image64(const double* mel, double* img, int64_t B, int64_t M, int64_t F, int64_t Tp,
+                               double scale, double shift, int64_t mel_bstride, int64_t img_bstride,
+                               rvc_stream_t stream) {
+    RVC_CHECK_ARG(mel && img && B > 0 && M > 0 && M <= 1024 && F > 1 && Tp >= F && Tp - F < F, "mel_image64: bad args");
+    RVC_CHECK_ARG(B == 1 || (mel_bstride >= M * F && img_bstride >= (Tp + 2) * (M + 2)), "mel_image64: bad strides");
+    hipLaunchKernelGGL(mel_image64_kernel, dim3((unsigned)Tp, (unsigned)B), dim3((unsigned)((M + 63) / 64 * 64)), 0,
+                       (hipStream_t)stream, mel, img, (int)M, F, Tp, scale, shift, mel_bstride, img_bstride);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+extern "C" int rvc_avgpool2_64(const double* in, double* out, int64_t B, int64_t C, int64_t H, int64_t W,
+                               int64_t in_bstride, int64_t out_bstride, rvc_stream_t stream) {
+    RVC_CHECK_ARG(in && out && B > 0 && C > 0 && H >= 2 && W >= 2, "avgpool2_64: bad args");
+    RVC_CHECK_ARG(B == 1 || (in_bstride >= C * (H + 2) * (W + 2) && out_bstride >= C * (H / 2 + 2) * (W / 2 + 2)),
+                  "avgpool2_64: bad strides");
+    const int64_t n = C * (H / 2) * (W / 2);
+    hipLaunchKernelGGL(avgpool2_64_kernel, dim3(cdiv(n, 256), (unsigned)B), dim3(256), 0, (hipStream_t)stream, in, out,
+                       (int)C, (int)H, (int)W, in_bstride, out_bstride);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+extern "C" int rvc_interleave4_64(const double* phases, double* out, int64_t B, int64_t C, int64_t H, int64_t W,
+                                  int64_t ph_bstride, int64_t out_bstride, rvc_stream_t stream) {
+    RVC_CHECK_ARG(phases && out && B > 0 && C > 0 && H > 0 && W > 0, "interleave4_64: bad args");
+    RVC_CHECK_ARG(B == 1 || (ph_bstride >= 4 * C * (H + 2) * (W + 2) && out_bstride >= C * (2 * H + 2) * (2 * W + 2)),
+                  "interleave4_64: bad strides");
+    const int64_t n = C * 4 * H * W;
+    hipLaunchKernelGGL(interleave4_64_kernel, dim3(cdiv(n, 256), (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                       phases, out, (int)C, (int)H, (int)W, ph_bstride, out_bstride);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+extern "C" int rvc_img_to_seq64(const double* img, double* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                                int64_t img_bstride, int64_t x_bstride, rvc_stream_t stream) {
+    RVC_CHECK_ARG(img && x && B > 0 && B < 65536 && C > 0 && H > 0 && W > 0, "img_to_seq64: bad args");
+    RVC_CHECK_ARG(B == 1 || (img_bstride >= C * (H + 2) * (W + 2) && x_bstride >= C * W * H),
+                  "img_to_seq64: bad strides");
+    hipLaunchKernelGGL(img_to_seq64_kernel, dim3(cdiv(H, 256), (unsigned)(C * W), (unsigned)B), dim3(256), 0,
+                       (hipStream_t)stream, img, x, (int)C, H, (int)W, img_bstride, x_bstride);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+extern "C" unsigned rvc_bigru_set_spin_limit(unsigned limit);
+
+extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double* whh, const double* bhh, double* y,
+                                   int64_t y_bs, void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream) {
+    RVC_CHECK_ARG(gi && whh && bhh && y && gran_ws && err && T > 0 && T < (1ll << 31) && B > 0, "bigru64: bad args");
+    RVC_CHECK_ARG(B == 1 || (gi_bs >= 2 * 3 * G_H * T && y_bs >= 2 * G_H * T), "bigru64: batch strides too small");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned spin = rvc_bigru_set_spin_limit(0);
+    for (int64_t b0 = 0; b0 < B; b0 += G_B_MAX) {
+        const int64_t nb = B - b0 < G_B_MAX ? B - b0 : G_B_MAX;
+        RVC_HIP(hipMemsetAsync(gran_ws, 0, (size_t)nb * RVC_BIGRU64_GRAN_BYTES, s));
+        hipLaunchKernelGGL(bigru64_kernel, dim3(2 * G_WG, (unsigned)nb), dim3(256), 0, s, gi + b0 * gi_bs, whh, bhh,
+                           y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
+        RVC_HIP(hipGetLastError());
+    }
+    return RVC_OK;
+}

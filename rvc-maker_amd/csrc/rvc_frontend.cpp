@@ -16,14 +16,25 @@ struct CvLayer {
     float *ln1g = nullptr, *ln1b = nullptr, *ln2g = nullptr, *ln2b = nullptr;
 };
 
+// f64 KM weights [Ci*K][Co] (+ bias) for rvc_conv64: the f64 RMVPE (rmvpe.py with precision "f64")
+struct W64 {
+    int64_t Co = 0, Ci = 0;
+    int K = 0;
+    double* w = nullptr;
+    double* b = nullptr;
+};
+
 // ConvBlockRes (RMVPE.py:11-44) with BatchNorm folded: conv.0 -> ReLU, conv.3 -> ReLU + shortcut
+// (c* for the f32 form, d* for the f64 form: one of the two sets is loaded)
 struct Cbr {
     ConvW c0, c3, sc;
+    W64 d0, d3, dsc;
     bool has_sc = false;
 };
 
 struct ConvT2d {  // ConvTranspose2d(3, stride 2, pad 1, out pad 1) + BN + ReLU as 4 phase convs
     ConvW ph[4];
+    W64 ph64[4];
     int ntap[4];
     int dy[4][4], dx[4][4];
     int64_t Co = 0;
@@ -39,9 +50,13 @@ struct ContentVec : ModelBase {
 };
 
 struct Rmvpe : ModelBase {
+    bool f64 = true;  // the f64 network (rmvpe64.hip) or the f32 one at the context's rm_prec
     ConvW mel, cnn, w_ih, fc;
+    fem::W64 mel64, cnn64, w_ih64, fc64;
     float in_scale = 1.f, in_shift = 0.f;
+    double in_scale64 = 1.0, in_shift64 = 0.0;
     float *window = nullptr, *w_hh = nullptr, *b_hh = nullptr;
+    double *w_hh64 = nullptr, *b_hh64 = nullptr;
     std::vector<std::vector<fem::Cbr>> enc, inter;  // [level][block]
     std::vector<fem::ConvT2d> dec_t;
     std::vector<std::vector<fem::Cbr>> dec;
@@ -183,6 +198,37 @@ int fold_bn(Params& P, const std::string& name, std::vector<double>& sc, std::ve
     return RVC_OK;
 }
 
+int upload64(ModelBase& m, const std::vector<double>& h, double** out) {
+    MTRY(dev_alloc(m, h.size() * 8, (void**)out));
+    MHIP(hipMemcpy(*out, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    return RVC_OK;
+}
+
+// f64 KM weights from w laid out [Co][Ci][K] (times scale[co] in f64 when given) + an f64 bias (ops.Conv64)
+int make_w64(Rmvpe& M, const HostT& w, int64_t Co, int64_t Ci, int K, const std::vector<double>* scale,
+             const std::vector<double>* bias, W64& cw) {
+    MCHECK((int64_t)w.v.size() == Co * Ci * K, "rvc_load_rmvpe: weight of %zu values, expected %lld x %lld x %d",
+           w.v.size(), (long long)Co, (long long)Ci, K);
+    cw.Co = Co;
+    cw.Ci = Ci;
+    cw.K = K;
+    std::vector<double> km((size_t)Co * Ci * K);
+    for (int64_t co = 0; co < Co; ++co)
+        for (int64_t ci = 0; ci < Ci; ++ci)
+            for (int t = 0; t < K; ++t) {
+                const double v = (double)w.v[(co * Ci + ci) * K + t];
+                km[(ci * K + t) * Co + co] = scale ? v * (*scale)[co] : v;
+            }
+    MTRY(upload64(M, km, &cw.w));
+    if (bias) {
+        MCHECK((int64_t)bias->size() == Co, "rvc_load_rmvpe: bias size %zu != %lld", bias->size(), (long long)Co);
+        MTRY(upload64(M, *bias, &cw.b));
+    }
+    return RVC_OK;
+}
+
+std::vector<double> to_f64(const std::vector<float>& v) { return std::vector<double>(v.begin(), v.end()); }
+
 // 3x3 / 1x1 Conv2d weight [Co][Ci][kh][kw] (optionally scaled per output channel) as a K = kh*kw conv
 int make_conv2d(rvc_ctx* c, Rmvpe& M, const HostT& w, const std::vector<double>* scale, const std::vector<float>& bias,
                 ConvW& cw) {
@@ -206,14 +252,23 @@ int make_cbr(rvc_ctx* c, Rmvpe& M, Params& P, const std::string& p, Cbr& blk) {
         MTRY(fold_bn(P, p + "." + convs[i][1], s, t));
         HostT w;
         MCHECK(P.get(p + "." + convs[i][0] + ".weight", w), "rvc_load_rmvpe: missing %s", P.missing.c_str());
-        std::vector<float> bf(t.begin(), t.end());
-        MTRY(make_conv2d(c, M, w, &s, bf, i == 0 ? blk.c0 : blk.c3));
+        if (M.f64) {
+            MTRY(make_w64(M, w, w.dim(0), w.dim(1), (int)(w.dim(2) * w.dim(3)), &s, &t, i == 0 ? blk.d0 : blk.d3));
+        } else {
+            std::vector<float> bf(t.begin(), t.end());
+            MTRY(make_conv2d(c, M, w, &s, bf, i == 0 ? blk.c0 : blk.c3));
+        }
     }
     if (P.has(p + ".shortcut.weight")) {
         HostT w, b;
         MCHECK(P.get(p + ".shortcut.weight", w) && P.get(p + ".shortcut.bias", b), "rvc_load_rmvpe: missing %s",
                P.missing.c_str());
-        MTRY(make_conv2d(c, M, w, nullptr, b.v, blk.sc));
+        if (M.f64) {
+            const std::vector<double> bd = to_f64(b.v);
+            MTRY(make_w64(M, w, w.dim(0), w.dim(1), (int)(w.dim(2) * w.dim(3)), nullptr, &bd, blk.dsc));
+        } else {
+            MTRY(make_conv2d(c, M, w, nullptr, b.v, blk.sc));
+        }
         blk.has_sc = true;
     }
     return RVC_OK;
@@ -235,10 +290,8 @@ int make_convT2d(rvc_ctx* c, Rmvpe& M, Params& P, const std::string& p, ConvT2d&
     for (int py = 0; py < 2; ++py)
         for (int px = 0; px < 2; ++px, ++ph) {
             int n = 0;
-            HostT wp;
             const int nt = tn[py] * tn[px];
-            wp.shape = {Co, Ci, nt};
-            wp.v.resize(Co * Ci * nt);
+            std::vector<double> wd((size_t)Co * Ci * nt);  // [Co][Ci][ntap], BN scale folded in f64
             for (int a = 0; a < tn[py]; ++a)
                 for (int b2 = 0; b2 < tn[px]; ++b2, ++n) {
                     const int ky = tk[py][a], kx = tk[px][b2];
@@ -246,10 +299,27 @@ int make_convT2d(rvc_ctx* c, Rmvpe& M, Params& P, const std::string& p, ConvT2d&
                     ct.dx[ph][n] = td[px][b2];
                     for (int64_t co = 0; co < Co; ++co)
                         for (int64_t ci = 0; ci < Ci; ++ci)
-                            wp.v[(co * Ci + ci) * nt + n] = (float)((double)w.v[((ci * Co + co) * 3 + ky) * 3 + kx] * s[co]);
+                            wd[(co * Ci + ci) * nt + n] = (double)w.v[((ci * Co + co) * 3 + ky) * 3 + kx] * s[co];
                 }
             ct.ntap[ph] = nt;
-            MTRY(make_conv(c, M, wp, &bias, ct.ph[ph]));
+            if (M.f64) {
+                W64& cw = ct.ph64[ph];
+                cw.Co = Co;
+                cw.Ci = Ci;
+                cw.K = nt;
+                std::vector<double> km((size_t)Co * Ci * nt);
+                for (int64_t co = 0; co < Co; ++co)
+                    for (int64_t ci = 0; ci < Ci; ++ci)
+                        for (int q = 0; q < nt; ++q) km[(ci * nt + q) * Co + co] = wd[(co * Ci + ci) * nt + q];
+                MTRY(upload64(M, km, &cw.w));
+                MTRY(upload64(M, t, &cw.b));
+            } else {
+                HostT wp;
+                wp.shape = {Co, Ci, nt};
+                wp.v.resize(wd.size());
+                for (size_t i = 0; i < wd.size(); ++i) wp.v[i] = (float)wd[i];
+                MTRY(make_conv(c, M, wp, &bias, ct.ph[ph]));
+            }
         }
     return RVC_OK;
 }
@@ -384,6 +454,168 @@ int rm_one(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, float
     return RVC_OK;
 }
 
+// ------------------------------------------------------------------ the f64 network (rmvpe.py, precision "f64")
+struct C64Opts {
+    int64_t Lout = -1;
+    int pad = 0, out_act = RVC_ACT_NONE, y_f32 = 0, ntoff = 0, wrap = 0;
+    int toff[16] = {0};
+    double out_slope = 0.0;
+    const double* res = nullptr;
+};
+
+int conv64(Rmvpe& M, const W64& cw, const double* x, int64_t Lin, void* y, const C64Opts& o, hipStream_t s) {
+    rvc_conv64_args a;
+    memset(&a, 0, sizeof(a));
+    a.x = x;
+    a.w = cw.w;
+    a.bias = cw.b;
+    a.res = o.res;
+    a.y = y;
+    a.B = 1;
+    a.Ci = cw.Ci;
+    a.Co = cw.Co;
+    a.Lin = Lin;
+    a.Lout = o.Lout >= 0 ? o.Lout : Lin + 2 * o.pad - (cw.K - 1);
+    a.K = cw.K;
+    a.pad = o.pad;
+    a.out_act = o.out_act;
+    a.y_f32 = o.y_f32;
+    a.out_slope = o.out_slope;
+    a.ntoff = o.ntoff;
+    a.wrap = o.wrap;
+    for (int i = 0; i < o.ntoff; ++i) a.toff[i] = o.toff[i];
+    const int64_t need = rvc_conv64_workspace_bytes(&a);
+    if (need < 0) return RVC_EINVAL;
+    MTRY(ensure_ws(M, need, s));
+    return rvc_conv64(&a, need ? M.ws : nullptr, need, s);
+}
+
+// _Conv2d.__call__ (f64) on bordered [C][H+2][W+2] images
+int conv2d64(Rmvpe& M, const W64& cw, const double* x, int64_t H, int64_t W, double* out, int out_act,
+             const double* res, hipStream_t s) {
+    const int64_t wrap = W + 2, L = (H + 2) * wrap;
+    C64Opts o;
+    o.Lout = L;
+    o.wrap = (int)wrap;
+    o.out_act = out_act;
+    o.res = res;
+    if (cw.K == 9) {
+        o.ntoff = 9;
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx) o.toff[dy * 3 + dx] = (int)(dy * wrap + dx);
+        o.pad = (int)(wrap + 1);
+    } else {
+        o.ntoff = 1;
+    }
+    return conv64(M, cw, x, L, out, o, s);
+}
+
+double* take64(Scratch& sc, int64_t n) { return (double*)sc.take(2 * n); }
+
+int cbr_run64(Rmvpe& M, Scratch& sc, const Cbr& blk, const double* x, int64_t H, int64_t W, double* out,
+              hipStream_t s) {
+    const int64_t img = (H + 2) * (W + 2);
+    double* h = take64(sc, blk.d0.Co * img);
+    RUN(conv2d64(M, blk.d0, x, H, W, h, RVC_ACT_RELU, nullptr, s));
+    const double* res = x;
+    if (blk.has_sc) {
+        double* scb = take64(sc, blk.d0.Co * img);
+        RUN(conv2d64(M, blk.dsc, x, H, W, scb, RVC_ACT_NONE, nullptr, s));
+        res = scb;
+    }
+    RUN(conv2d64(M, blk.d3, h, H, W, out, RVC_ACT_RELU, res, s));
+    return RVC_OK;
+}
+
+// rm_one in f64: the same launch sequence as RMVPEAMD's f64 form, the salience rounded to f32 once
+int rm_one64(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, float* sal, hipStream_t s) {
+    const int64_t F = 1 + N / kHop, Tp = 32 * ((F - 1) / 32 + 1);
+    double* mag = take64(sc, (int64_t)(kNfft / 2 + 1) * F);
+    RUN(rvc_stft_mag64(wav, M.window, mag, 1, N, F, kNfft, kHop, 0, 0, s));
+    double* mel = take64(sc, (int64_t)kMels * F);
+    {
+        C64Opts o;
+        o.out_act = RVC_ACT_LOGCLAMP;
+        o.out_slope = 1e-5;
+        RUN(conv64(M, M.mel64, mag, F, mel, o, s));
+    }
+    int64_t H = Tp, W = kMels;
+    double* x = take64(sc, (H + 2) * (W + 2));
+    RUN(hipMemsetAsync(x, 0, (H + 2) * (W + 2) * 8, s) == hipSuccess ? RVC_OK : RVC_EHIP);
+    RUN(rvc_mel_image64(mel, x, 1, kMels, F, Tp, M.in_scale64, M.in_shift64, 0, 0, s));
+    struct Cat {
+        double* buf;
+        int64_t C, H, W;
+    };
+    std::vector<Cat> cats;
+    int64_t C = M.enc[0][0].d0.Co;
+    const int nb = (int)M.enc[0].size();
+    for (size_t l = 0; l < M.enc.size(); ++l) {
+        const int64_t img = (H + 2) * (W + 2);
+        double* cat = take64(sc, 2 * C * img);
+        RUN(hipMemsetAsync(cat, 0, 2 * C * img * 8, s) == hipSuccess ? RVC_OK : RVC_EHIP);
+        for (int b = 0; b < nb; ++b) {
+            double* out = b == nb - 1 ? cat + C * img : take64(sc, C * img);
+            MTRY(cbr_run64(M, sc, M.enc[l][b], x, H, W, out, s));
+            x = out;
+        }
+        cats.push_back({cat, C, H, W});
+        double* pooled = take64(sc, C * (H / 2 + 2) * (W / 2 + 2));
+        RUN(hipMemsetAsync(pooled, 0, C * (H / 2 + 2) * (W / 2 + 2) * 8, s) == hipSuccess ? RVC_OK : RVC_EHIP);
+        RUN(rvc_avgpool2_64(x, pooled, 1, C, H, W, 0, 0, s));
+        x = pooled;
+        H /= 2;
+        W /= 2;
+        C *= 2;
+    }
+    for (auto& layer : M.inter)
+        for (auto& blk : layer) {
+            double* out = take64(sc, blk.d0.Co * (H + 2) * (W + 2));
+            MTRY(cbr_run64(M, sc, blk, x, H, W, out, s));
+            x = out;
+        }
+    for (size_t i = 0; i < M.dec_t.size(); ++i) {
+        const Cat& ct = cats[cats.size() - 1 - i];
+        const ConvT2d& T2 = M.dec_t[i];
+        const int64_t wrap = W + 2, Lc = (H + 2) * wrap;
+        double* ph = take64(sc, 4 * T2.Co * Lc);
+        for (int p = 0; p < 4; ++p) {
+            C64Opts o;
+            o.Lout = Lc;
+            o.wrap = (int)wrap;
+            o.out_act = RVC_ACT_RELU;
+            o.ntoff = T2.ntap[p];
+            for (int t = 0; t < T2.ntap[p]; ++t) o.toff[t] = (int)(T2.dy[p][t] * wrap + T2.dx[p][t]);
+            RUN(conv64(M, T2.ph64[p], x, Lc, ph + p * T2.Co * Lc, o, s));
+        }
+        RUN(rvc_interleave4_64(ph, ct.buf, 1, T2.Co, H, W, 0, 0, s));
+        x = ct.buf;
+        H = ct.H;
+        W = ct.W;
+        for (auto& blk : M.dec[i]) {
+            double* out = take64(sc, blk.d0.Co * (H + 2) * (W + 2));
+            MTRY(cbr_run64(M, sc, blk, x, H, W, out, s));
+            x = out;
+        }
+    }
+    double* img = take64(sc, 3 * (H + 2) * (W + 2));
+    RUN(conv2d64(M, M.cnn64, x, H, W, img, RVC_ACT_NONE, nullptr, s));
+    double* seq = take64(sc, 3 * W * H);
+    RUN(rvc_img_to_seq64(img, seq, 1, 3, H, W, 0, 0, s));
+    double* gi = take64(sc, 1536 * Tp);
+    {
+        C64Opts o;
+        RUN(conv64(M, M.w_ih64, seq, Tp, gi, o, s));
+    }
+    double* y = take64(sc, 512 * Tp);
+    RUN(rvc_bigru64_batched(gi, 0, M.w_hh64, M.b_hh64, y, 0, M.gran, M.err, 1, Tp, s));
+    C64Opts o;
+    o.out_act = RVC_ACT_SIGMOID;
+    o.y_f32 = 1;
+    RUN(conv64(M, M.fc64, y, Tp, sal, o, s));
+    return RVC_OK;
+}
+
 }  // namespace fem
 
 using namespace fem;
@@ -512,6 +744,7 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
     rmvpe_delete(c->rm);
     c->rm = new Rmvpe();
     Rmvpe& M = *c->rm;
+    M.f64 = c->rm_prec == RVC_PREC_FP64;
     HostT w, b;
 #define GET(k, t) MCHECK(P.get(k, t), "rvc_load_rmvpe: missing %s", P.missing.c_str())
     // constants: Hann window, mel basis (rmvpe.py __init__, melbasis.py)
@@ -555,12 +788,15 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
         }
     }
     mb.shape.push_back(1);
-    MTRY(make_conv(c, M, mb, nullptr, M.mel));
+    if (M.f64) MTRY(make_w64(M, mb, kMels, kNfft / 2 + 1, 1, nullptr, nullptr, M.mel64));
+    else MTRY(make_conv(c, M, mb, nullptr, M.mel));
     {
         std::vector<double> s, t;
         MTRY(fold_bn(P, "unet.encoder.bn", s, t));
         M.in_scale = (float)s[0];
         M.in_shift = (float)t[0];
+        M.in_scale64 = s[0];
+        M.in_shift64 = t[0];
     }
     const int nblk = 4;  // E2E(4, 1, (2, 2))
     for (int l = 0; P.has("unet.encoder.layers." + std::to_string(l) + ".conv.0.conv.0.weight"); ++l) {
@@ -582,11 +818,16 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
         M.dec.emplace_back(nblk);
         for (int bb = 0; bb < nblk; ++bb) MTRY(make_cbr(c, M, P, p + ".conv2." + std::to_string(bb), M.dec.back()[bb]));
     }
-    MCHECK(M.enc.size() == 5 && M.dec.size() == 5 && M.enc[0][0].c0.Ci == 1,
+    MCHECK(M.enc.size() == 5 && M.dec.size() == 5 && (M.f64 ? M.enc[0][0].d0.Ci : M.enc[0][0].c0.Ci) == 1,
            "rvc_load_rmvpe: expected the E2E(4, 1, (2, 2)) U-Net (5 encoder / decoder levels)");
     GET("cnn.weight", w);
     GET("cnn.bias", b);
-    MTRY(make_conv2d(c, M, w, nullptr, b.v, M.cnn));
+    if (M.f64) {
+        const std::vector<double> bd = to_f64(b.v);
+        MTRY(make_w64(M, w, w.dim(0), w.dim(1), (int)(w.dim(2) * w.dim(3)), nullptr, &bd, M.cnn64));
+    } else {
+        MTRY(make_conv2d(c, M, w, nullptr, b.v, M.cnn));
+    }
     const std::string g = "fc.0.gru.";
     HostT wi, wir, bi, bir;
     GET(g + "weight_ih_l0", wi);
@@ -597,7 +838,12 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
     wi.v.insert(wi.v.end(), wir.v.begin(), wir.v.end());
     wi.shape = {1536, 384, 1};
     bi.v.insert(bi.v.end(), bir.v.begin(), bir.v.end());
-    MTRY(make_conv(c, M, wi, &bi, M.w_ih));
+    if (M.f64) {
+        const std::vector<double> bd = to_f64(bi.v);
+        MTRY(make_w64(M, wi, 1536, 384, 1, nullptr, &bd, M.w_ih64));
+    } else {
+        MTRY(make_conv(c, M, wi, &bi, M.w_ih));
+    }
     HostT wh, whr, bh, bhr;
     GET(g + "weight_hh_l0", wh);
     GET(g + "weight_hh_l0_reverse", whr);
@@ -605,15 +851,25 @@ extern "C" int rvc_load_rmvpe(rvc_ctx* c, const rvc_param* params, int n) {
     GET(g + "bias_hh_l0_reverse", bhr);
     wh.v.insert(wh.v.end(), whr.v.begin(), whr.v.end());
     bh.v.insert(bh.v.end(), bhr.v.begin(), bhr.v.end());
-    MTRY(upload(M, wh.v, &M.w_hh));
-    MTRY(upload(M, bh.v, &M.b_hh));
+    if (M.f64) {
+        MTRY(upload64(M, to_f64(wh.v), &M.w_hh64));
+        MTRY(upload64(M, to_f64(bh.v), &M.b_hh64));
+    } else {
+        MTRY(upload(M, wh.v, &M.w_hh));
+        MTRY(upload(M, bh.v, &M.b_hh));
+    }
     GET("fc.1.weight", w);
     GET("fc.1.bias", b);
     MCHECK(w.dim(0) == kClass && w.dim(1) == 512, "rvc_load_rmvpe: fc.1 must be Linear(512, 360)");
     w.shape.push_back(1);
-    MTRY(make_conv(c, M, w, &b, M.fc));
+    if (M.f64) {
+        const std::vector<double> bd = to_f64(b.v);
+        MTRY(make_w64(M, w, kClass, 512, 1, nullptr, &bd, M.fc64));
+    } else {
+        MTRY(make_conv(c, M, w, &b, M.fc));
+    }
 #undef GET
-    MTRY(dev_alloc(M, 8192, &M.gran));
+    MTRY(dev_alloc(M, RVC_BIGRU64_GRAN_BYTES, &M.gran));
     MTRY(dev_alloc(M, 4, (void**)&M.err));
     MHIP(hipMemset(M.err, 0, 4));
     MHIP(hipDeviceSynchronize());
@@ -629,19 +885,33 @@ extern "C" int rvc_rmvpe_forward(rvc_ctx* c, const float* wav, int64_t B, int64_
     MHIP(hipSetDevice(c->device));
     Rmvpe& M = *c->rm;
     const int prev = c->prec;
-    c->prec = RVC_PREC_FP32SA;  // exact products whatever the context's precision (rmvpe.py: self.precision)
+    // the f32 form runs at the RMVPE precision it was loaded for, whatever the context's conv precision
+    // (rmvpe.py: self.precision); the f64 form has its own engine
+    if (!M.f64) c->prec = c->rm_prec;
+    auto one = [&](Scratch& scr, const float* x, float* sal) {
+        return M.f64 ? rm_one64(c, M, scr, x, N, sal, s) : rm_one(c, M, scr, x, N, sal, s);
+    };
     Scratch sc;
-    int rc = rm_one(c, M, sc, wav, N, salience, s);
+    int rc = one(sc, wav, salience);
     if (rc == RVC_OK) rc = ensure_arena(M, sc.off, s);
     const int64_t ld = rvc_rmvpe_salience_ld(N);
     for (int64_t b = 0; b < B && rc == RVC_OK; ++b) {
         Scratch run;
         run.dry = false;
         run.base = M.arena;
-        rc = rm_one(c, M, run, wav + b * N, N, salience + b * kClass * ld, s);
+        rc = one(run, wav + b * N, salience + b * kClass * ld);
     }
     c->prec = prev;
     return rc;
+}
+
+extern "C" int rvc_ctx_set_rmvpe_precision(rvc_ctx* c, int prec) {
+    MCHECK(c, "rvc_ctx_set_rmvpe_precision: null ctx");
+    MCHECK(prec == RVC_PREC_FP64 || prec == RVC_PREC_FP32 || prec == RVC_PREC_BF16 || prec == RVC_PREC_BF16X3 ||
+               prec == RVC_PREC_FP32X6 || prec == RVC_PREC_FP32SA || prec == RVC_PREC_F16X3,
+           "rvc_ctx_set_rmvpe_precision: unknown precision %d", prec);
+    c->rm_prec = prec;
+    return RVC_OK;
 }
 
 extern "C" int rvc_rmvpe_check(rvc_ctx* c) {

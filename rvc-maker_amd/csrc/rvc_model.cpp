@@ -64,8 +64,13 @@ int rb_passes(const rvc_ctx* c, int K) {
     return base_passes(c);
 }
 
+// the fused pair takes the pass sets ops.RB_PASSES lists (6, 3, 1, split-fp16); any other (FP32SA) runs as two
+// rvc_conv1d launches, as ops.resblock_fusable decides
+bool rb_pass_ok(int passes) { return passes == 6 || passes == 3 || passes == 1 || passes == RVC_ARITH_F16X3; }
+
 bool resblock_fusable(const rvc_ctx* c, const ConvW& c1, const ConvW& c2, int d) {
-    return c->fused_rb && c1.wx_bf && c2.wx_bf && c1.Ci == c1.Co && c1.Co == c2.Ci && c2.Ci == c2.Co &&
+    return c->fused_rb && rb_pass_ok(rb_passes(c, c1.K)) && c1.wx_bf && c2.wx_bf && c1.Ci == c1.Co &&
+           c1.Co == c2.Ci && c2.Ci == c2.Co &&
            (c1.Co == 32 || c1.Co == 64) && c1.K == c2.K && c1.K % 2 == 1 && c1.K <= 15 && (c1.K - 1) * d <= 64;
 }
 

@@ -30,6 +30,15 @@ class Conv1dArgs(ctypes.Structure):
                 ("wx", c_void_p), ("wx_nmf", c_int), ("wx_passes", c_int)]
 
 
+class Conv64Args(ctypes.Structure):
+    """rvc_conv64_args: the f64 implicit-GEMM conv of the f64 RMVPE (rmvpe64.hip)."""
+    _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("res", c_void_p), ("y", c_void_p),
+                ("B", c_int64), ("Ci", c_int64), ("Co", c_int64), ("Lin", c_int64), ("Lout", c_int64),
+                ("x_bstride", c_int64), ("y_bstride", c_int64), ("res_bstride", c_int64),
+                ("K", c_int), ("pad", c_int), ("out_act", c_int), ("y_f32", c_int), ("out_slope", c_double),
+                ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16)]
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("rk", c_void_p),
                 ("ev", c_void_p), ("ml", c_void_p),
@@ -147,6 +156,17 @@ SIGNATURES = {
     "rvc_bigru_set_spin_limit": [ctypes.c_uint],
     "rvc_bigru_batched": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64,
                           c_void_p],
+    "rvc_conv64": [POINTER(Conv64Args), c_void_p, c_int64, c_void_p],
+    "rvc_conv64_workspace_bytes": [POINTER(Conv64Args)],
+    "rvc_stft_mag64": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_int, c_int64, c_int64,
+                       c_void_p],
+    "rvc_mel_image64": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_double, c_double, c_int64, c_int64,
+                        c_void_p],
+    "rvc_avgpool2_64": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_interleave4_64": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_img_to_seq64": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_void_p],
+    "rvc_bigru64_batched": [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                            c_int64, c_void_p],
     "rvc_rmvpe_decode": [c_void_p, c_int64, c_int64, c_double, c_double, POINTER(F0Post), c_void_p, c_void_p,
                          c_void_p, c_void_p],
     "rvc_filtfilt_work_bytes": [c_int64],
@@ -179,6 +199,7 @@ SIGNATURES = {
     "rvc_ctx_create": [c_int, POINTER(c_void_p)],
     "rvc_ctx_destroy": [c_void_p],
     "rvc_ctx_set_precision": [c_void_p, c_int],
+    "rvc_ctx_set_rmvpe_precision": [c_void_p, c_int],
     "rvc_load_synth": [c_void_p, POINTER(Param), c_int, POINTER(SynthCfg)],
     "rvc_synth_out_len": [c_void_p, c_int64],
     "rvc_load_contentvec": [c_void_p, POINTER(Param), c_int, POINTER(ContentVecCfg)],
@@ -207,6 +228,7 @@ SIGNATURES = {
                         c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
+             "rvc_conv64_workspace_bytes": c_int64,
              "rvc_conv1d_f16_bytes": c_int64, "rvc_pm_frames": c_int64, "rvc_pm_work_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,

@@ -60,7 +60,7 @@ def _coll(dist, t):
     return t.cpu() if dist.get_backend() == "gloo" else t
 
 
-def exchange_tiles(compute_tile, rows: int, Tp: int, dist, device, halo: int = HALO):
+def exchange_tiles(compute_tile, rows: int, Tp: int, dist, device, halo: int = HALO, dtype=None):
     """The sharded-by-time pass + its exchange: rank r computes rows [r0, r1) with ``compute_tile(r0, r1)``
     -> [rows][r1 - r0], keeps its [a, b), and one all_gather gives every rank the whole [rows][Tp]."""
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -68,7 +68,9 @@ def exchange_tiles(compute_tile, rows: int, Tp: int, dist, device, halo: int = H
     a, b, r0, r1 = plan[rank]
     maxlen = max(pb - pa for pa, pb, _, _ in plan)
     tile = compute_tile(r0, r1) if b > a else None
-    mine = torch.zeros(rows, maxlen, device=device, dtype=tile.dtype if tile is not None else torch.float32)
+    # every rank must gather one dtype: pass it when a rank may have no tile
+    mine = torch.zeros(rows, maxlen, device=device,
+                       dtype=dtype or (tile.dtype if tile is not None else torch.float32))
     if tile is not None:
         mine[:, : b - a] = tile[:, a - r0: b - r0]
     mine = _coll(dist, mine)
@@ -80,18 +82,18 @@ def exchange_tiles(compute_tile, rows: int, Tp: int, dist, device, halo: int = H
 def sharded_f0(vc, xp: torch.Tensor, pitch, dist, halo: int = HALO):
     """Steps 2-3: (coarse int64 [F], pitchf f32 [F]) of the padded signal xp on every rank."""
     rm = vc._rmvpe()
-    with ops.precision(rm.precision or ops.get_precision()):
-        mel = rm.mel_spectrogram(xp)  # replicated: ~0.1 GFLOP per 10 s
-        F = mel.shape[-1]
-        img, Tp = rm.mel_image(mel)  # [1][Tp+2][130]
+    mel = rm.mel_spectrogram(xp)  # replicated: ~0.1 GFLOP per 10 s
+    F = mel.shape[-1]
+    img, Tp = rm.mel_image(mel)  # [1][Tp+2][130]
 
-        def unet_tile(r0, r1):
-            tile = torch.zeros(1, r1 - r0 + 2, img.shape[-1], device=xp.device)
-            tile[0, 1:-1] = img[0, 1 + r0: 1 + r1]  # interior rows; the tile's own border rows stay zero
-            return rm.unet_seq(tile, r1 - r0)
+    def unet_tile(r0, r1):
+        tile = torch.zeros(1, r1 - r0 + 2, img.shape[-1], device=xp.device, dtype=img.dtype)
+        tile[0, 1:-1] = img[0, 1 + r0: 1 + r1]  # interior rows; the tile's own border rows stay zero
+        return rm.unet_seq(tile, r1 - r0)
 
-        seq_all = exchange_tiles(unet_tile, 384, Tp, dist, xp.device, halo)  # 384 x Tp f32 GRU inputs
-        sal = rm.head(seq_all)
+    # 384 x Tp GRU inputs (f64 in the f64 RMVPE: 3 KB per frame)
+    seq_all = exchange_tiles(unet_tile, 384, Tp, dist, xp.device, halo, dtype=img.dtype)
+    sal = rm.head(seq_all)
     coarse, pitchf, _ = rm.decode(sal, Tp, F, 0.03, float(pitch))
     return coarse, pitchf
 

@@ -13,6 +13,7 @@ binds; here it also pins the native sequence against ``SynthesizerAMD`` (tests/t
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -20,7 +21,12 @@ import torch
 from . import _lib
 from ._lib import check
 
-PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3, "fp32x6": 6, "fp32sa": 7, "f16x3": 16}
+PREC = {"fp32": 0, "bf16": 1, "bf16x3": 3, "fp32x6": 6, "fp32sa": 7, "f16x3": 16, "f64": 64}
+
+
+def _rmvpe_precision(name):
+    """RMVPE's arithmetic as RMVPEAMD picks it (RVC_RMVPE_PRECISION, default "f64")."""
+    return PREC[name or os.environ.get("RVC_RMVPE_PRECISION", "f64")]
 
 
 def _params(W: dict):
@@ -204,8 +210,10 @@ class NativeContentVec(_Ctx):
 class NativeRMVPE(_Ctx):
     """RMVPE salience / f0 through rvc_load_rmvpe / rvc_rmvpe_forward / rvc_rmvpe_decode."""
 
-    def __init__(self, sd: dict, device: str = "cuda", window=None, mel_basis=None):
+    def __init__(self, sd: dict, device: str = "cuda", window=None, mel_basis=None, rmvpe_precision=None):
         super().__init__(device)
+        check(self.lib.rvc_ctx_set_rmvpe_precision(self.ctx, _rmvpe_precision(rmvpe_precision)),
+              "rvc_ctx_set_rmvpe_precision")
         W = dict(sd)
         if window is not None:
             W["window"] = window
@@ -283,8 +291,10 @@ class NativeVC(_Ctx):
     peak normalisation).  ``synth_weights`` / ``hub_weights`` / ``rmvpe_consts`` as the single-model classes."""
 
     def __init__(self, hub_ckpt: dict, rmvpe_sd: dict, synth_cpt: dict, device: str = "cuda", precision="fp32",
-                 synth_weights=None, hub_weights=None, window=None, mel_basis=None):
+                 synth_weights=None, hub_weights=None, window=None, mel_basis=None, rmvpe_precision=None):
         super().__init__(device, precision)
+        check(self.lib.rvc_ctx_set_rmvpe_precision(self.ctx, _rmvpe_precision(rmvpe_precision)),
+              "rvc_ctx_set_rmvpe_precision")
         cfg = hub_ckpt["cfg"]["model"]
         c = _lib.ContentVecCfg()
         c.encoder_embed_dim = cfg.get("encoder_embed_dim", 768)

@@ -547,6 +547,150 @@ def bigru_batched(gi, whh, bhh, y, gran, err, B, T):
     return y
 
 
+# ------------------------------------------------------------------ f64 RMVPE (rmvpe64.hip)
+def _pd(t):
+    if t is None:
+        return None
+    if not t.is_cuda or t.dtype != torch.float64:
+        raise TypeError(f"rvc_amd: expected a CUDA f64 tensor, got {t.dtype} on {t.device}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Conv64:
+    """A Conv weight [Co, Ci, K] (and bias [Co]) kept in f64 KM layout for ``conv64``."""
+
+    def __init__(self, w, b=None, device="cuda"):
+        self.Co, self.Ci, self.K = (int(s) for s in w.shape)
+        self.w = pack_km(w.double()).to(device)
+        self.b = b.double().to(device) if b is not None else None
+
+    def __call__(self, x, Lout=None, **kw):
+        return conv64(x, self.w, self.Ci, self.Co, self.K, bias=self.b, Lout=Lout, **kw)
+
+
+def conv64(x, w, Ci, Co, K, *, bias=None, pad=0, Lout=None, out=None, res=None, out_act=ACT_NONE, out_slope=0.0,
+           B=None, Lin=None, x_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, out_f32=False):
+    """The f64 conv (rvc_conv64): x [B][Ci][Lin] f64, y f64 (or f32 when ``out_f32``), stride 1, K taps at
+    ``toff`` (or 0..K-1), 2-D border masking with ``wrap``; see include/rvc_amd.h."""
+    if B is None:
+        B, Cx, Lx = _shape3(x)
+        if Lin is None:
+            Lin = Lx
+        if Cx != Ci:
+            raise ValueError(f"conv64: x has {Cx} channels, weight expects {Ci}")
+        if not x.is_contiguous():
+            raise ValueError("conv64: x must be contiguous")
+    if Lout is None:
+        Lout = Lin + 2 * pad - (K - 1)
+    if Lout <= 0:
+        raise ValueError("conv64: empty output")
+    if w.numel() < Ci * K * Co or w.dtype != torch.float64:
+        raise ValueError("conv64: f64 KM weight [Ci*K][Co] expected")
+    ydt = torch.float32 if out_f32 else torch.float64
+    if out is None:
+        out = torch.empty(*((B,) if B > 1 else ()), Co, Lout, device=x.device, dtype=ydt)
+    elif out.dtype != ydt or _room(out) < (B - 1) * (y_bstride or Co * Lout) + Co * Lout:
+        raise ValueError("conv64: output buffer too small or of the wrong dtype")
+    if res is not None and _room(res) < (B - 1) * (res_bstride or Co * Lout) + Co * Lout:
+        raise ValueError("conv64: residual too small")
+    if _room(x) < (B - 1) * (x_bstride or Ci * Lin) + Ci * Lin:
+        raise ValueError("conv64: input buffer too small")
+    if bias is not None and bias.numel() < Co:
+        raise ValueError("conv64: bias too small")
+    a = _lib.Conv64Args()
+    a.x, a.w, a.bias, a.res = _pd(x), _pd(w), _pd(bias), _pd(res)
+    a.y = _p(out) if out_f32 else _pd(out)
+    a.B, a.Ci, a.Co, a.Lin, a.Lout = B, Ci, Co, Lin, Lout
+    a.x_bstride, a.y_bstride, a.res_bstride = x_bstride, y_bstride, res_bstride
+    a.K, a.pad, a.out_act, a.y_f32, a.out_slope = K, pad, out_act, int(bool(out_f32)), out_slope
+    if toff is not None:
+        if len(toff) != K or K > 16:
+            raise ValueError("conv64: toff must have K <= 16 entries")
+        a.ntoff = K
+        for i, v in enumerate(toff):
+            a.toff[i] = int(v)
+    a.wrap = wrap
+    lib = _lib.load()
+    need = lib.rvc_conv64_workspace_bytes(ctypes.byref(a))
+    if need < 0:
+        raise RuntimeError(f"rvc_amd: conv64 plan failed: {lib.rvc_last_error().decode()}")
+    ws = _workspace(out.device, need, "c64") if need else None
+    check(lib.rvc_conv64(ctypes.byref(a), _p(ws), need, _stream()), "conv64")
+    return out
+
+
+def _bs(t, nd):
+    """Batch stride of a [B][...] view (0 for an unbatched tensor of ``nd`` dims)."""
+    return t.stride(0) if t.dim() > nd else 0
+
+
+def stft_mag64(x, win, mag, N, F, nfft, hop):
+    """|STFT| in f64 (unrounded): x [N] or [B][N] f32 -> mag f64 [nfft/2+1][F] or [B][nfft/2+1][F]."""
+    B = x.shape[0] if x.dim() == 2 else 1
+    K = nfft // 2 + 1
+    if (x.shape[-1] < N or win.numel() < nfft or mag.numel() < B * K * F or mag.shape[-1] != F
+            or (B > 1 and (mag.dim() != 3 or mag.shape[0] != B))):
+        raise ValueError("stft_mag64: size mismatch")
+    if x.stride(-1) != 1 or mag.stride(-1) != 1:
+        raise ValueError("stft_mag64: x / mag rows must be contiguous")
+    check(_lib.load().rvc_stft_mag64(_p(x), _p(win), _pd(mag), B, N, F, nfft, hop, x.stride(0) if B > 1 else 0,
+                                     mag.stride(0) if B > 1 else 0, _stream()), "stft_mag64")
+    return mag
+
+
+def mel_image64(mel, img, M, F, Tp, scale, shift):
+    """mel [(B)][M][F] f64 -> interior of bordered images [(B)][1][Tp+2][M+2] f64 (reflect-padded frames)."""
+    B = mel.shape[0] if mel.dim() == 3 else 1
+    if mel.numel() < B * M * F or img.numel() < B * (Tp + 2) * (M + 2):
+        raise ValueError("mel_image64: size mismatch")
+    check(_lib.load().rvc_mel_image64(_pd(mel), _pd(img), B, M, F, Tp, scale, shift, _bs(mel, 2), _bs(img, 3),
+                                      _stream()), "mel_image64")
+    return img
+
+
+def avgpool2_64(x, out, C, H, W):
+    B = x.shape[0] if x.dim() == 4 else 1
+    if _room(x) < B * C * (H + 2) * (W + 2) or _room(out) < B * C * (H // 2 + 2) * (W // 2 + 2):
+        raise ValueError("avgpool2_64: size mismatch")
+    check(_lib.load().rvc_avgpool2_64(_pd(x), _pd(out), B, C, H, W, _bs(x, 3), _bs(out, 3), _stream()), "avgpool2_64")
+    return out
+
+
+def interleave4_64(phases, out, C, H, W):
+    """phases [(B)][4][C][H+2][W+2] -> the first C channels of bordered out [(B)][*][2H+2][2W+2]."""
+    B = phases.shape[0] if phases.dim() == 5 else 1
+    if _room(phases) < B * 4 * C * (H + 2) * (W + 2) or _room(out) < B * C * (2 * H + 2) * (2 * W + 2):
+        raise ValueError("interleave4_64: size mismatch")
+    check(_lib.load().rvc_interleave4_64(_pd(phases), _pd(out), B, C, H, W, _bs(phases, 4), _bs(out, 3), _stream()),
+          "interleave4_64")
+    return out
+
+
+def img_to_seq64(img, x, C, H, W):
+    B = img.shape[0] if img.dim() == 4 else 1
+    if _room(img) < B * C * (H + 2) * (W + 2) or _room(x) < B * C * W * H:
+        raise ValueError("img_to_seq64: size mismatch")
+    check(_lib.load().rvc_img_to_seq64(_pd(img), _pd(x), B, C, H, W, _bs(img, 3), _bs(x, 2), _stream()),
+          "img_to_seq64")
+    return x
+
+
+GRU64_GRAN = 16384 // 8  # int64 words of bigru64 hand-off scratch per sequence (RVC_BIGRU64_GRAN_BYTES)
+
+
+def bigru64_batched(gi, whh, bhh, y, gran, err, B, T):
+    """B f64 BiGRU recurrences: gi [(B)][1536][T], y [(B)][512][T] f64."""
+    if gi.shape[-2] != 1536 or y.shape[-2] != 512 or gi.shape[-1] < T or y.shape[-1] < T:
+        raise ValueError("bigru64: gi [(B)][1536][T], y [(B)][512][T] expected")
+    if (gi.dim() == 3 and gi.shape[0] < B) or (y.dim() == 3 and y.shape[0] < B) or (B > 1 and gi.dim() != 3):
+        raise ValueError("bigru64: batch mismatch")
+    if gran.numel() < GRU64_GRAN * min(B, GRU_B_MAX) or whh.numel() < 2 * 768 * 256 or whh.dtype != torch.float64:
+        raise ValueError("bigru64: size mismatch")
+    check(_lib.load().rvc_bigru64_batched(_pd(gi), _bs(gi, 2), _pd(whh), _pd(bhh), _pd(y), _bs(y, 2), _p(gran), _p(err),
+                                          B, T, _stream()), "bigru64")
+    return y
+
+
 class F0Post:
     """The optional steps of VC.get_f0 between the raw f0 and the quantiser (convert.py:311-318):
     autotune strength (None = off) and the f0-file override ``rep`` (f64 values for frames

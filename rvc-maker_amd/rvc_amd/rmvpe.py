@@ -13,6 +13,14 @@ into the convolutions on the host at load.  On the device:
             buffers; ConvTranspose2d = 4 phase convs + interleave4
   head      cnn conv -> img_to_seq -> W_ih GEMM (both directions) -> bigru recurrence
             -> Linear 512->360 + sigmoid -> f64 decode + coarse pitch (rmvpe_decode)
+
+Arithmetic (``precision``, RVC_RMVPE_PRECISION): "f64" (the default) runs every step above in f64 -- the convs on
+the f64 matrix cores (rmvpe64.hip), the BiGRU recurrence in f64 -- and rounds only the salience to f32 for the
+decode.  RMVPE's f0 is a per-frame decision (argmax over 360 bins, 0.03 voicing threshold) and on the headline
+clip the exact model's top two bins are 3.2e-6 apart at one frame, while every f32 evaluation errs by up to
+1.7e-4 (the reference's own at other thread counts included): only an f64 network takes the exact model's
+decisions everywhere.  "fp32sa" / any ops.PASSES name runs the f32 form (split-bf16 MFMA convs,
+f32 BiGRU) for A/B comparisons.
 """
 from __future__ import annotations
 
@@ -34,8 +42,11 @@ RMVPE_SPLITK = int(os.environ["RVC_RMVPE_SPLITK"]) if os.environ.get("RVC_RMVPE_
 
 
 def _at_precision(fn):
-    """Run a RMVPEAMD stage at the model's own arithmetic (self.precision) and split-K policy, whoever calls it."""
+    """Run a RMVPEAMD stage at the model's own arithmetic (self.precision) and split-K policy, whoever calls it
+    (the f64 form has its own engine: the f32 engine's precision and split-K settings do not apply)."""
     def wrapped(self, *a, **k):
+        if self.f64:
+            return fn(self, *a, **k)
         with ops.precision(self.precision or ops.get_precision()), ops.splitk_target(RMVPE_SPLITK):
             return fn(self, *a, **k)
     wrapped.__name__, wrapped.__doc__ = fn.__name__, fn.__doc__
@@ -50,14 +61,19 @@ def _fold_bn(sd, name):
 
 
 class _Conv2d:
-    """3x3 (pad 1) or 1x1 conv on bordered images through the conv1d engine (2-D mode)."""
+    """3x3 (pad 1) or 1x1 conv on bordered images through the conv engine in 2-D mode: the f64 engine
+    (conv64) or the f32 one (conv1d).  w / b come folded in f64."""
 
-    def __init__(self, w, b, device):
+    def __init__(self, w, b, device, f64=True):
         Co, Ci, kh, kw = w.shape
-        self.Co, self.Ci, self.k = Co, Ci, kh
-        self.w = pack_km(w.reshape(Co, Ci, kh * kw).float()).to(device)
-        self.b = b.float().to(device) if b is not None else None
-        self.wx, self.wx_nmf = ops.pack_x6(self.w, 1, Ci, kh * kw, Co)
+        self.Co, self.Ci, self.k, self.f64 = Co, Ci, kh, f64
+        if f64:
+            self.w = pack_km(w.reshape(Co, Ci, kh * kw).double()).to(device)
+            self.b = b.double().to(device) if b is not None else None
+        else:
+            self.w = pack_km(w.reshape(Co, Ci, kh * kw).float()).to(device)
+            self.b = b.float().to(device) if b is not None else None
+            self.wx, self.wx_nmf = ops.pack_x6(self.w, 1, Ci, kh * kw, Co)
 
     def __call__(self, x, H, W, out, **kw):
         """x / out: bordered images [C][H+2][W+2], or [B][C][H+2][W+2] views (batch strides from the views)."""
@@ -68,6 +84,9 @@ class _Conv2d:
             pad = wrap + 1
         else:
             toff, pad = [0], 0
+        if self.f64:
+            return ops.conv64(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L,
+                              out=out, toff=toff, wrap=wrap, **_batch_kw(x, out, kw), **kw)
         return ops.conv1d(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L,
                           out=out, toff=toff, wrap=wrap, wx=self.wx, wx_nmf=self.wx_nmf, **_batch_kw(x, out, kw), **kw)
 
@@ -87,18 +106,22 @@ class _ConvT2d:
     # per output parity: list of (kernel index, source offset on the input grid)
     TAPS = {0: [(1, 0)], 1: [(0, 1), (2, 0)]}
 
-    def __init__(self, w, scale, shift, device):
+    def __init__(self, w, scale, shift, device, f64=True):
         Ci, Co = w.shape[0], w.shape[1]
-        self.Ci, self.Co = Ci, Co
+        self.Ci, self.Co, self.f64 = Ci, Co, f64
         wf = w.double() * scale.view(1, Co, 1, 1)
-        self.bias = shift.float().to(device)
+        self.bias = shift.double().to(device) if f64 else shift.float().to(device)
         self.phases = []
         for py in (0, 1):
             for px in (0, 1):
                 taps = [(ky, kx, dy, dx) for ky, dy in self.TAPS[py] for kx, dx in self.TAPS[px]]
                 wp = torch.stack([wf[:, :, ky, kx].t() for ky, kx, _, _ in taps], dim=-1)  # [Co, Ci, ntap]
-                wkm = pack_km(wp.float()).to(device)
-                self.phases.append((wkm, [(dy, dx) for _, _, dy, dx in taps]) + ops.pack_x6(wkm, 1, Ci, len(taps), Co))
+                dyx = [(dy, dx) for _, _, dy, dx in taps]
+                if f64:
+                    self.phases.append((pack_km(wp).to(device), dyx, None, 0))
+                else:
+                    wkm = pack_km(wp.float()).to(device)
+                    self.phases.append((wkm, dyx) + ops.pack_x6(wkm, 1, Ci, len(taps), Co))
 
     def __call__(self, x, H, W, out_cat):
         """x bordered [Ci][H+2][W+2] -> first Co channels of bordered out_cat [*][2H+2][2W+2]
@@ -107,35 +130,52 @@ class _ConvT2d:
         L = (H + 2) * wrap
         B = x.shape[0] if x.dim() == 4 else None
         # the phase convs write the zero border
-        ph = torch.empty((B or 1), 4, self.Co, H + 2, W + 2, device=x.device)
+        ph = torch.empty((B or 1), 4, self.Co, H + 2, W + 2, device=x.device, dtype=x.dtype)
         for i, (wp, taps, wx, wx_nmf) in enumerate(self.phases):
             toff = [dy * wrap + dx for dy, dx in taps]
             out = ph[:, i] if B else ph[0, i]
-            ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, out=out,
-                       toff=toff, wrap=wrap, out_act=ACT_RELU, wx=wx, wx_nmf=wx_nmf, **_batch_kw(x, out, {}))
-        for b in range(B or 1):
-            ops.interleave4(ph[b], out_cat[b] if B else out_cat, self.Co, H, W)
+            if self.f64:
+                ops.conv64(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, out=out,
+                           toff=toff, wrap=wrap, out_act=ACT_RELU, **_batch_kw(x, out, {}))
+            else:
+                ops.conv1d(x, wp, self.Ci, self.Co, len(taps), bias=self.bias, pad=0, Lin=L, Lout=L, out=out,
+                           toff=toff, wrap=wrap, out_act=ACT_RELU, wx=wx, wx_nmf=wx_nmf, **_batch_kw(x, out, {}))
+        if self.f64:
+            ops.interleave4_64(ph if B else ph[0], out_cat, self.Co, H, W)
+        else:
+            for b in range(B or 1):
+                ops.interleave4(ph[b], out_cat[b] if B else out_cat, self.Co, H, W)
 
 
 class RMVPEAMD:
-    def __init__(self, sd: dict, device: str = "cuda", n_blocks: int = 4):
+    def __init__(self, sd: dict, device: str = "cuda", n_blocks: int = 4, precision: str | None = None):
         dev = device
         self.device = dev
         self.nb = n_blocks
+        # The f0 is a per-frame decision (argmax over 360 bins, voicing threshold): by default the whole network
+        # runs in f64 (module note).  Any ops.PASSES name selects the f32 form at that conv arithmetic ("fp32sa":
+        # 6-pass split-bf16 with split accumulators, round 3's default).
+        self.precision = precision or os.environ.get("RVC_RMVPE_PRECISION", "f64")
+        if self.precision != "f64" and self.precision not in ops.PASSES:
+            raise ValueError(f"RMVPE precision must be 'f64' or one of {sorted(ops.PASSES)}")
+        self.f64 = self.precision == "f64"
+        f64 = self.f64
+        self.dt = torch.float64 if f64 else torch.float32
         self.mel_basis = torch.from_numpy(melbasis.mel_filterbank(16000, NFFT, N_MELS, 30, 8000))
         self.window = torch.hann_window(NFFT).to(dev)  # float32 periodic, as RMVPE.py:166
-        self.mel = ops.Conv(self.mel_basis.unsqueeze(-1), None, device=dev)
+        self.mel = (ops.Conv64 if f64 else ops.Conv)(self.mel_basis.unsqueeze(-1), None, device=dev)
         s, t = _fold_bn(sd, "unet.encoder.bn")
-        self.in_scale, self.in_shift = float(s[0]), float(t[0])
+        self.in_scale, self.in_shift = (float(s[0]), float(t[0])) if f64 else \
+            (float(s[0].float()), float(t[0].float()))
 
         def cbr(p):
             out = {}
             for conv, bn in (("conv.0", "conv.1"), ("conv.3", "conv.4")):
                 sc, sh = _fold_bn(sd, f"{p}.{bn}")
                 w = sd[f"{p}.{conv}.weight"].double() * sc.view(-1, 1, 1, 1)
-                out[conv] = _Conv2d(w.float(), sh.float(), dev)
+                out[conv] = _Conv2d(w if f64 else w.float(), sh if f64 else sh.float(), dev, f64)
             if f"{p}.shortcut.weight" in sd:
-                out["sc"] = _Conv2d(sd[f"{p}.shortcut.weight"].float(), sd[f"{p}.shortcut.bias"].float(), dev)
+                out["sc"] = _Conv2d(sd[f"{p}.shortcut.weight"], sd[f"{p}.shortcut.bias"], dev, f64)
             return out
 
         self.enc = [[cbr(f"unet.encoder.layers.{l}.conv.{b}") for b in range(n_blocks)] for l in range(5)]
@@ -145,24 +185,20 @@ class RMVPEAMD:
         for l in range(5):
             p = f"unet.decoder.layers.{l}"
             sc, sh = _fold_bn(sd, p + ".conv1.1")
-            self.dec.append((_ConvT2d(sd[p + ".conv1.0.weight"], sc, sh, dev),
+            self.dec.append((_ConvT2d(sd[p + ".conv1.0.weight"], sc, sh, dev, f64),
                              [cbr(f"{p}.conv2.{b}") for b in range(n_blocks)]))
-        self.cnn = _Conv2d(sd["cnn.weight"].float(), sd["cnn.bias"].float(), dev)
+        self.cnn = _Conv2d(sd["cnn.weight"], sd["cnn.bias"], dev, f64)
         g = "fc.0.gru."
-        self.w_ih = ops.Conv(torch.cat([sd[g + "weight_ih_l0"], sd[g + "weight_ih_l0_reverse"]], 0).float().unsqueeze(-1),
-                             torch.cat([sd[g + "bias_ih_l0"], sd[g + "bias_ih_l0_reverse"]], 0).float(), device=dev)
-        self.w_hh = torch.stack([sd[g + "weight_hh_l0"], sd[g + "weight_hh_l0_reverse"]], 0).float().contiguous().to(dev)
-        self.b_hh = torch.stack([sd[g + "bias_hh_l0"], sd[g + "bias_hh_l0_reverse"]], 0).float().contiguous().to(dev)
-        self.fc = ops.Conv(sd["fc.1.weight"].float().unsqueeze(-1), sd["fc.1.bias"].float(), device=dev)
-        self.gran = torch.zeros(1024, dtype=torch.int64, device=dev)  # the default stream's BiGRU hand-off scratch
+        Lin = ops.Conv64 if f64 else ops.Conv
+        self.w_ih = Lin(torch.cat([sd[g + "weight_ih_l0"], sd[g + "weight_ih_l0_reverse"]], 0).unsqueeze(-1),
+                        torch.cat([sd[g + "bias_ih_l0"], sd[g + "bias_ih_l0_reverse"]], 0), device=dev)
+        self.w_hh = torch.stack([sd[g + "weight_hh_l0"], sd[g + "weight_hh_l0_reverse"]], 0).to(self.dt).contiguous().to(dev)
+        self.b_hh = torch.stack([sd[g + "bias_hh_l0"], sd[g + "bias_hh_l0_reverse"]], 0).to(self.dt).contiguous().to(dev)
+        self.fc = Lin(sd["fc.1.weight"].unsqueeze(-1), sd["fc.1.bias"], device=dev)
+        self.gran_words = ops.GRU64_GRAN if f64 else 1024  # BiGRU hand-off scratch per sequence (int64 words)
+        self.gran = torch.zeros(self.gran_words, dtype=torch.int64, device=dev)  # the default stream's
         self._grans = {}
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        # The f0 is a per-frame decision (argmax over 360 bins, voicing threshold): RMVPE's convs run at the
-        # 6-pass split-bf16 arithmetic with split accumulators ("fp32sa") whatever ops.precision says (None =
-        # follow it).  With one accumulator the U-Net's error against an f64 evaluation was 1.5x the reference's own
-        # f32 error (scripts/rmvpe_prec.py); at 3 passes the salience moved by 1.5e-2 and at 1 pass by 0.24 on the
-        # synthetic weights, flipping decisions.  RMVPE is 5 % of a 48k clip's FLOPs and runs beside ContentVec.
-        self.precision = os.environ.get("RVC_RMVPE_PRECISION", "fp32sa")
 
     @classmethod
     def from_file(cls, path, device="cuda"):
@@ -171,11 +207,11 @@ class RMVPEAMD:
     # ------------------------------------------------------------------ pieces
     @_at_precision
     def mel_spectrogram(self, audio: torch.Tensor) -> torch.Tensor:
-        """MelSpectrogram.forward (RMVPE.py:162-181): audio [N] f32 -> log-mel [128][F]."""
+        """MelSpectrogram.forward (RMVPE.py:162-181): audio [N] f32 -> log-mel [128][F] (f64 in the f64 form)."""
         N = audio.numel()
         F = 1 + N // HOP
-        mag = torch.empty(NFFT // 2 + 1, F, device=audio.device)
-        ops.stft_mag(audio, self.window, mag, N, F, NFFT, HOP)
+        mag = torch.empty(NFFT // 2 + 1, F, device=audio.device, dtype=self.dt)
+        (ops.stft_mag64 if self.f64 else ops.stft_mag)(audio, self.window, mag, N, F, NFFT, HOP)
         return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
 
     @_at_precision
@@ -183,8 +219,8 @@ class RMVPEAMD:
         """B equal-length signals [B][N] -> log-mel [B][128][F] (the GEMMs batched, framing per signal)."""
         B, N = xb.shape
         F = 1 + N // HOP
-        mag = torch.empty(B, NFFT // 2 + 1, F, device=xb.device)
-        ops.stft_mag(xb, self.window, mag, N, F, NFFT, HOP)
+        mag = torch.empty(B, NFFT // 2 + 1, F, device=xb.device, dtype=self.dt)
+        (ops.stft_mag64 if self.f64 else ops.stft_mag)(xb, self.window, mag, N, F, NFFT, HOP)
         return self.mel(mag, out_act=ACT_LOGCLAMP, out_slope=1e-5)
 
     def _cbr(self, blk, x, H, W, out):
@@ -192,10 +228,10 @@ class RMVPEAMD:
         Co = blk["conv.0"].Co
         bshape = (x.shape[0],) if x.dim() == 4 else ()
         # 2-D convs cover the whole bordered image and write its border as 0: no zero-fill needed
-        h = torch.empty(*bshape, Co, H + 2, W + 2, device=dev)
+        h = torch.empty(*bshape, Co, H + 2, W + 2, device=dev, dtype=self.dt)
         blk["conv.0"](x, H, W, h, out_act=ACT_RELU)
         if "sc" in blk:
-            sc = torch.empty(*bshape, Co, H + 2, W + 2, device=dev)
+            sc = torch.empty(*bshape, Co, H + 2, W + 2, device=dev, dtype=self.dt)
             blk["sc"](x, H, W, sc)
             res = sc
         else:
@@ -208,46 +244,72 @@ class RMVPEAMD:
         to Tp = F rounded up to 32, input BatchNorm applied), Tp."""
         F = mel.shape[-1]
         Tp = 32 * ((F - 1) // 32 + 1)
-        x = torch.zeros(1, Tp + 2, N_MELS + 2, device=mel.device)
-        ops.mel_image(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
+        x = torch.zeros(1, Tp + 2, N_MELS + 2, device=mel.device, dtype=self.dt)
+        (ops.mel_image64 if self.f64 else ops.mel_image)(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
         return x, Tp
 
-    @_at_precision
-    def unet_seq(self, x: torch.Tensor, H: int) -> torch.Tensor:
-        """E2E up to the GRU input (RMVPE.py:143-144, 254): bordered image [1][H+2][130] (H % 32 == 0)
-        -> cnn head rows [384][H]."""
+    def _pool(self, x, pooled, C, H, W):
+        if self.f64:
+            ops.avgpool2_64(x, pooled, C, H, W)
+        elif x.dim() == 4:
+            for b in range(x.shape[0]):
+                ops.avgpool2(x[b], pooled[b], C, H, W)
+        else:
+            ops.avgpool2(x, pooled, C, H, W)
+
+    def _to_seq(self, img, seq, H, W):
+        if self.f64:
+            ops.img_to_seq64(img, seq, 3, H, W)
+        elif img.dim() == 4:
+            for b in range(img.shape[0]):
+                ops.img_to_seq(img[b], seq[b], 3, H, W)
+        else:
+            ops.img_to_seq(img, seq, 3, H, W)
+
+    def _unet(self, x, H, bshape):
+        """E2E up to the GRU input on bordered images x [(B)][1][H+2][130] -> cnn head rows [(B)][384][H]."""
         dev = x.device
         W = N_MELS
         cats = []
         C = 16
         for l in range(5):
-            cat = torch.zeros(2 * C, H + 2, W + 2, device=dev)
+            cat = torch.zeros(*bshape, 2 * C, H + 2, W + 2, device=dev, dtype=self.dt)
             for b, blk in enumerate(self.enc[l]):
-                out = cat[C:] if b == self.nb - 1 else torch.empty(C, H + 2, W + 2, device=dev)
+                out = cat[..., C:, :, :] if b == self.nb - 1 else \
+                    torch.empty(*bshape, C, H + 2, W + 2, device=dev, dtype=self.dt)
                 x = self._cbr(blk, x, H, W, out)
             cats.append((cat, C, H, W))
-            pooled = torch.zeros(C, H // 2 + 2, W // 2 + 2, device=dev)
-            ops.avgpool2(x, pooled, C, H, W)
+            pooled = torch.zeros(*bshape, C, H // 2 + 2, W // 2 + 2, device=dev, dtype=self.dt)
+            self._pool(x, pooled, C, H, W)
             x, H, W = pooled, H // 2, W // 2
             C *= 2
         for layer in self.inter:
             for blk in layer:
-                x = self._cbr(blk, x, H, W, torch.empty(blk["conv.0"].Co, H + 2, W + 2, device=dev))
+                x = self._cbr(blk, x, H, W, torch.empty(*bshape, blk["conv.0"].Co, H + 2, W + 2, device=dev,
+                                                        dtype=self.dt))
         for i, (convt, blocks) in enumerate(self.dec):
             cat, C, Ho, Wo = cats[-1 - i]
             convt(x, H, W, cat)
             x, H, W = cat, Ho, Wo
             for blk in blocks:
-                x = self._cbr(blk, x, H, W, torch.empty(blk["conv.0"].Co, H + 2, W + 2, device=dev))
-        img = torch.empty(3, H + 2, W + 2, device=dev)
+                x = self._cbr(blk, x, H, W, torch.empty(*bshape, blk["conv.0"].Co, H + 2, W + 2, device=dev,
+                                                        dtype=self.dt))
+        img = torch.empty(*bshape, 3, H + 2, W + 2, device=dev, dtype=self.dt)
         self.cnn(x, H, W, img)
-        seq = torch.empty(3 * W, H, device=dev)
-        ops.img_to_seq(img, seq, 3, H, W)
+        seq = torch.empty(*bshape, 3 * W, H, device=dev, dtype=self.dt)
+        self._to_seq(img, seq, H, W)
         return seq
 
-    def gran_ws(self, n: int = 1024) -> torch.Tensor:
-        """BiGRU hand-off scratch for the current stream: recurrences running at once on different streams (the
-        clip stream's alternating front pipelines) must not share one."""
+    @_at_precision
+    def unet_seq(self, x: torch.Tensor, H: int) -> torch.Tensor:
+        """E2E up to the GRU input (RMVPE.py:143-144, 254): bordered image [1][H+2][130] (H % 32 == 0)
+        -> cnn head rows [384][H]."""
+        return self._unet(x, H, ())
+
+    def gran_ws(self, n: int = 1) -> torch.Tensor:
+        """BiGRU hand-off scratch for ``n`` sequences on the current stream: recurrences running at once on
+        different streams (the clip stream's alternating front pipelines) must not share one."""
+        n *= self.gran_words
         s = torch.cuda.current_stream(self.device)
         if s == torch.cuda.default_stream(self.device) and n <= self.gran.numel():
             return self.gran
@@ -258,14 +320,25 @@ class RMVPEAMD:
             self._grans[key] = g
         return g
 
+    def _head(self, seq, B, Tp):
+        """W_ih GEMM -> BiGRU (B recurrences side by side) -> Linear + sigmoid: seq [(B)][384][Tp] ->
+        salience [(B)][360][Tp] f32."""
+        gi = self.w_ih(seq)  # [(B)][1536][Tp]
+        y = torch.empty(*((B,) if seq.dim() == 3 else ()), 512, Tp, device=seq.device, dtype=self.dt)
+        gran = self.gran_ws(min(B, ops.GRU_B_MAX))
+        if self.f64:
+            ops.bigru64_batched(gi, self.w_hh, self.b_hh, y, gran, self.err, B, Tp)
+            return self.fc(y, out_act=ACT_SIGMOID, out_f32=True)
+        if seq.dim() == 3:
+            ops.bigru_batched(gi, self.w_hh, self.b_hh, y, gran, self.err, B, Tp)
+        else:
+            ops.bigru(gi, self.w_hh, self.b_hh, y, gran, self.err, Tp)
+        return self.fc(y, out_act=ACT_SIGMOID)
+
     @_at_precision
     def head(self, seq: torch.Tensor) -> torch.Tensor:
-        """BiGRU + Linear + Sigmoid (RMVPE.py:254-260, 141): seq [384][Tp] -> salience [360][Tp]."""
-        Tp = seq.shape[-1]
-        gi = self.w_ih(seq)  # [1536][Tp]
-        y = torch.empty(512, Tp, device=seq.device)
-        ops.bigru(gi, self.w_hh, self.b_hh, y, self.gran_ws(), self.err, Tp)
-        return self.fc(y, out_act=ACT_SIGMOID)
+        """BiGRU + Linear + Sigmoid (RMVPE.py:254-260, 141): seq [384][Tp] -> salience [360][Tp] (f32)."""
+        return self._head(seq, 1, seq.shape[-1])
 
     @_at_precision
     def salience(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
@@ -285,57 +358,28 @@ class RMVPEAMD:
     @_at_precision
     def salience_batch(self, mel: torch.Tensor) -> tuple[torch.Tensor, int]:
         """salience for B clips at once: mel [B][128][F] -> [B][360][Tp].  Every conv of the U-Net, the
-        W_ih / fc GEMMs and the BiGRU (B recurrences side by side) run batched; the per-image glue
-        kernels (mel image, pooling, phase interleave, image->sequence) run per clip."""
+        W_ih / fc GEMMs and the BiGRU (B recurrences side by side) run batched (and in the f64 form the image
+        glue kernels too)."""
         dev = mel.device
         B, _, F = mel.shape
         Tp = 32 * ((F - 1) // 32 + 1)
-        H, W = Tp, N_MELS
-        x = torch.zeros(B, 1, H + 2, W + 2, device=dev)
-        for b in range(B):
-            ops.mel_image(mel[b], x[b], N_MELS, F, Tp, self.in_scale, self.in_shift)
-        cats = []
-        C = 16
-        for l in range(5):
-            cat = torch.zeros(B, 2 * C, H + 2, W + 2, device=dev)
-            for bi, blk in enumerate(self.enc[l]):
-                out = cat[:, C:] if bi == self.nb - 1 else torch.empty(B, C, H + 2, W + 2, device=dev)
-                x = self._cbr(blk, x, H, W, out)
-            cats.append((cat, C, H, W))
-            pooled = torch.zeros(B, C, H // 2 + 2, W // 2 + 2, device=dev)
+        x = torch.zeros(B, 1, Tp + 2, N_MELS + 2, device=dev, dtype=self.dt)
+        if self.f64:
+            ops.mel_image64(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
+        else:
             for b in range(B):
-                ops.avgpool2(x[b], pooled[b], C, H, W)
-            x, H, W = pooled, H // 2, W // 2
-            C *= 2
-        for layer in self.inter:
-            for blk in layer:
-                x = self._cbr(blk, x, H, W, torch.empty(B, blk["conv.0"].Co, H + 2, W + 2, device=dev))
-        for i, (convt, blocks) in enumerate(self.dec):
-            cat, C, Ho, Wo = cats[-1 - i]
-            convt(x, H, W, cat)
-            x, H, W = cat, Ho, Wo
-            for blk in blocks:
-                x = self._cbr(blk, x, H, W, torch.empty(B, blk["conv.0"].Co, H + 2, W + 2, device=dev))
-        img = torch.empty(B, 3, H + 2, W + 2, device=dev)
-        self.cnn(x, H, W, img)
-        seq = torch.empty(B, 3 * W, H, device=dev)
-        for b in range(B):
-            ops.img_to_seq(img[b], seq[b], 3, H, W)
-        gi = self.w_ih(seq)  # [B][1536][Tp]
-        y = torch.empty(B, 512, Tp, device=dev)
-        gran = self.gran_ws(1024 * min(B, ops.GRU_B_MAX))
-        ops.bigru_batched(gi, self.w_hh, self.b_hh, y, gran, self.err, B, Tp)
-        return self.fc(y, out_act=ACT_SIGMOID), Tp
+                ops.mel_image(mel[b], x[b], N_MELS, F, Tp, self.in_scale, self.in_shift)
+        seq = self._unet(x, Tp, (B,))
+        return self._head(seq, B, Tp), Tp
 
     def f0_device_batch(self, xb: torch.Tensor, thred: float = 0.03, pitch_shift: float = 0.0, post=None,
                         want_f0=False, want_salience=False):
         """B equal-length signals [B][N] -> (coarse int64 [B][F], pitchf f32 [B][F]) [+ raw f0 f64 [B][F]]
         [+ salience [B][360][Tp]]; same per-clip result as ``f0_device`` up to the summation order of the batched
         GEMMs (split-K follows the batched grid)."""
-        with ops.precision(self.precision or ops.get_precision()):
-            mel = self.mel_spectrogram_batch(xb)
-            B, _, F = mel.shape
-            sal, Tp = self.salience_batch(mel)
+        mel = self.mel_spectrogram_batch(xb)
+        B, _, F = mel.shape
+        sal, Tp = self.salience_batch(mel)
         coarse = torch.empty(B, F, dtype=torch.int64, device=xb.device)
         pitchf = torch.empty(B, F, device=xb.device)
         f0 = torch.empty(B, F, dtype=torch.float64, device=xb.device) if want_f0 else None
@@ -349,10 +393,9 @@ class RMVPEAMD:
                   post=None):
         """audio [N] f32 device -> (coarse int64 [F], pitchf f32 [F], f0 f64 [F] | None) on the device;
         ``post`` (ops.F0Post) adds get_f0's autotune / f0-file steps."""
-        with ops.precision(self.precision or ops.get_precision()):
-            mel = self.mel_spectrogram(audio)
-            F = mel.shape[-1]
-            sal, Tp = self.salience(mel)
+        mel = self.mel_spectrogram(audio)
+        F = mel.shape[-1]
+        sal, Tp = self.salience(mel)
         return self.decode(sal, Tp, F, thred, pitch_shift, want_f0, post)
 
     def check_error(self):

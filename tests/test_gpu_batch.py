@@ -27,20 +27,44 @@ def clips(n, secs, seed):
     return [torch.from_numpy(synthetic.synthetic_audio(secs, seed=seed + i)).to(DEV) for i in range(n)]
 
 
+@pytest.mark.parametrize("f64", [False, True])
 @pytest.mark.parametrize("B", [1, 3, 18])
-def test_bigru_batched_bit_identical(models, B):
+def test_bigru_batched_bit_identical(models, B, f64):
+    """B recurrences side by side (two launches at B = 18) equal each sequence's own launch, in the f32 form
+    (rmvpe.hip) and the f64 one (rmvpe64.hip), and the f64 form matches torch's f64 GRU on the host."""
     _, rm, _, _ = models
     T = 96
+    dt = torch.float64 if f64 else torch.float32
     g = torch.Generator().manual_seed(B)
-    gi = (torch.randn(B, 1536, T, generator=g) * 0.5).to(DEV)
-    y = torch.empty(B, 512, T, device=DEV)
-    gran = torch.zeros(1024 * min(B, ops.GRU_B_MAX), dtype=torch.int64, device=DEV)
-    ops.bigru_batched(gi, rm.w_hh, rm.b_hh, y, gran, rm.err, B, T)
+    gi = (torch.randn(B, 1536, T, generator=g, dtype=torch.float64) * 0.5).to(dt).to(DEV)
+    whh = (torch.randn(2, 768, 256, generator=g, dtype=torch.float64) * 0.06).to(dt).to(DEV)
+    bhh = (torch.randn(2, 768, generator=g, dtype=torch.float64) * 0.1).to(dt).to(DEV)
+    y = torch.empty(B, 512, T, device=DEV, dtype=dt)
+    words = ops.GRU64_GRAN if f64 else 1024
+    gran = torch.zeros(words * min(B, ops.GRU_B_MAX), dtype=torch.int64, device=DEV)
+    (ops.bigru64_batched if f64 else ops.bigru_batched)(gi, whh, bhh, y, gran, rm.err, B, T)
     for b in range(B):
-        yb = torch.empty(512, T, device=DEV)
-        ops.bigru(gi[b].contiguous(), rm.w_hh, rm.b_hh, yb, rm.gran, rm.err, T)
-        assert torch.equal(y[b], yb)
+        yb = torch.empty(1, 512, T, device=DEV, dtype=dt)
+        g1 = torch.zeros(words, dtype=torch.int64, device=DEV)
+        if f64:
+            ops.bigru64_batched(gi[b:b + 1].contiguous(), whh, bhh, yb, g1, rm.err, 1, T)
+        else:
+            ops.bigru(gi[b].contiguous(), whh, bhh, yb[0], g1, rm.err, T)
+        assert torch.equal(y[b], yb[0])
     rm.check_error()
+    if f64:  # torch's own f64 GRU (what oracle.rmvpe.bigru_torch runs), fed the same gi through an identity W_ih
+        x = gi[0].cpu().t()  # [T][1536]
+        gru = torch.nn.GRU(1536, 256, bidirectional=True, batch_first=True).double()
+        with torch.no_grad():
+            for d, sfx in enumerate(("", "_reverse")):
+                eye = torch.zeros(768, 1536, dtype=torch.float64)
+                eye[:, d * 768:(d + 1) * 768] = torch.eye(768, dtype=torch.float64)
+                getattr(gru, "weight_ih_l0" + sfx).copy_(eye)
+                getattr(gru, "bias_ih_l0" + sfx).zero_()
+                getattr(gru, "weight_hh_l0" + sfx).copy_(whh[d].cpu())
+                getattr(gru, "bias_hh_l0" + sfx).copy_(bhh[d].cpu())
+            want = gru(x.unsqueeze(0))[0][0].t()  # [512][T]
+        assert (y[0].cpu() - want).abs().max().item() < 1e-12
 
 
 def test_contentvec_batched_matches_per_clip(models):
@@ -79,8 +103,8 @@ def test_rmvpe_batched_matches_per_clip(models):
         sd_b = sal_b[b, :, :F].t().cpu().numpy().astype(np.float64)
         sd_1 = sal[:, :F].t().cpu().numpy().astype(np.float64)
         _, _, rep_b = f0check.check(None, synthetic.rmvpe_state_dict(72), audio,
-                                    device=(sd_b, f0_b[b].cpu().numpy()))
-        _, _, rep_1 = f0check.check(None, synthetic.rmvpe_state_dict(72), audio, device=(sd_1, None))
+                                    device=(sd_b, f0_b[b].cpu().numpy()), exact=rm.f64)
+        _, _, rep_1 = f0check.check(None, synthetic.rmvpe_state_dict(72), audio, device=(sd_1, None), exact=rm.f64)
         differ = np.flatnonzero((coarse_b[b] != coarse).cpu().numpy())
         allowed = set(rep_b["flips_vs_exact"]) | set(rep_1["flips_vs_exact"])
         for t in differ:  # the coarse quantiser of an equal decision may still round a 1e-6 pitch change
