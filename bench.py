@@ -3,10 +3,16 @@ per GPU per step (BASELINE.json configs[1]; N>1 = configs[3]-style utterance sha
 output waveforms gathered to rank 0 over RCCL).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--no-cpu-baseline] [--no-stream]
+    python bench.py --gpus N --utterances 120 --seconds 30     # BASELINE configs[3]: 1 h over N GPUs
 
 Default: a clip stream (VC.pipeline_device_stream) -- K steps are K clips per GPU, clip k+1's front end
 (filtfilt, RMVPE, ContentVec) running on its own streams under clip k's synthesizer; the line also carries
 "per_call", the same K clips as one finished pipeline_device call each.
+
+--utterances U (BASELINE configs[3], SURVEY §8(d) cfg 4): a fixed job of U utterances of --seconds each (1 h =
+120 x 30 s), sharded longest-first over the ranks (rvc_amd.shard.shard_utterances), each rank's share issued as
+one clip stream, the output waveforms gathered to rank 0 by grouped send / recv (RCCL over xGMI); a step is the
+whole job, "scaling": "strong".
 
 --gpus N without WORLD_SIZE in the environment starts N ranks itself (torch.distributed.run as a
 child process, one rank per GPU); under an external launcher WORLD_SIZE must equal N.
@@ -307,6 +313,9 @@ def main():
                          "the default clip stream (VC.pipeline_device_stream: clip k+1's filtfilt / f0 / features on "
                          "a front stream while clip k's synthesizer runs on a back stream; K steps = K clips per GPU, "
                          "all issued inside the timed region)")
+    ap.add_argument("--utterances", type=int, default=0,
+                    help="> 0: BASELINE configs[3] -- a fixed job of U utterances sharded over the ranks (strong "
+                         "scaling; a step = the whole job)")
     ap.add_argument("--index-rate", type=float, default=0.0,
                     help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
@@ -348,8 +357,17 @@ def main():
         cap = args.f0.split("-", 1)[1]
         vc.crepe[cap] = CrepeAMD(synthetic.crepe_state_dict(1240, cap), cap, dev)
     # inputs resident in HBM before the timed region: one distinct clip per chunk
-    clips = [torch.from_numpy(synthetic.synthetic_audio(args.seconds, seed=1000 + 97 * rank + c)).to(dev)
-             for c in range(max(1, args.chunks))]
+    mine = None
+    if args.utterances > 0:  # cfg 4: this rank's share of the whole job (seed = 1000 + utterance index, §8(d))
+        from rvc_amd.shard import shard_utterances
+        if args.graph or args.batch > 1 or args.chunks > 1:
+            raise SystemExit("bench.py: --utterances runs the clip stream (no --graph / --batch / --chunks)")
+        mine = shard_utterances([int(args.seconds * 16000)] * args.utterances, world)[rank]
+        clips = [torch.from_numpy(synthetic.synthetic_audio(args.seconds, seed=1000 + i)).to(dev) for i in mine]
+        args.stream = True
+    else:
+        clips = [torch.from_numpy(synthetic.synthetic_audio(args.seconds, seed=1000 + 97 * rank + c)).to(dev)
+                 for c in range(max(1, args.chunks))]
     audio_dev = clips[0]
     vc.seed = 17 + rank
 
@@ -387,6 +405,18 @@ def main():
     def run_stream(nsteps):
         # one stream over nsteps x chunks clips: every clip's whole pass is issued inside the call, and the
         # call returns after the last clip's output is ordered on this stream
+        if mine is not None:  # cfg 4: a step is the whole job -- this rank's utterances, then the gather
+            last = None
+            for _ in range(nsteps):
+                outs = vc.pipeline_device_stream(hub, net_g, 0, clips, 0, "v2", 0.33, index, args.index_rate,
+                                                 args.f0) if clips else []
+                if dist is not None:
+                    got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0,
+                                           stats=p2p)
+                    if got is not None:
+                        gathered[0] += sum(len(g) for g in got)
+                last = outs[-1] if outs else last
+            return last
         order = [clips[i % len(clips)] for i in range(nsteps * len(clips))]
         outs = vc.pipeline_device_stream(hub, net_g, 0, order, 0, "v2", 0.33, index, args.index_rate, args.f0,
                                          batch=args.batch)
@@ -395,6 +425,8 @@ def main():
             if got is not None:
                 gathered[0] += sum(len(g) for g in got)
         return outs[-1]
+
+    p2p = {}
 
     gathered = [0]
 
@@ -423,7 +455,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     per_call = None
-    if args.stream and world == 1 and not args.no_per_call:
+    if args.stream and world == 1 and not args.no_per_call and mine is None:
         # the same K steps as one pipeline_device call per clip, each finished before the next (the
         # reference's loop): the stream's gain over it, measured on the same box right after
         torch.cuda.synchronize()
@@ -434,12 +466,16 @@ def main():
         dt1 = time.perf_counter() - t1
         per_call = {"value": round(args.steps * len(clips) * (out.numel() / float(args.sr)) / dt1, 3),
                     "ms_per_step": round(dt1 / args.steps * 1e3, 3)}
-    audio_s = out.numel() / float(args.sr)  # every clip has the same length
-    value = world * args.steps * len(clips) * audio_s / dt  # whole job: every rank's clips over the max time
+    # every clip has the same length (a cfg-4 rank with no utterances has no output of its own)
+    audio_s = out.numel() / float(args.sr) if out is not None else 0.0  # (only rank 0, which has one, prints)
+    if mine is not None:  # cfg 4: the whole job's audio over the max-over-ranks time (strong scaling)
+        value = args.steps * args.utterances * audio_s / dt
+    else:
+        value = world * args.steps * len(clips) * audio_s / dt  # whole job: every rank's clips over the max time
     gathered_per_step = gathered[0] / max(args.warmup + args.steps, 1) if dist is not None else len(clips)
 
     roof = None
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and mine is None:
         with ConvProbe() as probe:  # one eager pass (a graph replay launches no host-side conv calls)
             # park the GPU first so that the host queues the pass's launches ahead of it: each event pair then
             # brackets its kernel, not the host's issue gap before it (short launches would otherwise count
@@ -502,11 +538,17 @@ def main():
                                "RCCL gather over xGMI" if backend == "nccl" else "gloo (ranks share a GPU)"),
                 "waveforms_gathered_per_step": gathered_per_step,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPES[args.precision],
+                "higher_is_better": True, "scaling": "strong" if mine is not None else "weak", "vs_baseline": None,
+                "dtype": DTYPES[args.precision],
                 "data": "synthetic 16 kHz audio (SURVEY §8d generator), random-init weights of the true shapes",
-                "config": {"workload": f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, "
-                                       f"{'one' if len(clips) == 1 else f'{len(clips)} x'} "
-                                       f"{args.seconds:g} s clip per GPU per step, "
+                "config": {"workload": (f"BASELINE configs[3]: {args.utterances} x {args.seconds:g} s utterances "
+                                        f"({args.utterances * args.seconds / 3600:g} h) sharded longest-first over "
+                                        f"{world} GPU(s), one clip stream per rank, waveforms gathered to rank 0 by "
+                                        f"grouped send/recv; VC.pipeline {args.sr // 1000}k v2, ContentVec-768, "
+                                        f"{args.f0} f0, " if mine is not None else
+                                        f"VC.pipeline {args.sr // 1000}k v2, ContentVec-768, {args.f0} f0, "
+                                        f"{'one' if len(clips) == 1 else f'{len(clips)} x'} "
+                                        f"{args.seconds:g} s clip per GPU per step, ")
                                        + (f"IVF-Flat index_rate {args.index_rate:g}" if index is not None else "no index")
                                        + ", protect 0.33" + (", hipGraph replay per clip" if args.graph else "")
                                        + (", clip stream (clip k+1 f0/features under clip k synthesizer)"
@@ -514,10 +556,13 @@ def main():
                                        + (f", RMVPE + ContentVec batched {args.batch} clips per pass"
                                           if args.batch > 1 else ""),
                            "model": f"RVC v2 {args.sr // 1000}k (NSF-HiFiGAN) + ContentVec + {args.f0}",
-                           "global_batch": world * len(clips),
+                           "global_batch": args.utterances if mine is not None else world * len(clips),
                            "seq_len": int(args.seconds * 16000), "parallelism": f"utterance-sharded x{world}",
                            "output_seconds_per_clip": round(audio_s, 4)},
                 "per_call": per_call, "roofline": roof, "cpu_baseline": cpu}
+        if mine is not None:
+            line["utterances_per_rank"] = len(mine)
+            line["gather_bytes_recv_per_step"] = p2p.get("bytes_recv", 0)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -88,3 +88,11 @@ def extract_features(W, source, output_layer=12):
 
 def final_proj(W, x):
     return F.linear(x, W["final_proj.weight"], W["final_proj.bias"])
+
+
+def n_layers(W):
+    """Encoder layers in the weight dict (transformers' last_hidden_state runs all of them)."""
+    n = 0
+    while f"encoder.layers.{n}.fc1.weight" in W:
+        n += 1
+    return n

@@ -112,13 +112,19 @@ def segment_points(audio: np.ndarray, c: Consts):
 
 
 def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, z_noise, sine_noise, trace=None,
-                     index=None, big_npy=None, index_rate=0.0):
-    """VC.voice_conversion (convert.py:328-386), ``.pt`` embedder, ``.pth`` model; ``index`` is an
-    ``IVFFlatIndex`` searched by the numpy restatement in ``oracle.ivf`` (convert.py:349-359)."""
+                     index=None, big_npy=None, index_rate=0.0, embed_suffix=".pt"):
+    """VC.voice_conversion (convert.py:328-386), ``.pth`` model; the embedder is ``.pt`` (fairseq
+    extract_features at layer 9 (v1) / 12 (v2), convert.py:337-340) or ``.safetensors`` (transformers
+    ``model(feats)["last_hidden_state"]``: every layer, final_proj on it for v1, convert.py:342-345) -- the same
+    network (``Wc`` in fairseq names); ``index`` is an ``IVFFlatIndex`` searched by the numpy restatement in
+    ``oracle.ivf`` (convert.py:349-359)."""
     window = 160
     feats = torch.from_numpy(audio0).float().view(1, -1)
     with torch.no_grad():
-        x = cv.extract_features(Wc, feats, 9 if version == "v1" else 12)
+        if embed_suffix == ".safetensors":
+            x = cv.extract_features(Wc, feats, cv.n_layers(Wc))
+        else:
+            x = cv.extract_features(Wc, feats, 9 if version == "v1" else 12)
         feats = cv.final_proj(Wc, x) if version == "v1" else x
         if trace is not None:
             trace["feats"] = feats.clone()
@@ -155,7 +161,7 @@ def voice_conversion(Wc, Ws, cfg, sid, audio0, pitch, pitchf, version, protect, 
 
 def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, noise, trace=None, index=None,
              index_rate=0.0, crepe=None, autotune_strength=None, inp_f0=None, volume_envelope=1.0, f0_track=None,
-             pm=False):
+             pm=False, embed_suffix=".pt"):
     """VC.pipeline (convert.py:388-458): f0 = rmvpe (or crepe), optional index, autotune, f0 file
     (``inp_f0`` [n][2] f32) and volume envelope.
 
@@ -200,7 +206,7 @@ def pipeline(Wc, Ws, Wr, mel_basis, cfg, sid, audio, pitch, version, protect, no
         tr = {} if trace is not None else None
         out = voice_conversion(Wc, Ws, cfg, sid_t, a0, pch, pchf, version, protect,
                                noise(seg, "z", (1, cfg[2], T)), noise(seg, "sine", (1, T * upp, 1)), tr,
-                               index=index, big_npy=big_npy, index_rate=index_rate)
+                               index=index, big_npy=big_npy, index_rate=index_rate, embed_suffix=embed_suffix)
         if trace is not None:
             trace.setdefault("segments", []).append(tr)
         return out[c.t_pad_tgt: -c.t_pad_tgt]

@@ -2,8 +2,11 @@
 (main/library/architectures/fairseq.py:1459 -> forward :1412-1431), the ``model`` that
 ``VC.voice_conversion`` calls at convert.py:337-340.
 
-Loaded from a fairseq ``.pt`` dict (``fairseq.py:30-36``); pos_conv weight-norm (dim 2)
-folded on the host at load.  Activations stay channels-first [C][T] on the device:
+Loaded from a fairseq ``.pt`` dict (``fairseq.py:30-36``), or (``from_transformers``) from the transformers
+layout the reference loads for a ``.safetensors`` embedder (``HubertModelWithFinalProj.from_pretrained``,
+main/library/utils.py:157-165: config.json + model.safetensors); pos_conv weight-norm (dim 2) folded on the
+host at load.  The two layouts are the same network; the embed suffix only changes which layer feeds
+final_proj (``embed_cf``, convert.py:337-345).  Activations stay channels-first [C][T] on the device:
 
   conv FE   conv1d(1->512, k10 s5) + chnorm_gelu (GroupNorm(512,512) + GELU), 6 x conv1d(k3/k2, s2) + GELU
   proj      layernorm_cf(512) + conv1d(K=1, 512->768)
@@ -43,6 +46,67 @@ class _FinalProj:
         out = torch.empty(1, T, y.shape[0], device=x.device)
         ops.transpose(y, out, 1, y.shape[0], T)
         return out
+
+
+# transformers HubertModel parameter names -> fairseq's (the layout ContentVecAMD is built from); the weight-norm
+# pair is "parametrizations.weight.original0 / 1" (torch.nn.utils.parametrizations) or "weight_g / weight_v"
+_HF_TOP = {"masked_spec_embed": "mask_emb",
+           "feature_extractor.conv_layers.0.layer_norm.weight": "feature_extractor.conv_layers.0.2.weight",
+           "feature_extractor.conv_layers.0.layer_norm.bias": "feature_extractor.conv_layers.0.2.bias",
+           "feature_projection.layer_norm.weight": "layer_norm.weight",
+           "feature_projection.layer_norm.bias": "layer_norm.bias",
+           "feature_projection.projection.weight": "post_extract_proj.weight",
+           "feature_projection.projection.bias": "post_extract_proj.bias",
+           "encoder.pos_conv_embed.conv.bias": "encoder.pos_conv.0.bias",
+           "encoder.pos_conv_embed.conv.parametrizations.weight.original0": "encoder.pos_conv.0.weight_g",
+           "encoder.pos_conv_embed.conv.parametrizations.weight.original1": "encoder.pos_conv.0.weight_v",
+           "encoder.pos_conv_embed.conv.weight_g": "encoder.pos_conv.0.weight_g",
+           "encoder.pos_conv_embed.conv.weight_v": "encoder.pos_conv.0.weight_v",
+           "encoder.layer_norm.weight": "encoder.layer_norm.weight", "encoder.layer_norm.bias": "encoder.layer_norm.bias",
+           "final_proj.weight": "final_proj.weight", "final_proj.bias": "final_proj.bias"}
+_HF_LAYER = {"attention.q_proj": "self_attn.q_proj", "attention.k_proj": "self_attn.k_proj",
+             "attention.v_proj": "self_attn.v_proj", "attention.out_proj": "self_attn.out_proj",
+             "layer_norm": "self_attn_layer_norm", "feed_forward.intermediate_dense": "fc1",
+             "feed_forward.output_dense": "fc2", "final_layer_norm": "final_layer_norm"}
+
+
+def hf_to_fairseq(sd: dict) -> dict:
+    """A transformers ``HubertModel(WithFinalProj)`` state dict under fairseq's names; raises on a key this
+    network does not have (a different architecture must not load silently)."""
+    import re
+    out = {}
+    for k, v in sd.items():
+        k2 = k[len("hubert."):] if k.startswith("hubert.") else k
+        if k2 in _HF_TOP:
+            out[_HF_TOP[k2]] = v
+            continue
+        m = re.fullmatch(r"feature_extractor\.conv_layers\.(\d+)\.conv\.weight", k2)
+        if m:
+            out[f"feature_extractor.conv_layers.{m.group(1)}.0.weight"] = v
+            continue
+        m = re.fullmatch(r"encoder\.layers\.(\d+)\.(.+)\.(weight|bias)", k2)
+        if m and m.group(2) in _HF_LAYER:
+            out[f"encoder.layers.{m.group(1)}.{_HF_LAYER[m.group(2)]}.{m.group(3)}"] = v
+            continue
+        raise ValueError(f"ContentVecAMD.from_transformers: unexpected parameter {k!r}")
+    return out
+
+
+def hf_config_to_fairseq(c: dict) -> dict:
+    """The transformers HubertConfig fields this build runs -> fairseq cfg["model"]; NotImplementedError for
+    another layout (stable layer norm, layer-normed extractor, other conv stacks or activations)."""
+    want = dict(feat_extract_norm="group", do_stable_layer_norm=False, conv_bias=False, hidden_act="gelu",
+                feat_extract_activation="gelu", conv_dim=[512] * 7, conv_stride=[5, 2, 2, 2, 2, 2, 2],
+                conv_kernel=[10, 3, 3, 3, 3, 2, 2], num_conv_pos_embeddings=128)
+    for k, v in want.items():
+        got = c.get(k, v)
+        if (list(got) if isinstance(got, (list, tuple)) else got) != v:
+            raise NotImplementedError(f"transformers HuBERT with {k}={got!r}: ContentVec/HuBERT-base layout only")
+    if c.get("feat_proj_layer_norm", True) is not True or abs(c.get("layer_norm_eps", 1e-5) - 1e-5) > 1e-12:
+        raise NotImplementedError("transformers HuBERT: feat_proj_layer_norm with eps 1e-5 only")
+    return dict(extractor_mode="default", layer_norm_first=False, encoder_embed_dim=c.get("hidden_size", 768),
+                encoder_attention_heads=c.get("num_attention_heads", 12),
+                conv_pos_groups=c.get("num_conv_pos_embedding_groups", 16))
 
 
 class ContentVecAMD:
@@ -86,6 +150,50 @@ class ContentVecAMD:
             i += 1
         self.final_proj = _FinalProj(Conv(W["final_proj.weight"].unsqueeze(-1), W["final_proj.bias"], device=dev))
         self.device = dev
+        self.embed_suffix = ".pt"
+
+    @classmethod
+    def from_transformers(cls, path: str, device: str = "cuda") -> "ContentVecAMD":
+        """``HubertModelWithFinalProj.from_pretrained(path)`` (main/library/utils.py:157-165) without transformers:
+        ``path`` is the model directory (config.json + model.safetensors, or *.safetensors shards) or a
+        .safetensors file with config.json beside it."""
+        import glob
+        import json
+        import os
+        from safetensors.torch import load_file
+        d = path if os.path.isdir(path) else os.path.dirname(path)
+        files = [path] if not os.path.isdir(path) else sorted(glob.glob(os.path.join(d, "*.safetensors")))
+        if not files:
+            raise FileNotFoundError(f"no .safetensors weights under {path}")
+        with open(os.path.join(d, "config.json")) as f:
+            cfg = json.load(f)
+        sd = {}
+        for fn in files:
+            sd.update(load_file(fn))
+        m = cls({"cfg": {"model": hf_config_to_fairseq(cfg)}, "model": hf_to_fairseq(sd)}, device)
+        m.embed_suffix = ".safetensors"
+        return m
+
+    def embed_cf(self, wav: torch.Tensor, version: str, embed_suffix: str | None = None) -> torch.Tensor:
+        """The features VC.voice_conversion takes from the embedder (convert.py:337-345), channels-first:
+        ".pt" (fairseq extract_features): layer 9 + final_proj for v1, layer 12 for v2; ".safetensors"
+        (transformers, ``model(feats)["last_hidden_state"]``): the last layer, + final_proj for v1."""
+        suffix = embed_suffix or self.embed_suffix
+        if suffix == ".safetensors":
+            feats = self.features_cf(wav, len(self.layers))
+        elif suffix == ".pt":
+            feats = self.features_cf(wav, 9 if version == "v1" else 12)
+        else:
+            raise NotImplementedError(f"embedder {suffix!r}: .pt and .safetensors are on the MI355X path")
+        return self.final_proj.conv(feats) if version == "v1" else feats
+
+    def __call__(self, feats: torch.Tensor) -> dict:
+        """The transformers forward as convert.py:343 calls it: feats [1, N] -> {"last_hidden_state": [1, T_f, 768]}."""
+        xc = self.features_cf(feats.reshape(-1).float().contiguous(), len(self.layers))
+        E, T = xc.shape
+        out = torch.empty(1, T, E, device=xc.device)
+        ops.transpose(xc, out, 1, E, T)
+        return {"last_hidden_state": out}
 
     def features_cf(self, wav: torch.Tensor, output_layer: int = 12) -> torch.Tensor:
         """wav: device f32 [N] (16 kHz) -> encoder output after ``output_layer`` layers, [768][T_f];

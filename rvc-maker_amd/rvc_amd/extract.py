@@ -133,12 +133,11 @@ def read_wave(wav_path, normalize=False):
 
 
 def embed_file(model, wav: np.ndarray, version: str, device) -> np.ndarray:
-    """process_file_embedding's model call (extract.py:278-290): [T_f, 768] (v2, layer 12) or
-    [T_f, 256] (v1, layer 9 + final_proj), f32 on the host."""
+    """process_file_embedding's model call (extract.py:278-290) for the model's embedder kind (ContentVecAMD
+    .embed_suffix): [T_f, 768] (v2) or [T_f, 256] (v1 final_proj; on layer 9 for ".pt", on the last layer for
+    ".safetensors"), f32 on the host."""
     x = torch.from_numpy(np.ascontiguousarray(wav.reshape(-1))).to(device)
-    feats = model.features_cf(x, 9 if version == "v1" else 12)
-    if version == "v1":
-        feats = model.final_proj.conv(feats)
+    feats = model.embed_cf(x, version)
     E, T = feats.shape
     out = torch.empty(T, E, device=x.device)
     ops.transpose(feats, out, 1, E, T)

@@ -19,8 +19,9 @@ index file is read without faiss (faiss_index.py) and kept resident per path.
 f0 methods: "rmvpe" and "crepe-{tiny,small,medium,large,full}" (crepe.py), both on the device.
 
 f0 autotune and f0 files run inside the f0 decode kernels; volume_envelope != 1 (change_rms) runs on
-the device after the segment loop.  Not on this path (raise): other f0 methods, ONNX/safetensors models,
-no-f0 models.
+the device after the segment loop.  Embedders: fairseq ``.pt`` and transformers ``.safetensors``
+(``ContentVecAMD.from_transformers``; the suffix picks the layer final_proj reads, convert.py:337-345).  Not on
+this path (raise): other f0 methods, ONNX models, no-f0 models.
 """
 from __future__ import annotations
 
@@ -65,6 +66,7 @@ class VC:
         self.device = config.device
         self.is_half = config.is_half
         self.rmvpe = rmvpe
+        self.embed_suffix = None  # pipeline()'s embed_suffix (convert.py:390); None = the model's own
         self.crepe = dict(crepe or {})  # capacity -> CrepeAMD (loaded on first use otherwise)
         self.noise_fn = None  # parity hook: noise_fn(seg, "z"|"sine", shape) -> device tensor
         self.seed = 0
@@ -124,11 +126,9 @@ class VC:
 
     # ------------------------------------------------------------------ device pieces
     def features_device(self, model, a0, version):
-        """convert.py:337-340: embedder features of segment a0 [N], channels-first [E][T_f]."""
-        feats = model.features_cf(a0, 9 if version == "v1" else 12)
-        if version == "v1":
-            feats = model.final_proj.conv(feats)
-        return feats
+        """convert.py:337-345: embedder features of segment a0 [N] (or [B][N]), channels-first [(B)][E][T_f], for
+        the pipeline's embed suffix (".pt": layer 9 + final_proj for v1; ".safetensors": the last layer)."""
+        return model.embed_cf(a0, version, self.embed_suffix)
 
     def voice_conversion_device(self, model, net_g, sid, a0, pitch, pitchf, version, protect, seg, feats=None,
                                 index=None, index_rate=0.0):
@@ -258,9 +258,7 @@ class VC:
                 coarse, pitchf = torch.stack([c for c, _ in pairs]), torch.stack([f for _, f in pairs])
             f0_done = torch.cuda.Event()
             f0_done.record(side)
-        feats = model.features_cf(xpb, 9 if version == "v1" else 12)
-        if version == "v1":
-            feats = model.final_proj.conv(feats)
+        feats = self.features_device(model, xpb, version)
         main.wait_event(f0_done)
         for t in (coarse, pitchf):
             t.record_stream(main)
@@ -589,8 +587,9 @@ class VC:
             index = self._index(file_index)
         if not pitch_guidance:
             raise NotImplementedError("no-f0 models: the reference's no-f0 Generator is not buildable (SURVEY §0)")
-        if suffix != ".pth" or embed_suffix != ".pt":
-            raise NotImplementedError("ONNX / safetensors models are not on the MI355X path")
+        if suffix != ".pth" or embed_suffix not in (".pt", ".safetensors"):
+            raise NotImplementedError("ONNX models are not on the MI355X path")
+        self.embed_suffix = embed_suffix  # convert.py:390
         if pbar is not None:
             pbar.update(1)
         inp_f0 = read_f0_file(f0_file)

@@ -211,6 +211,49 @@ def make_contentvec_ckpt(seed: int = 4321) -> dict:
     return {"cfg": {"model": dict(HUBERT_CFG), "task": {"sample_rate": 16000}}, "model": contentvec_state_dict(seed)}
 
 
+# transformers' HubertConfig for the same network (HubertModelWithFinalProj, main/library/utils.py:157-165)
+HF_HUBERT_CONFIG = dict(model_type="hubert", architectures=["HubertModelWithFinalProj"], hidden_size=768,
+                        num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072, hidden_act="gelu",
+                        feat_extract_norm="group", feat_extract_activation="gelu", conv_dim=[512] * 7,
+                        conv_stride=[5, 2, 2, 2, 2, 2, 2], conv_kernel=[10, 3, 3, 3, 3, 2, 2], conv_bias=False,
+                        num_conv_pos_embeddings=128, num_conv_pos_embedding_groups=16, do_stable_layer_norm=False,
+                        layer_norm_eps=1e-5, feat_proj_layer_norm=True, classifier_proj_size=256)
+
+
+def make_hf_hubert(seed: int = 4321) -> tuple[dict, dict]:
+    """(config.json dict, state dict) of a transformers-layout ContentVec (``HubertModelWithFinalProj``, the
+    ``.safetensors`` embedder of convert.py:342-345) holding the values of ``contentvec_state_dict(seed)`` under
+    transformers' parameter names (the weight-norm pair as ``parametrizations.weight.original0 / 1``)."""
+    src = contentvec_state_dict(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    sd["masked_spec_embed"] = src["mask_emb"]
+    for i in range(len(FE_LAYERS)):
+        sd[f"feature_extractor.conv_layers.{i}.conv.weight"] = src[f"feature_extractor.conv_layers.{i}.0.weight"]
+    sd["feature_extractor.conv_layers.0.layer_norm.weight"] = src["feature_extractor.conv_layers.0.2.weight"]
+    sd["feature_extractor.conv_layers.0.layer_norm.bias"] = src["feature_extractor.conv_layers.0.2.bias"]
+    sd["feature_projection.layer_norm.weight"] = src["layer_norm.weight"]
+    sd["feature_projection.layer_norm.bias"] = src["layer_norm.bias"]
+    sd["feature_projection.projection.weight"] = src["post_extract_proj.weight"]
+    sd["feature_projection.projection.bias"] = src["post_extract_proj.bias"]
+    sd["encoder.pos_conv_embed.conv.bias"] = src["encoder.pos_conv.0.bias"]
+    sd["encoder.pos_conv_embed.conv.parametrizations.weight.original0"] = src["encoder.pos_conv.0.weight_g"]
+    sd["encoder.pos_conv_embed.conv.parametrizations.weight.original1"] = src["encoder.pos_conv.0.weight_v"]
+    sd["encoder.layer_norm.weight"] = src["encoder.layer_norm.weight"]
+    sd["encoder.layer_norm.bias"] = src["encoder.layer_norm.bias"]
+    for i in range(12):
+        a, b = f"encoder.layers.{i}.", f"encoder.layers.{i}."
+        for n in ("k_proj", "v_proj", "q_proj", "out_proj"):
+            for t in ("weight", "bias"):
+                sd[f"{b}attention.{n}.{t}"] = src[f"{a}self_attn.{n}.{t}"]
+        for hf, fs in (("layer_norm", "self_attn_layer_norm"), ("feed_forward.intermediate_dense", "fc1"),
+                       ("feed_forward.output_dense", "fc2"), ("final_layer_norm", "final_layer_norm")):
+            for t in ("weight", "bias"):
+                sd[f"{b}{hf}.{t}"] = src[f"{a}{fs}.{t}"]
+    sd["final_proj.weight"] = src["final_proj.weight"]
+    sd["final_proj.bias"] = src["final_proj.bias"]
+    return dict(HF_HUBERT_CONFIG), sd
+
+
 # ---------------------------------------------------------------- RMVPE
 def _bn(g: _Gen, sd, name, c):
     sd[name + ".weight"] = g.uniform((c,), 0.8, 1.2)

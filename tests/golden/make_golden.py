@@ -218,15 +218,49 @@ def gen_rmvpe(seconds, seed):
     print("rmvpe", tuple(mel.shape), tuple(hidden.shape), float(np.mean(f0)))
 
 
+def write_hf_embedder(seed, name="contentvec_hf_synth"):
+    """A transformers-layout ContentVec (config.json + model.safetensors, synthetic.make_hf_hubert) under
+    assets/models/embedders/<name>, loaded through the reference's own load_embedders_model(.., "transformers")
+    (main/library/utils.py:131-165: HubertModelWithFinalProj.from_pretrained)."""
+    import json
+    from safetensors.torch import save_file
+    from main.library.utils import load_embedders_model
+    cfg, sd = synthetic.make_hf_hubert(seed)
+    d = os.path.join("assets", "models", "embedders", name)
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "config.json"), "w") as f:
+        json.dump(cfg, f)
+    save_file({k: v.contiguous() for k, v in sd.items()}, os.path.join(d, "model.safetensors"))
+    hub, _, suffix = load_embedders_model(name, "transformers")
+    assert suffix == ".safetensors"
+    return hub.float().eval()
+
+
+def gen_contentvec_hf(seconds, seed):
+    """The .safetensors embedder's outputs as VC.voice_conversion takes them (convert.py:342-345):
+    model(feats)["last_hidden_state"] and final_proj of it (v1)."""
+    hub = write_hf_embedder(seed)
+    audio = synthetic.synthetic_audio(seconds, seed=seed + 5)
+    with torch.no_grad():
+        last = hub(torch.from_numpy(audio).view(1, -1))["last_hidden_state"]
+        v1 = hub.final_proj(last[0]).unsqueeze(0)
+    np.savez_compressed(os.path.join(OUT, "contentvec_hf.npz"), seed=seed, audio=audio, last_hidden_state=last.numpy(),
+                        feats_v1=v1.numpy())
+    print("contentvec_hf", tuple(last.shape), float(last.std()))
+
+
 def gen_pipeline(name, sr, version, seconds, seed, pitch, protect, f0_autotune=False, f0_autotune_strength=1,
-                 f0_lines=None, volume_envelope=1):
+                 f0_lines=None, volume_envelope=1, embed=".pt"):
     import main.inference.convert as conv
     ck = synthetic.make_synth_ckpt(sr, version, seed=seed)
     net_g = build_ref_synth(ck)
-    from main.library.architectures import fairseq
-    cpath = os.path.join("assets", "models", "embedders", "contentvec_synth.pt")
-    torch.save(synthetic.make_contentvec_ckpt(seed + 1), cpath)
-    hub = fairseq.load_model(cpath)[0][0].float().eval()
+    if embed == ".safetensors":
+        hub = write_hf_embedder(seed + 1)
+    else:
+        from main.library.architectures import fairseq
+        cpath = os.path.join("assets", "models", "embedders", "contentvec_synth.pt")
+        torch.save(synthetic.make_contentvec_ckpt(seed + 1), cpath)
+        hub = fairseq.load_model(cpath)[0][0].float().eval()
     torch.save(synthetic.rmvpe_state_dict(seed + 2), os.path.join("assets", "models", "predictors", "rmvpe.pt"))
     vc = conv.VC(sr, conv.config)
     audio = synthetic.synthetic_audio(seconds, seed=seed + 3)
@@ -241,7 +275,10 @@ def gen_pipeline(name, sr, version, seconds, seed, pitch, protect, f0_autotune=F
                           file_index="", index_rate=0.0, pitch_guidance=1, filter_radius=3,
                           volume_envelope=volume_envelope, version=version, protect=protect, hop_length=64,
                           f0_autotune=f0_autotune, f0_autotune_strength=f0_autotune_strength, suffix=".pth",
-                          embed_suffix=".pt", f0_file=f0_file, f0_onnx=False, pbar=Pbar())
+                          embed_suffix=embed, f0_file=f0_file, f0_onnx=False, pbar=Pbar())
+    # transformers' HubertEncoder draws one scalar torch.rand([]) per layer for LayerDrop even in eval mode (its
+    # value unused there): not a synthesizer draw
+    rec.draws = [(k, t) for k, t in rec.draws if not (k == "rand" and t.dim() == 0)]
     kinds = [k for k, _ in rec.draws]
     assert len(kinds) % 3 == 0 and kinds[:3] == ["randn_like", "rand", "randn_like"], kinds
     nseg = len(kinds) // 3
@@ -257,7 +294,8 @@ def gen_pipeline(name, sr, version, seconds, seed, pitch, protect, f0_autotune=F
     if volume_envelope != 1:
         opts["volume_envelope"] = volume_envelope
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), sr=sr, version=version, seed=seed, pitch=pitch,
-                        protect=protect, audio=audio, out=out, nseg=nseg, x_pad=conv.config.x_pad, **arrs, **opts)
+                        protect=protect, audio=audio, out=out, nseg=nseg, x_pad=conv.config.x_pad, embed=embed,
+                        **arrs, **opts)
     print(name, "out", out.shape, float(np.sqrt(np.mean(out ** 2))), "segments", nseg)
 
 
@@ -595,6 +633,10 @@ def gen_ref_spread(seconds=30.0, seed=201, threads=(8, 7, 6, 5, 4, 3, 2, 1)):
 
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "safetensors":
+        # transformers probes its optional packages (librosa, ...) once, at import: import it before the stub
+        # modules below exist, so that it sees the image as it is
+        from transformers import HubertModel  # noqa: F401
     setup_harness()
     torch.set_num_threads(8)
     if len(sys.argv) > 1 and sys.argv[1] == "spread":
@@ -608,6 +650,11 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "convert":
         gen_convert(seed=121)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "safetensors":
+        gen_contentvec_hf(1.0, seed=131)
+        gen_pipeline("pipeline_48k_v2_st", 48000, "v2", 2.0, seed=141, pitch=0, protect=0.33, embed=".safetensors")
+        gen_pipeline("pipeline_32k_v1_st", 32000, "v1", 1.5, seed=142, pitch=3, protect=0.5, embed=".safetensors")
         return
     if len(sys.argv) > 1 and sys.argv[1] == "edges":
         gen_edges(seed=101)

@@ -91,7 +91,45 @@ def golden_opts(g):
     return opts
 
 
-@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1", "pipeline_48k_v2_opts"])
+def test_contentvec_safetensors_matches_reference(golden):
+    """The .safetensors embedder (transformers HubertModelWithFinalProj, loaded by the reference's own
+    load_embedders_model: tests/golden/make_golden.py safetensors): last_hidden_state = every encoder layer,
+    v1 = final_proj of it (convert.py:342-345) -- the oracle on the same values under fairseq names."""
+    g = golden("contentvec_hf")
+    W = ocv.load_weights(synthetic.make_contentvec_ckpt(int(g["seed"])))
+    src = torch.from_numpy(g["audio"]).view(1, -1)
+    with torch.no_grad():
+        last = ocv.extract_features(W, src, ocv.n_layers(W))
+        v1 = ocv.final_proj(W, last)
+    assert ocv.n_layers(W) == 12
+    assert rms(last, g["last_hidden_state"]) < 1e-4
+    assert rms(v1, g["feats_v1"]) < 1e-4
+
+
+def test_hf_names_map_to_fairseq():
+    """ContentVecAMD.from_transformers' name map: every transformers parameter lands on the fairseq name holding
+    the same values (make_hf_hubert is what transformers loaded without a missing or unexpected key), and an
+    unknown parameter raises."""
+    from rvc_amd import contentvec
+    cfg, sd = synthetic.make_hf_hubert(7)
+    fs = contentvec.hf_to_fairseq(sd)
+    src = synthetic.contentvec_state_dict(7)
+    assert set(fs) == set(src) - {"label_embs_concat"}
+    for k, v in fs.items():
+        assert torch.equal(v, src[k]), k
+    # the older weight_g / weight_v spelling of the pos_conv weight norm, and a "hubert." prefix
+    old = {("hubert." + k).replace("parametrizations.weight.original0", "weight_g")
+           .replace("parametrizations.weight.original1", "weight_v"): v for k, v in sd.items()}
+    assert set(contentvec.hf_to_fairseq(old)) == set(fs)
+    with pytest.raises(ValueError):
+        contentvec.hf_to_fairseq({**sd, "encoder.layers.0.attention.rel_bias": torch.zeros(1)})
+    assert contentvec.hf_config_to_fairseq(cfg)["encoder_embed_dim"] == 768
+    with pytest.raises(NotImplementedError):
+        contentvec.hf_config_to_fairseq({**cfg, "do_stable_layer_norm": True})
+
+
+@pytest.mark.parametrize("name", ["pipeline_48k_v2", "pipeline_32k_v1", "pipeline_48k_v2_opts",
+                                  "pipeline_48k_v2_st", "pipeline_32k_v1_st"])
 def test_pipeline_matches_reference(golden, name):
     g = golden(name)
     sr, version, seed = int(g["sr"]), str(g["version"]), int(g["seed"])
@@ -107,7 +145,8 @@ def test_pipeline_matches_reference(golden, name):
         return a
 
     out = opl.pipeline(Wc, Ws, Wr, mb, ck["config"], 0, g["audio"].astype(np.float32), float(g["pitch"]), version,
-                       float(g["protect"]), noise, **golden_opts(g))
+                       float(g["protect"]), noise, embed_suffix=str(g["embed"]) if "embed" in g else ".pt",
+                       **golden_opts(g))
     assert out.shape == g["out"].shape
     assert rms(out, g["out"]) < 1e-5
 

@@ -34,17 +34,21 @@ def _worker(rank, world, port, lengths, q):
         mine = shard_utterances(lengths, world)[rank]
         # each "utterance" output is a deterministic ramp identifying it
         outs = [torch.arange(lengths[i], dtype=torch.float32) + 1000 * i for i in mine]
-        got = gather_waveforms(outs, dist, dst=0)
+        st = {}
+        got = gather_waveforms(outs, dist, dst=0, stats=st)
+        sent = torch.tensor([st["bytes_sent"], st["bytes_recv"]], dtype=torch.int64)
+        dist.all_reduce(sent)
         if rank == 0:
-            q.put([[(int(p[0]) // 1000 if p.numel() else -1, p.numel(), float(p.sum())) for p in parts]
-                   for parts in got])
+            q.put(([[(int(p[0]) // 1000 if p.numel() else -1, p.numel(), float(p.sum())) for p in parts]
+                    for parts in got], sent.tolist()))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
-def test_gather_waveforms_world2_gloo():
-    lengths = [300, 120, 250, 7, 199]
+@pytest.mark.parametrize("lengths", [[300, 120, 250, 7, 199], [5000, 3, 2, 1], [64]])
+def test_gather_waveforms_world2_gloo(lengths):
+    """Uneven shards (and a rank with nothing): exactly the non-root ranks' samples travel, no padding."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -52,11 +56,13 @@ def test_gather_waveforms_world2_gloo():
     procs = [ctx.Process(target=_worker, args=(r, world, port, lengths, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=100)
+    res, moved = q.get(timeout=100)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     shards = shard_utterances(lengths, world)
+    # bytes sent (all ranks) == bytes received at rank 0 == 4 x the samples of rank 1's utterances
+    assert moved == [4 * sum(lengths[i] for i in shards[1])] * 2
     for r in range(world):
         assert len(res[r]) == len(shards[r])
         for (uid, n, s), i in zip(res[r], shards[r]):
