@@ -212,17 +212,43 @@ def park_gpu(seconds):
 _SLEEP_RATE = None
 
 
+def kernel_source_hash():
+    """sha256 over the library's sources (rvc-maker_amd/csrc/*.hip|cpp|h, include/*.h): the tree a PMC summary was
+    measured on (scripts/pmc_traffic.py stamps it)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(REPO, "rvc-maker_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(REPO, "rvc-maker_amd", "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(REPO, "rvc-maker_amd", "csrc", "*.h")) +
+                   glob.glob(os.path.join(REPO, "include", "*.h")))
+    for fn in files:
+        h.update(os.path.relpath(fn, REPO).encode())
+        with open(fn, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(kernel_family="x6"):
-    """Per-launch HBM bytes of a conv family from the committed PMC summary of this same bench step
-    (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled
-    per MI355X_MICROARCH.md), or None when absent."""
-    for name in ("r3_pmc_traffic.json", "r2_pmc_traffic.json"):  # the newest committed summary
+    """Per-launch HBM bytes of a conv family from the newest committed PMC summary of this same bench step
+    (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, FETCH_SIZE doubled per
+    MI355X_MICROARCH.md) -- only when it was measured on these kernel sources (its "source_hash" equals
+    kernel_source_hash()); otherwise (None, reason)."""
+    import glob
+    names = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")), reverse=True)
+    for fn in names:
         try:
-            with open(os.path.join(REPO, "profiles", name)) as f:
-                return json.load(f)[kernel_family]["traffic_bytes_per_launch"], name
+            with open(fn) as f:
+                d = json.load(f)
+            val = d[kernel_family]["traffic_bytes_per_launch"]
         except (OSError, KeyError, ValueError):
             continue
-    return None, None
+        src = d.get("source_hash")
+        if src != kernel_source_hash():
+            return None, f"{os.path.basename(fn)} was measured on kernel sources {src}, not this tree's " \
+                         f"{kernel_source_hash()}: traffic not re-measured"
+        return val, os.path.basename(fn)
+    return None, "no PMC summary committed"
 
 
 def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
@@ -255,9 +281,26 @@ def cpu_calibration():
         return None
 
 
+def cpu_threads():
+    """The torch thread count the committed host scan (scripts/cpu_threads.py -> profiles/*cpu_threads.json)
+    measured fastest on the GPU box's CPU share, or None (torch's default, OMP_NUM_THREADS)."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "*cpu_threads.json")), reverse=True):
+        try:
+            with open(fn) as f:
+                return int(json.load(f)["best_threads"]), os.path.basename(fn)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
+
+
 def cpu_baseline(seconds=30.0):
     """The torch-CPU oracle (a restatement of the reference's CPU path) on the config's own clip length
-    (30 s, ~15-20 s of CPU work on the GPU box's host threads)."""
+    (30 s, ~15-20 s of CPU work on the GPU box's host threads), at the thread count the committed scan found
+    fastest (cpu_threads)."""
+    best, scan = cpu_threads()
+    if best:
+        torch.set_num_threads(best)
     from oracle import contentvec as ocv
     from oracle import pipeline as opl
     from oracle import rmvpe as orm
@@ -278,9 +321,10 @@ def cpu_baseline(seconds=30.0):
     return {"value": round(len(out) / 48000 / dt, 4), "unit": "audio-s/s", "cores": torch.get_num_threads(),
             "host_cpus": os.cpu_count(), "kind": "port",
             "sample": f"{seconds:g} s clip, 48k v2, RMVPE, fp32, torch-CPU oracle (oracle/), wall {dt:.2f} s, "
-                      f"{torch.get_num_threads()} torch threads (OMP_NUM_THREADS="
-                      f"{os.environ.get('OMP_NUM_THREADS', 'unset')}: the host's CPU share for this GPU; "
-                      f"os.cpu_count() = {os.cpu_count()} counts every GPU's share)",
+                      f"{torch.get_num_threads()} torch threads ("
+                      + (f"the fastest of the host scan profiles/{scan}; " if best else "")
+                      + f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}: the host's CPU share for "
+                      f"this GPU; os.cpu_count() = {os.cpu_count()} counts every GPU's share)",
             "oracle_over_reference_time": cal.get("oracle_over_reference_time") if cal else None,
             "calibration": (f"oracle / reference wall time on one {cal['seconds']:g} s clip in the build container "
                             f"({cal['threads']} threads): {cal['oracle_s']:.2f} s / {cal['reference_s']:.2f} s "
@@ -512,7 +556,8 @@ def main():
                 # HBM bytes per launch of the family from PMC (default 48k / rmvpe / fp32 step only), beside the
                 # algorithmic bytes per launch measured here
                 "traffic": traffic,
-                "traffic_unit": f"bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/{tsrc})",
+                "traffic_unit": (f"bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/{tsrc})" if traffic
+                                 else f"null: {tsrc}"),
                 "algorithmic_bytes_per_launch": round(alg_bytes),
                 "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
                 "kernel": "conv_x6_kernel<*> + resblock_x6_kernel<*> (implicit-GEMM convs / fused ResBlock conv "

@@ -801,16 +801,21 @@ void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
 }
 
+// The tiles compiled with split accumulators (RVC_ARITH_FP32_SA): <= 64 rows on 4 / 8 waves and 128 x 128 on 8
+// -- the ones plan() gives RMVPE's convs under the default engine switches.  A request on any other tile (e.g.
+// RVC_X6_W8=0) is refused by plan() rather than run without the split accumulators.
+constexpr bool x6_sa_tile(int FM, int FN, int WM, int WN) {
+    return (WM * WN == 8 && FN == 4) || (WM * WN == 4 && FM <= 2 && FN == 2) || (WM == 2 && WN == 4);
+}
+
 template <int FM, int FN, int WM, int WN>
 hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     if (p.wx_passes == RVC_ARITH_F16X3) launch_x6_np<FM, FN, WM, WN, 3, true>(p, grid, lds, s);
     else if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
     else if (p.wx_passes == 3) launch_x6_np<FM, FN, WM, WN, 3>(p, grid, lds, s);
     else if (p.wx_passes == RVC_ARITH_FP32_SA) {
-        // split accumulators: only the tiles RMVPE's convs take (<= 64 rows on 4 / 8 waves, 128 x 128 on 8)
-        if constexpr ((WM * WN == 8 && FN == 4) || (WM * WN == 4 && FM <= 2 && FN == 2) || (WM == 2 && WN == 4))
-            launch_x6_np<FM, FN, WM, WN, 6, false, true>(p, grid, lds, s);
-        else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);
+        // split accumulators: only the tiles RMVPE's convs take (x6_sa_tile; plan() refuses any other)
+        if constexpr (x6_sa_tile(FM, FN, WM, WN)) launch_x6_np<FM, FN, WM, WN, 6, false, true>(p, grid, lds, s);
     }
     else launch_x6_np<FM, FN, WM, WN, 6>(p, grid, lds, s);
     return hipGetLastError();
@@ -928,6 +933,9 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         else if (Cog > 32) cfg = {2, 4, 2, 2, true};   // 64 x 128
         else if (Cog > 16) cfg = {2, 2, 1, 4, true};   // 32 x 128
         else cfg = {1, 2, 1, 4, true};                 // 16 x 128
+        RVC_CHECK_ARG(a->wx_passes != RVC_ARITH_FP32_SA || x6_sa_tile(cfg.FM, cfg.FN, cfg.WM, cfg.WN),
+                      "conv1d: RVC_ARITH_FP32_SA has no split-accumulator kernel for the %dx%d tile on %d waves "
+                      "(engine switches changed?)", 16 * cfg.FM * cfg.WM, 16 * cfg.FN * cfg.WN, cfg.WM * cfg.WN);
         const int BM = 16 * cfg.FM * cfg.WM, BN = 16 * cfg.FN * cfg.WN;
         p.span = (BN - 1) * a->stride + max_tap_off(a) + 1;
         p.span_s = p.span;
@@ -941,7 +949,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
         split_k(p, tiles, p.wx_nch);
         lds = (size_t)2 * (p.wx_passes == 6 || p.wx_passes == RVC_ARITH_FP32_SA ? 3 : (p.wx_passes == 1 ? 1 : 2)) *
-              p.span * 64 + 16;  // + F16 tile max / split-K flag
+              p.span * 64 + 16;  // + the split-fp16 tile |max|
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         return RVC_OK;

@@ -239,8 +239,7 @@ def _workspace(device, nbytes, kind="conv"):
     if buf is None or buf.numel() * 4 < nbytes:
         if buf is not None and _WS_PRIVATE is not None:
             pool.setdefault("_retired", []).append(buf)  # a captured node may still point at it
-        # zeroed: the conv engine keeps its split-K arrival counters at the head and expects them zero
-        buf = torch.zeros((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
+        buf = torch.empty((nbytes + 3) // 4 + (1 << 20), dtype=torch.float32, device=device)
         pool[key] = buf
     return buf
 

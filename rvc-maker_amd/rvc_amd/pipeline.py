@@ -8,10 +8,11 @@ reference signature and returns float32 numpy audio at tgt_sr.  ``model`` is a
 (``self.rmvpe``, loaded once from ``assets/models/predictors/rmvpe.pt`` or injected).
 
 Everything runs on the device in the order of convert.py:388-458 -- the f64 filtfilt and
-reflect padding included (filtfilt.hip); only the quiet-point search for inputs > x_max stays
-on the host (it needs the filtered signal there, as the reference).  The segment loop keeps all
-tensors in HBM; ``pipeline_device`` is the HBM-resident form the bench times, ``pipeline`` adds
-the host copies of the reference signature.
+reflect padding included (filtfilt.hip), and the quiet-point search for inputs > x_max (pipeline.hip;
+only its result, the segment plan, is read back to the host, which issues the segments).  The segment
+loop keeps all tensors in HBM; ``pipeline_device`` is the HBM-resident form the bench times,
+``pipeline`` adds the host copies of the reference signature.  ``VC.close()`` (or ``with VC(...)``)
+releases the streams the library created for it.
 
 FAISS retrieval (``file_index`` + ``index_rate``) runs on the device (retrieval.py / ivf.hip); the
 index file is read without faiss (faiss_index.py) and kept resident per path.
@@ -26,6 +27,7 @@ this path (raise): other f0 methods, ONNX models, no-f0 models.
 from __future__ import annotations
 
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -35,6 +37,33 @@ from . import contentvec as cvm
 from . import ops
 
 BH, AH = signal.butter(N=5, Wn=48, btype="high", fs=16000)  # convert.py:30
+
+
+class _CuMaskedStream:
+    """One stream restricted to part of the chip (rvc_stream_create_cu_mask), owned by a VC: ``close`` waits for
+    its work and destroys it (rvc_stream_destroy).  Left to process teardown, such a stream crashed rocprofv3's
+    kernel-trace finalisation."""
+
+    def __init__(self, device, words):
+        import ctypes
+        out = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            ops.check(ops._lib.load().rvc_stream_create_cu_mask(words, len(words), ctypes.byref(out)),
+                      "stream_create_cu_mask")
+        self.device, self.handle = device, out.value
+        self.stream = torch.cuda.ExternalStream(out.value, device=device)
+
+    def close(self):
+        if self.handle:
+            torch.cuda.synchronize(self.device)
+            h, self.handle = self.handle, None
+            ops.check(ops._lib.load().rvc_stream_destroy(h), "stream_destroy")
+
+
+def _close_streams(owned):
+    """VC's finalizer (weakref.finalize: on close(), when the VC is collected, or at interpreter exit)."""
+    while owned:
+        owned.pop().close()
 
 
 class Config:
@@ -66,6 +95,9 @@ class VC:
         self.device = config.device
         self.is_half = config.is_half
         self.rmvpe = rmvpe
+        # library-created streams (CU-masked) this VC owns: destroyed by close() / at exit, after their work
+        self._owned = []
+        self._finalizer = weakref.finalize(self, _close_streams, self._owned)
         self.embed_suffix = None  # pipeline()'s embed_suffix (convert.py:390); None = the model's own
         self.crepe = dict(crepe or {})  # capacity -> CrepeAMD (loaded on first use otherwise)
         self.noise_fn = None  # parity hook: noise_fn(seg, "z"|"sine", shape) -> device tensor
@@ -441,9 +473,27 @@ class VC:
         if getattr(self, "_streams", None) is None:
             self._streams = {}
         if key not in self._streams:
-            self._streams[key] = (self._masked_stream(device, mask) if mask != "none" else
-                                  torch.cuda.Stream(device=device, priority=prio))
+            if mask != "none":
+                owner = _CuMaskedStream(device, self._cu_mask_words(device, mask))
+                self._owned.append(owner)
+                self._streams[key] = owner.stream
+            else:
+                self._streams[key] = torch.cuda.Stream(device=device, priority=prio)
         return self._streams[key]
+
+    def close(self):
+        """Wait for and destroy the streams the library created for this VC (also done when the VC is collected
+        and at interpreter exit); the VC creates new ones if used again."""
+        self._finalizer()
+        self._streams = {}
+        self._owned = []
+        self._finalizer = weakref.finalize(self, _close_streams, self._owned)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     # The synthesizer (back) stream leaves 32 CUs -- every CU whose mask index is 7 mod 8, i.e. 4 on each XCD --
     # to the front end (RVC_BACK_CU_MASK: "mod:m:r", "top:n" or "none").  Without it RMVPE's BiGRU, whose 32
@@ -457,9 +507,9 @@ class VC:
     BACK_CU_MASK = os.environ.get("RVC_BACK_CU_MASK", "mod:8:7")
 
     @staticmethod
-    def _masked_stream(device, spec):
-        """A stream restricted to part of the chip (BACK_CU_MASK): "top:n" leaves out the last n CUs of the
-        mask, "mod:m:r" every CU whose index is r mod m (rvc_stream_create_cu_mask)."""
+    def _cu_mask_words(device, spec):
+        """The CU mask of BACK_CU_MASK's form: "top:n" leaves out the last n CUs of the mask, "mod:m:r" every CU
+        whose index is r mod m."""
         import ctypes
         ncu = torch.cuda.get_device_properties(device).multi_processor_count
         kind, *arg = spec.split(":")
@@ -475,32 +525,7 @@ class VC:
         for i in range(ncu):
             if keep[i]:
                 words[i // 32] |= 1 << (i % 32)
-        out = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            ops.check(ops._lib.load().rvc_stream_create_cu_mask(words, len(words), ctypes.byref(out)),
-                      "stream_create_cu_mask")
-        VC._release_at_exit(device, out.value)
-        return torch.cuda.ExternalStream(out.value, device=device)
-
-    _masked = []
-
-    @staticmethod
-    def _release_at_exit(device, handle):
-        """Destroy the library-created streams when the process exits (after their work has finished): left to
-        process teardown, rocprofv3's kernel trace crashed in its finalisation."""
-        if not VC._masked:
-            import atexit
-
-            def release():
-                for dev, h in VC._masked:
-                    try:
-                        torch.cuda.synchronize(dev)
-                        ops._lib.load().rvc_stream_destroy(h)
-                    except Exception:  # noqa: BLE001 -- best effort at exit
-                        pass
-                VC._masked.clear()
-            atexit.register(release)
-        VC._masked.append((device, handle))
+        return words
 
     def _side_stream(self, device):
         # RMVPE / CREPE (the longer branch, with the BiGRU's co-resident workgroups) on a high-priority

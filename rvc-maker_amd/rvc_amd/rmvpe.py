@@ -37,7 +37,9 @@ N_MELS, N_CLASS, NFFT, HOP = 128, 360, 1024, 160
 EPS = 1e-5
 
 
-# split-K target grid of RMVPE's convs (RVC_RMVPE_SPLITK; unset = the engine's default)
+# split-K target grid of the f32 form's convs (RVC_RMVPE_SPLITK; unset = the engine's default).  A Python-only
+# diagnostic: the native rvc_rmvpe_forward does not read it, so setting it voids the native-vs-Python bit identity
+# of the f32 form (the f64 form has its own split-K policy, RVC_C64_SPLITK_TILES, read by the library for both)
 RMVPE_SPLITK = int(os.environ["RVC_RMVPE_SPLITK"]) if os.environ.get("RVC_RMVPE_SPLITK") else None
 
 

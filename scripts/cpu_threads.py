@@ -27,8 +27,9 @@ def main():
         r = bench.cpu_baseline(seconds=10.0)
         rows.append({"threads": n, "xRT": r["value"], "wall_s": round(time.perf_counter() - t0, 2)})
         print(json.dumps(rows[-1]), flush=True)
+    best = max(rows, key=lambda r: r["xRT"])["threads"]
     print(json.dumps({"os_cpu_count": os.cpu_count(), "affinity": aff, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
-                      "rows": rows}))
+                      "rows": rows, "best_threads": best}))
 
 
 if __name__ == "__main__":

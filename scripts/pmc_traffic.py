@@ -7,8 +7,12 @@ the model build (weight packing) included, so only the conv families are summari
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_source_hash  # noqa: E402
 
 root = sys.argv[1]
 fam = {"conv_x6_kernel": "x6", "resblock_x6_kernel": "x6", "conv1d_mfma_kernel": "f32"}
@@ -36,4 +40,5 @@ for key, d in out.items():
     res[key] = {"launches": n, "hbm_read_bytes_per_launch": 2 * fetch_kib * 1024,
                 "hbm_write_bytes_per_launch": write_kib * 1024,
                 "traffic_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024}
+res["source_hash"] = kernel_source_hash()  # bench.py uses the summary only on these kernel sources
 print(json.dumps(res, indent=1))
