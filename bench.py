@@ -41,6 +41,7 @@ import torch  # noqa: E402
 METRIC = "audio-seconds/sec/GPU (xRT) end-to-end VC, 48k v2; 1/2/4/8 GPU scaling"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 PEAK_MFMA16_TFLOPS = 2500.0  # bf16 / fp16 dense MFMA peak (MI355X_MICROARCH.md)
+PEAK_F64_MFMA_TFLOPS = 78.6  # MI355X f64 matrix peak (AMD spec; the f64 RMVPE's conv engine, rmvpe64.hip)
 
 
 def pass_peak(passes):
@@ -78,6 +79,7 @@ class ConvProbe:
         self.ops = ops
         self.orig = ops.conv1d
         self.orig_rb = ops.resblock_pair
+        self.orig_64 = ops.conv64
         self.rec = []
 
     def __enter__(self):
@@ -112,13 +114,27 @@ class ConvProbe:
             nbytes = 4.0 * (B * C * L * (2 + bool(accumulate)) + 2 * C * C * c1.K)  # x, y (+ y read), both weights
             self.rec.append((e0, e1, flops, 1, nbytes, self.ops.rb_passes(c1.K)))
             return out
+        def wrapped_64(x, w, Ci, Co, K, **k):
+            # the f64 RMVPE's convs (engine 2): events around the call (its split-K reduce included)
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            out = self.orig_64(x, w, Ci, Co, K, **k)
+            e1.record(s)
+            B = k.get("B") or (1 if x.dim() == 2 else x.shape[0])
+            Lout, wrap = out.shape[-1] if k.get("Lout") is None else k["Lout"], k.get("wrap", 0)
+            valid = (Lout // wrap - 2) * (wrap - 2) if wrap else Lout
+            self.rec.append((e0, e1, 2.0 * B * Co * Ci * K * valid, 2, 0.0, 64))
+            return out
         self.ops.conv1d = wrapped
         self.ops.resblock_pair = wrapped_rb
+        self.ops.conv64 = wrapped_64
         return self
 
     def __exit__(self, *exc):
         self.ops.conv1d = self.orig
         self.ops.resblock_pair = self.orig_rb
+        self.ops.conv64 = self.orig_64
 
     @staticmethod
     def _bytes(a, k, out):
@@ -528,6 +544,7 @@ def main():
             vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index, args.index_rate, args.f0)
         n, ms, flops = probe.summary(engine=1)  # dominant family: the split-operand conv engine
         n32, ms32, fl32 = probe.summary(engine=0)
+        n64, ms64, fl64 = probe.summary(engine=2)
         groups, peak = probe.by_passes()
         timing = "HIP events around each launch (bench.py ConvProbe)"
         # the same pass again under torch.profiler, whose kernel records are the device's own start / end stamps
@@ -572,7 +589,10 @@ def main():
                 "launches_per_step": n, "avg_launch_ms": round(ms / max(n, 1), 4), "timing": timing,
                 "algorithmic_gflop_per_step": round(flops / 1e9, 1), "kernel_ms_per_step": round(ms, 3),
                 "f32_engine": {"launches": n32, "kernel_ms": round(ms32, 3), "gflop": round(fl32 / 1e9, 1),
-                               "tflops": round(fl32 / max(ms32, 1e-9) / 1e9, 2), "peak": PEAK_F32_MFMA_TFLOPS}}
+                               "tflops": round(fl32 / max(ms32, 1e-9) / 1e9, 2), "peak": PEAK_F32_MFMA_TFLOPS},
+                "f64_engine": {"launches": n64, "kernel_ms": round(ms64, 3), "gflop": round(fl64 / 1e9, 1),
+                               "tflops": round(fl64 / max(ms64, 1e-9) / 1e9, 2), "peak": PEAK_F64_MFMA_TFLOPS,
+                               "note": "the f64 RMVPE's convs (rmvpe64.hip conv64_kernel, split-K reduce included)"}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()

@@ -265,7 +265,8 @@ int rvc_bigru_batched(const float* gi, int64_t gi_bs, const float* whh, const fl
  * conv64: y[b][m][t] = act(sum_{c,k} w[c*K + k][m] x[b][c][t - pad + off(k)] + bias[m]) (+ res[b][m][t]),
  *   off(k) = toff[k] (ntoff == K) or k; x positions outside [0, Lin) read 0.  w is KM [Ci*K][Co] f64.
  *   wrap > 0: 2-D mode on zero-bordered images flattened to Lout = rows x wrap -- border cells are stored as 0.
- *   y is f64, or f32 (rounded once) when y_f32.  out_act: RVC_ACT_* with out_slope (LOGCLAMP's clamp).
+ *   y is f64, or f32 (rounded once) when y_f32.  out_act: RVC_ACT_NONE / RELU / SIGMOID / LOGCLAMP (out_slope =
+ *   the clamp).
  *   Stride 1, no groups.  Replaces torch.nn.Conv2d (3x3 pad 1 / 1x1) and nn.Linear in E2E / MelSpectrogram
  *   (RMVPE.py:11-44, 78-107, 141-144, 162-181), batch b in [0, B) with strides (0 = dense). */
 typedef struct rvc_conv64_args {

@@ -406,9 +406,9 @@ constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2
 // hH and the two sums are added once at the end: the f32 accumulator of the large terms is rounded once per
 // 32 products instead of six times, the corrections' roundings are 2^-8 smaller (RMVPE, whose f0 is a
 // per-frame decision: scripts/conv_prec.py).
-// LD: the loaders' register ring of staged chunks (chunk c + 1's loads are issued while chunk c computes).  A
-// 4-deep ring (with an L2 prefetch of the K = 1 weight panels by the loaders) measured no faster on ContentVec's
-// K = 1 GEMMs and slower end to end: not kept.
+// The loaders keep one chunk in flight in registers (chunk c + 2's loads are issued while chunk c computes, after
+// chunk c + 1 was staged).  A 4-deep ring (with an L2 prefetch of the K = 1 weight panels by the loaders) measured
+// no faster on ContentVec's K = 1 GEMMs and slower end to end: not kept.
 template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
@@ -421,7 +421,6 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     constexpr int BN = 16 * FN * WN;
     extern __shared__ uint4 xs[];  // [2 buffers][span][NPL planes][4 x 16 B]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int LD = 2;  // the loaders' chunk ring
     // XCD-aware tile order (cdna_hip_programming.md T1, the bijective form): blocks are dealt round-robin over
     // the 8 XCDs, so block b serves tile t(b), which gives each XCD a contiguous run of the row-major tile
     // order -- whole rows of column tiles, which read the same weight fragments, share that XCD's L2 instead
@@ -496,8 +495,37 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
             ioff[it] = (uint32_t)(ig8[it] * 8 * lin + qc);
         }
-        float xr[LD][X6_NI][8];
-        auto xload = [&](int ch, float (&r)[X6_NI][8]) __attribute__((always_inline)) {
+        // General form: items are PAIRS of consecutive input positions (q, q + 1) with q even -- one 8-byte load per
+        // channel, half the loads of one position per item, so that the ring (NI2 x 8 loads of a chunk in flight)
+        // stays far below what vmcnt can count; with single positions the 6-item split-fp16 loaders kept 96 loads
+        // in flight and waited vmcnt(0) per chunk.  Pair it covers staged positions ppos and ppos + 1 (the first
+        // may be -1, unstaged); element j is always lane .x / .y of its load, so no per-element select -- a
+        // select between two ring registers made hipcc keep the ring in scratch.  A pair starting below 0 is
+        // wholly masked (q even), one past the end of a row reads the next row or 0 (buffer range): masked too.
+        constexpr int NI2 = (X6_NI + 1) / 2;
+        const int par = base & 1;
+        const int npair = (span + par + 1) >> 1;
+        int ppos[NI2], pg8[NI2], pq[NI2];
+        unsigned pok = 0, pstage = 0;
+#pragma unroll
+        for (int it = 0; it < NI2; ++it) {
+            const int idx = ltid + 256 * it;
+            const int g8 = idx / npair;
+            pg8[it] = g8 < 4 ? g8 : 3;
+            ppos[it] = 2 * (idx - g8 * npair) - par;
+            const int q0 = base + ppos[it];  // even
+            pq[it] = q0 < 0 ? 0 : q0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int bit = 2 * it + j, q = q0 + j, pos = ppos[it] + j;
+                const bool staged = idx < 4 * npair && pos >= 0 && pos < span;
+                pstage |= (unsigned)staged << bit;
+                pok |= (unsigned)(staged && q >= 0 && q < lin) << bit;
+            }
+        }
+        constexpr int NR = FASTL ? X6_NI : 2 * NI2;  // ring rows per chunk: items (fast form) or pair halves
+        float xr[2][NR][8];  // slot 1: the chunk in flight; slot 0: chunk 0 and the split-fp16 |max| pass
+        auto xload = [&](int ch, float (&r)[NR][8]) __attribute__((always_inline)) {
             // unconditional (clamped) loads so that the vmcnt bookkeeping is static
             if constexpr (FASTL) {
 #pragma unroll
@@ -507,26 +535,32 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                     for (int it = 0; it < X6_NI; ++it) r[it][e] = (kAblations && (p.dbg & 4)) ? 0.f : xrow[ioff[it]];
                 }
             } else {
+                // general form: position pairs, one 8-byte buffer load per channel (see the pair mapping above):
+                // a per-chunk buffer resource over the chunk's (at most 32) real channel rows -- rows past Ci read
+                // 0 by the range check, so the per-lane byte offsets are chunk-invariant (24 VGPRs, no 64-bit
+                // address per load; Lin < 2^24: x6_eligible)
+                const int c0 = __builtin_amdgcn_readfirstlane(ch * 32);
+                const int nrow = Cig - c0 < 32 ? Cig - c0 : 32;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(xb + (int64_t)c0 * lin), (short)0, nrow * lin * 4, 0x00020000);
 #pragma unroll
-                for (int it = 0; it < X6_NI; ++it) {
-                    const int q = base + ipos[it];
-                    const int qc = q < 0 ? 0 : (q >= lin ? lin - 1 : q);
+                for (int it = 0; it < NI2; ++it)
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        int c = ch * 32 + ig8[it] * 8 + e;
-                        c = c < Cig ? c : Cig - 1;
-                        r[it][e] = (kAblations && (p.dbg & 4)) ? 0.f : xb[(int64_t)c * lin + qc];
+                        const int off = ((pg8[it] * 8 + e) * lin + pq[it]) * 4;
+                        const rvc_f2 v = __builtin_bit_cast(rvc_f2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+                        r[2 * it][e] = (kAblations && (p.dbg & 4)) ? 0.f : v.x;
+                        r[2 * it + 1][e] = (kAblations && (p.dbg & 4)) ? 0.f : v.y;
                     }
-                }
             }
         };
         float sc = 1.f;  // F16: the tile's activation scale (power of 2)
-        auto xstore = [&](int ch, const float (&r)[X6_NI][8], uint4* dst) __attribute__((always_inline)) {
+        auto xstore_fast = [&](int ch, const float (&r)[NR][8], uint4* dst) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < X6_NI; ++it) {
                 if (ltid + 256 * it < 4 * span) {
                     uint32_t hw[4], mw[4], lw[4];
-                    if constexpr (FASTL && !F16) {
+                    {  // the fast form (FASTL, never split-fp16)
                         const bool ok = (iok >> it) & 1u;
 #pragma unroll
                         for (int e2 = 0; e2 < 4; ++e2) {
@@ -537,20 +571,6 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                             }
                             split3_pk(ok ? v0 : 0.f, ok ? v1 : 0.f, hw[e2], mw[e2], lw[e2]);
                         }
-                    } else
-#pragma unroll
-                    for (int e2 = 0; e2 < 4; ++e2) {
-                        float v2[2];
-#pragma unroll
-                        for (int u = 0; u < 2; ++u) {
-                            const int e = 2 * e2 + u;
-                            const bool ok = ((iok >> it) & 1u) && ch * 32 + ig8[it] * 8 + e < Cig;
-                            float v = r[it][e] * p.in_scale;
-                            if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
-                            v2[u] = ok ? (F16 ? v * sc : v) : 0.f;
-                        }
-                        if constexpr (F16) split2h_pk(v2[0], v2[1], hw[e2], mw[e2]);
-                        else split3_pk(v2[0], v2[1], hw[e2], mw[e2], lw[e2]);
                     }
                     const int pos = ipos[it];
                     dst[x_slot<NPL>(pos, 0, ig8[it])] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
@@ -559,19 +579,52 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 }
             }
         };
-        // prologue: chunk 0 -> LDS buffer 0, chunk 1 in flight
+        // general form: pair it's element j (position ppos + j) is lane .x (j = 0) / .y (j = 1) of its load
+        auto xstore_gen = [&](int ch, const float (&r)[2 * NI2][8], uint4* dst) __attribute__((always_inline)) {
+#pragma unroll
+            for (int it = 0; it < NI2; ++it)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int bit = 2 * it + j;
+                    if ((pstage >> bit) & 1u) {
+                        uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+                        for (int e2 = 0; e2 < 4; ++e2) {
+                            float v2[2];
+#pragma unroll
+                            for (int u = 0; u < 2; ++u) {
+                                const int e = 2 * e2 + u;
+                                const bool ok = ((pok >> bit) & 1u) && ch * 32 + pg8[it] * 8 + e < Cig;
+                                float v = r[2 * it + j][e] * p.in_scale;
+                                if (p.in_act == RVC_ACT_LRELU) v = v >= 0.f ? v : v * p.in_slope;
+                                v2[u] = ok ? (F16 ? v * sc : v) : 0.f;
+                            }
+                            if constexpr (F16) split2h_pk(v2[0], v2[1], hw[e2], mw[e2]);
+                            else split3_pk(v2[0], v2[1], hw[e2], mw[e2], lw[e2]);
+                        }
+                        const int pos = ppos[it] + j;
+                        dst[x_slot<NPL>(pos, 0, pg8[it])] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                        if constexpr (NPL >= 2) dst[x_slot<NPL>(pos, 1, pg8[it])] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+                        if constexpr (NPL >= 3) dst[x_slot<NPL>(pos, 2, pg8[it])] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                    }
+                }
+        };
+        auto xstore = [&](int ch, const float (&r)[NR][8], uint4* dst) __attribute__((always_inline)) {
+            if constexpr (FASTL) xstore_fast(ch, r, dst);
+            else xstore_gen(ch, r, dst);
+        };
+        // prologue: chunk 0 -> LDS buffer 0, chunk 1 in flight in ring slot 1
         if constexpr (F16) {
             // tile |max| over the raw loads (clamped addresses read real elements of x, and lrelu only
             // shrinks: an upper bound of |pre(x)| over the staged tile); chunks 0 and 1 are loaded last and kept
-            auto rmax = [&](const float (&r)[X6_NI][8]) __attribute__((always_inline)) {
+            auto rmax = [&](const float (&r)[NR][8]) __attribute__((always_inline)) {
                 float m = 0.f;
 #pragma unroll
-                for (int it = 0; it < X6_NI; ++it)
+                for (int it = 0; it < NR; ++it)
 #pragma unroll
                     for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(r[it][e]));
                 return m;
             };
-            static_assert(LD == 2, "split-fp16 keeps the 2-deep ring");
             float am = 0.f;
             for (int i = 2; i < nck; i += 2) {
                 xload(pchunk(i), xr[0]);
@@ -584,26 +637,23 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             if (lane == 0) tmax[wave - NCW] = am;
             __syncthreads();  // tile max published
             sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+            xstore(pchunk(0), xr[0], xs);
         } else {
-#pragma unroll
-            for (int d = 0; d < LD; ++d) xload(pchunk(d), xr[d]);
+            xload(pchunk(0), xr[0]);
+            xstore(pchunk(0), xr[0], xs);
+            xload(pchunk(1), xr[1]);
         }
-        xstore(pchunk(0), xr[0], xs);
         __syncthreads();
-        // iteration i (chunk ch_beg + i computing): ring slot i % LD held chunk i (staged last iteration), so it
-        // takes chunk i + LD's loads; chunk i + 1 goes from slot (i + 1) % LD to the other LDS buffer.  Unrolled
-        // by LD so that every slot index is a compile-time constant.  Every iteration issues its loads
-        // unconditionally (pchunk clamps past the last chunk), so that every path through the loop issues the
-        // same loads: with the loads under "if (i + 1 < nck)" hipcc's vmcnt bookkeeping could not follow the
-        // ring across the loop's back-edge and waited vmcnt(0) at the loop head -- on the chunk just requested.
-        // The stores and the barrier stay guarded (no loads inside).
-        for (int i = 0; i < nck; i += LD) {
-#pragma unroll
-            for (int u = 0; u < LD; ++u) {
-                xload(pchunk(i + u + LD), xr[u]);
-                if (i + u + 1 < nck) xstore(pchunk(i + u + 1), xr[(u + 1) % LD], xs + ((i + u + 1) & 1) * bufsz);
-                if (i + u < nck) __syncthreads();
-            }
+        // iteration i (chunk ch_beg + i computing): stage chunk i + 1 from ring slot 1 into the other LDS buffer
+        // (released by chunk i - 1 at the last barrier), then load chunk i + 2 into the same slot -- one chunk of
+        // registers in the steady state (the 2-slot ring of rounds 1-3 held two: ~96 VGPRs of loader state that
+        // spilled), and the wait before each staging is on loads issued a whole chunk earlier, behind a barrier.
+        // The loads are issued unconditionally (pchunk clamps past the last chunk) so that every path through the
+        // loop issues the same loads and hipcc's vmcnt bookkeeping stays static; only the stores are guarded.
+        for (int i = 0; i < nck; ++i) {
+            if (i + 1 < nck) xstore(pchunk(i + 1), xr[1], xs + ((i + 1) & 1) * bufsz);
+            xload(pchunk(i + 2), xr[1]);
+            __syncthreads();
         }
       };
         // the loader body, once per form (a wave-uniform choice made once per block)
@@ -885,9 +935,10 @@ constexpr int X6_K_MAX = 64;
 // and the operand reads of even positions are 2-way bank conflicted
 bool x6_eligible(const rvc_conv1d_args* a) {
     static const int s2 = getenv("RVC_X6_STRIDE2") ? atoi(getenv("RVC_X6_STRIDE2")) : 1;
-    return a->wx && (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
+    return a->wx && a->Lin < (1 << 24) &&
+           (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
            a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= X6_K_MAX &&
-           (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX && a->wx_nmf % 8 == 0 &&
+           (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX - 2 && a->wx_nmf % 8 == 0 &&
            (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 ||
                                                 a->wx_passes == RVC_ARITH_FP32_SA || a->wx_passes == 3 ||
                                                 a->wx_passes == 1 || a->wx_passes == RVC_ARITH_F16X3);
@@ -924,7 +975,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         // 331 -> 307; end to end 820 -> 850 xRT.  The 6-pass form loses (its weight ring drops to 1 k-step
         // to fit 64 accumulators: C=128 K=11 883 -> 1113 us).
         static const int bn256 = getenv("RVC_X6_BN256") ? atoi(getenv("RVC_X6_BN256")) : 1;
-        if (Cog > 64 && w8 && bn256 && a->stride == 1 && 255 + max_tap_off(a) + 1 <= 64 * X6_NI_MAX &&
+        if (Cog > 64 && w8 && bn256 && a->stride == 1 && 255 + max_tap_off(a) + 1 <= 64 * X6_NI_MAX - 2 &&
             (bn256 == 2 || np == RVC_ARITH_F16X3))
             cfg = {2, 8, 4, 2, true};
         else if (Cog > 64 && w8) cfg = {2, 4, 4, 2, true};  // 128 x 128 on 8 compute waves

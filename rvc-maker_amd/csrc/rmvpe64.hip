@@ -25,12 +25,10 @@ namespace {
 // v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4], B[l>>4][l&15]; C/D: col = l&15, row = (l>>4) + 4 r
 RVC_DEV doublex4 mfma64(double a, double b, doublex4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
+// the activations RMVPE's f64 network uses (plan64 refuses the others)
 RVC_DEV double act64(double v, int act, double slope) {
     switch (act) {
-        case RVC_ACT_LRELU: return v >= 0.0 ? v : v * slope;
         case RVC_ACT_RELU: return v > 0.0 ? v : 0.0;
-        case RVC_ACT_TANH: return tanh(v);
-        case RVC_ACT_GELU: return 0.5 * v * (1.0 + erf(v * 0.70710678118654752440));
         case RVC_ACT_SIGMOID: return 1.0 / (1.0 + exp(-v));
         case RVC_ACT_LOGCLAMP: return log(fmax(v, slope));
         default: return v;
@@ -96,7 +94,7 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
     constexpr int NA = KC * BM / 256;     // weight doubles staged per thread
     static_assert(WM * WN == 4 && NA >= 1 && (KC * BM) % 256 == 0, "tile");
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int xs_n = p.rows_max * p.span_s;
+    const int xs_n = p.rows_max * p.span_s + 1;  // + a dump cell
     double* Wsb = sm;                       // [2][KC][WS]
     double* Xsb = sm + 2 * KC * WS;         // [2][xs_n]
     int* koffb = (int*)(Xsb + 2 * xs_n);    // [2][KC]
@@ -168,12 +166,13 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
         double* Xs = Xsb + buf * xs_n;
 #pragma unroll
         for (int g = 0; g < NB64; g += 4) {
-            if (g * 256 < n) {
+            if (g * 256 < n) {  // block-uniform
 #pragma unroll
                 for (int i = g; i < g + 4; ++i) {
                     const int r = bslot[i] >> 16, j = bslot[i] & 0xffff;
                     const bool ok = r < rows && ((bok >> i) & 1u);
-                    if (tid + 256 * i < n) Xs[r * p.span_s + j] = ok ? rb[i] : 0.0;
+                    // slots past the tile go to the dump cell after it (no per-lane branch)
+                    Xs[tid + 256 * i < n ? r * p.span_s + j : xs_n - 1] = ok ? rb[i] : 0.0;
                 }
             }
         }
@@ -202,20 +201,30 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
         if (more) gload(ch + 1);
         const double* Ws = Wsb + cur * KC * WS + wm * 16 * FM + ln;
         const double* Xs = Xsb + cur * xs_n + wn * 16 * FN + ln;
-        const int* ko = koffb + cur * KC;
+        // the chunk's tap offsets first (one LDS read per k-step, all issued together), then the operands
+        // of k-step ks + 1 are read while k-step ks's MFMAs run (register double buffer)
+        int ko[KC / 4];
+#pragma unroll
+        for (int ks = 0; ks < KC / 4; ++ks) ko[ks] = koffb[cur * KC + ks * 4 + lk];
+        double a[2][FM], bv[2][FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[0][i] = Ws[lk * WS + i * 16];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bv[0][j] = Xs[ko[0] + j * 16];
 #pragma unroll
         for (int ks = 0; ks < KC / 4; ++ks) {
-            const int kk = ks * 4 + lk;
-            double a[FM], bv[FN];
+            const int q = ks & 1;
+            if (ks + 1 < KC / 4) {
+                const int kk = (ks + 1) * 4 + lk;
 #pragma unroll
-            for (int i = 0; i < FM; ++i) a[i] = Ws[kk * WS + i * 16];
-            const double* xr = Xs + ko[kk];
+                for (int i = 0; i < FM; ++i) a[q ^ 1][i] = Ws[kk * WS + i * 16];
 #pragma unroll
-            for (int j = 0; j < FN; ++j) bv[j] = xr[j * 16];
+                for (int j = 0; j < FN; ++j) bv[q ^ 1][j] = Xs[ko[ks + 1] + j * 16];
+            }
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < FN; ++j) acc[i][j] = mfma64(a[i], bv[j], acc[i][j]);
+                for (int j = 0; j < FN; ++j) acc[i][j] = mfma64(a[q][i], bv[q][j], acc[i][j]);
         }
         if (more) sstore(ch + 1, cur ^ 1);
         __syncthreads();
@@ -274,6 +283,9 @@ int plan64(const rvc_conv64_args* a, C64& p, Cfg64& cfg, dim3& grid, size_t& lds
                       a->pad >= 0 && a->Ci * a->K < (1ll << 30),
                   "conv64: per-batch tensor exceeds 2^31 elements (use the batch dimension)");
     RVC_CHECK_ARG(a->ntoff == 0 || (a->ntoff == a->K && a->K <= 16), "conv64: toff needs ntoff == K <= 16");
+    RVC_CHECK_ARG(a->out_act == RVC_ACT_NONE || a->out_act == RVC_ACT_RELU || a->out_act == RVC_ACT_SIGMOID ||
+                      a->out_act == RVC_ACT_LOGCLAMP,
+                  "conv64: out_act %d (NONE, RELU, SIGMOID, LOGCLAMP)", a->out_act);
     RVC_CHECK_ARG(a->wrap == 0 || (a->wrap >= 3 && a->Lout % a->wrap == 0), "conv64: Lout must be rows x wrap");
     int maxoff = a->ntoff ? 0 : a->K - 1;
     for (int i = 0; i < a->ntoff; ++i) {
@@ -327,7 +339,7 @@ int plan64(const rvc_conv64_args* a, C64& p, Cfg64& cfg, dim3& grid, size_t& lds
     p.cps = (nch + ks - 1) / ks;
     p.ksplit = (nch + p.cps - 1) / p.cps;
     const int WS = BM + 4;
-    lds = (size_t)(2 * KC * WS + 2 * rows_max * p.span_s) * 8 + 2 * KC * 4;
+    lds = (size_t)(2 * KC * WS + 2 * (rows_max * p.span_s + 1)) * 8 + 2 * KC * 4;
     RVC_CHECK_ARG(lds <= 160 * 1024, "conv64: LDS %zu too large", lds);
     grid = dim3(cdiv(a->Lout, BN), (unsigned)mt, (unsigned)(a->B * p.ksplit));
     RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv64: grid too large");
@@ -399,11 +411,46 @@ __global__ void img_to_seq64_kernel(const double* img, double* x, int C, int64_t
 
 // ---------------------------------------------------------------- f64 bidirectional GRU recurrence
 // rmvpe.hip's bigru_kernel in f64: 16 workgroups per direction, 16 hidden units each, W_hh rows in registers
-// (48 doubles per thread); h is exchanged every step as two 8-byte {tag, 32-bit half} granules per unit
-// (lo, hi), double-buffered by step parity; a reader takes a unit's value once both halves carry the step's
-// tag.  Every spin is bounded; a timeout sets *err and the kernel drains.
+// (48 doubles per thread); h is exchanged every step as one 16-byte granule per unit {tag | lo, tag | hi}
+// (each 8-byte half carries the step tag, so a read that straddles two steps is seen and retried), written and
+// polled with one agent-coherent (sc1) dwordx4 access -- what the 8-byte atomics compile to, 16 bytes wide --
+// double-buffered by step parity.  Every spin is bounded; a timeout sets *err and the kernel drains.
+//
+// The gate math is the step's critical path (scripts/bigru64_bench.hip: 1.45 of 3.3 us per step with ocml's f64
+// exp / division / tanh), so: sigmoid(a) = 1 / (1 + e^-a) and tanh(a) = 1 - 2 / (1 + e^2a) on one short f64 exp
+// (exp64: Cody-Waite reduction, degree-12 Taylor, ~1 ulp) and a Newton-refined reciprocal, and r and z are
+// evaluated at once on two lanes of the unit's 16-lane group (lane 0: r, lane 1: z), n after r on lane 0.
 constexpr int G_H = 256;
 constexpr int G_WG = 16;
+
+RVC_DEV double exp64(double x) {
+    x = fmin(fmax(x, -700.0), 700.0);
+    const double k = rint(x * 1.4426950408889634);
+    double r = fma(-k, 6.93147180369123816490e-01, x);
+    r = fma(-k, 1.90821492927058770002e-10, r);  // |r| <= 0.347
+    double p = 2.08767569878680989792e-09;        // 1/12!
+    p = fma(p, r, 2.50521083854417187751e-08);   // 1/11!
+    p = fma(p, r, 2.75573192239858906526e-07);
+    p = fma(p, r, 2.75573192239858906526e-06);
+    p = fma(p, r, 2.48015873015873015873e-05);
+    p = fma(p, r, 1.98412698412698412698e-04);
+    p = fma(p, r, 1.38888888888888888889e-03);
+    p = fma(p, r, 8.33333333333333333333e-03);
+    p = fma(p, r, 4.16666666666666666667e-02);
+    p = fma(p, r, 1.66666666666666666667e-01);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
+RVC_DEV double rcp64(double d) {  // 1 / d for d >= 1: hardware estimate + 2 Newton steps
+    double y = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-d, y, 1.0);
+    return fma(y, e, y);
+}
 
 __global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const double* whh, const double* bhh,
                                                       double* y, unsigned long long* gran, int* err, int64_t T,
@@ -427,37 +474,31 @@ __global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const do
         wz[i] = W[(int64_t)(G_H + u) * G_H + 16 * s + i];
         wn[i] = W[(int64_t)(2 * G_H + u) * G_H + 16 * s + i];
     }
-    const double bhr = bhh[d * 3 * G_H + u], bhz = bhh[d * 3 * G_H + G_H + u], bhn = bhh[d * 3 * G_H + 2 * G_H + u];
+    // lane 0 of the group: r's input projection and bias (and n's); lane 1: z's
+    const int gsel = s == 1 ? 1 : 0;
+    const double bhg = bhh[d * 3 * G_H + gsel * G_H + u], bhn = bhh[d * 3 * G_H + 2 * G_H + u];
     const double* G = gi + (int64_t)d * 3 * G_H * T;
     unsigned long long* GR = gran + (int64_t)d * 2 * G_H * 2;  // [parity][unit][lo, hi]
     double hprev = 0.0;
-    double gxr = 0.0, gxz = 0.0, gxn = 0.0;
-    if (s == 0) {
+    double gxg = 0.0, gxn = 0.0;  // the current step's input projections (lane 0: r and n, lane 1: z)
+    if (s < 2) {
         const int64_t tau0 = d ? T - 1 : 0;
-        gxr = G[(int64_t)u * T + tau0];
-        gxz = G[(int64_t)(G_H + u) * T + tau0];
+        gxg = G[(int64_t)(gsel * G_H + u) * T + tau0];
         gxn = G[(int64_t)(2 * G_H + u) * T + tau0];
     }
     hs[0][tid] = 0.0;
     __syncthreads();
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     for (int64_t t = 0; t < T; ++t) {
         const int64_t tau = d ? T - 1 - t : t;
         const int cur = (int)(t & 1);
         if (t > 0) {
-            unsigned long long* g = GR + ((t - 1) & 1) * G_H * 2 + 2 * tid;
-            unsigned long long v0 = 0, v1 = 0;
-            bool ok0 = false, ok1 = false;
+            const unsigned long long* g = GR + ((t - 1) & 1) * G_H * 2 + 2 * tid;
+            u64x2 v;
             unsigned spins = 0;
             for (;;) {
-                if (!ok0) {
-                    v0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok0 = (uint32_t)(v0 >> 32) == (uint32_t)t;
-                }
-                if (!ok1) {
-                    v1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok1 = (uint32_t)(v1 >> 32) == (uint32_t)t;
-                }
-                if (ok0 && ok1) break;
+                asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(g) : "memory");
+                if ((uint32_t)(v.x >> 32) == (uint32_t)t && (uint32_t)(v.y >> 32) == (uint32_t)t) break;
                 if (++spins > spin_limit) {
                     atomicExch(err, 1);
                     abort_flag = 1;
@@ -465,15 +506,14 @@ __global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const do
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            hs[cur][tid] = __hiloint2double((int)(uint32_t)v1, (int)(uint32_t)v0);
+            hs[cur][tid] = __hiloint2double((int)(uint32_t)v.y, (int)(uint32_t)v.x);
             __syncthreads();
             if (abort_flag) break;
         }
-        double nxr = 0.0, nxz = 0.0, nxn = 0.0;
-        if (s == 0 && t + 1 < T) {
+        double nxg = 0.0, nxn = 0.0;
+        if (s < 2 && t + 1 < T) {
             const int64_t tn = d ? T - 2 - t : t + 1;
-            nxr = G[(int64_t)u * T + tn];
-            nxz = G[(int64_t)(G_H + u) * T + tn];
+            nxg = G[(int64_t)(gsel * G_H + u) * T + tn];
             nxn = G[(int64_t)(2 * G_H + u) * T + tn];
         }
         double pr = 0.0, pz = 0.0, pn = 0.0;
@@ -490,20 +530,22 @@ __global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const do
             pz += __shfl_xor(pz, o, 64);
             pn += __shfl_xor(pn, o, 64);
         }
+        // lanes 0 / 1 of the group: r / z = sigmoid(gx + (W_h h + b_h)) in one evaluation
+        const double sg = rcp64(1.0 + exp64(-(gxg + ((gsel ? pz : pr) + bhg))));
+        const double zz = __shfl_down(sg, 1, 64);  // lane 0 <- lane 1's z
         if (s == 0) {
-            const double r = 1.0 / (1.0 + exp(-(gxr + (pr + bhr))));
-            const double z = 1.0 / (1.0 + exp(-(gxz + (pz + bhz))));
-            const double n = tanh(gxn + r * (pn + bhn));
-            const double h = (hprev - n) * z + n;
+            const double n = 1.0 - 2.0 * rcp64(1.0 + exp64(2.0 * (gxn + sg * (pn + bhn))));
+            const double h = (hprev - n) * zz + n;
             hprev = h;
             const unsigned long long tag = (unsigned long long)(uint32_t)(t + 1) << 32;
             unsigned long long* o = GR + (t & 1) * G_H * 2 + 2 * u;
-            __hip_atomic_store(o, tag | (uint32_t)__double2loint(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 1, tag | (uint32_t)__double2hiint(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u64x2 gv;
+            gv.x = tag | (uint32_t)__double2loint(h);
+            gv.y = tag | (uint32_t)__double2hiint(h);
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(o), "v"(gv) : "memory");
             y[(int64_t)(d * G_H + u) * T + tau] = h;
         }
-        gxr = nxr;
-        gxz = nxz;
+        gxg = nxg;
         gxn = nxn;
     }
 }

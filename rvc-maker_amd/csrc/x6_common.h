@@ -54,6 +54,7 @@ RVC_DEV void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
 // conversion), the residuals come from the packed halves; h / m / l are the pairs' packed words (element 0 in the
 // low half), bit for bit what two split3 calls packed give.
 typedef float rvc_f2 __attribute__((ext_vector_type(2)));
+typedef float rvc_f2u __attribute__((ext_vector_type(2), aligned(4)));  // a float pair at any float offset
 typedef __bf16 rvc_bf2 __attribute__((ext_vector_type(2)));
 RVC_DEV uint32_t pk_bf16(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((rvc_f2){a, b}, rvc_bf2));

@@ -495,15 +495,15 @@ class VC:
     def __exit__(self, *exc):
         self.close()
 
-    # The synthesizer (back) stream leaves 32 CUs -- every CU whose mask index is 7 mod 8, i.e. 4 on each XCD --
-    # to the front end (RVC_BACK_CU_MASK: "mod:m:r", "top:n" or "none").  Without it RMVPE's BiGRU, whose 32
-    # workgroups must all be resident to advance (blocks are dealt round-robin over the XCDs: 4 per XCD), waits
-    # for CUs the generator's kernels hold, partly resident and spinning: the clip stream ran 890-1000 xRT from
-    # run to run on one box.  Measured (one box each, 2 runs per setting, interleaved): 4 CUs per XCD left free
-    # 986-990 against 899-1003 unmasked; 8 per XCD 986-989; 2 per XCD 765-768 and 1 per XCD 660 (too few
-    # for the recurrence's workgroups); 32 contiguous mask bits (one XCD's worth) 798-801.  The masked stream is
-    # its own pooled stream, apart from the per-call side stream (sharing it put the per-call RMVPE on 224 CUs
-    # at default priority: 805 -> 650 xRT per call).
+    # The synthesizer (back) stream is created through hipExtStreamCreateWithCUMask (RVC_BACK_CU_MASK:
+    # "mod:m:r", "top:n" or "none").  What a mask does was probed in round 4 (scripts/cu_mask_probe.hip,
+    # profiles/r4_cu_mask_probe.txt): mask bit i lands on XCD i mod 8, so "mod:8:7" names all 32 CUs of one XCD,
+    # and the runtime then applies no mask at all -- its launches still run on all 256 CUs; "top:32" does
+    # leave 4 CUs on each XCD (28 of 32 used per XCD).  The default "mod:8:7" is therefore an unmasked stream of
+    # default priority on a hardware queue of its own; that is what the round-3 numbers measured (986-990 xRT
+    # against 899-1003 for the high-priority back stream, "none"), while the real 4-CU-per-XCD mask ("top:32")
+    # ran 798-801.  The stream is its own
+    # pooled stream, apart from the per-call side stream (sharing it: 805 -> 650 xRT per call).
     BACK_CU_MASK = os.environ.get("RVC_BACK_CU_MASK", "mod:8:7")
 
     @staticmethod

@@ -246,6 +246,7 @@ class RMVPEAMD:
         to Tp = F rounded up to 32, input BatchNorm applied), Tp."""
         F = mel.shape[-1]
         Tp = 32 * ((F - 1) // 32 + 1)
+        mel = mel.to(self.dt).contiguous()  # a caller's f32 mel (the reference's mel2hidden input) in the f64 form
         x = torch.zeros(1, Tp + 2, N_MELS + 2, device=mel.device, dtype=self.dt)
         (ops.mel_image64 if self.f64 else ops.mel_image)(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
         return x, Tp
@@ -365,6 +366,7 @@ class RMVPEAMD:
         dev = mel.device
         B, _, F = mel.shape
         Tp = 32 * ((F - 1) // 32 + 1)
+        mel = mel.to(self.dt).contiguous()
         x = torch.zeros(B, 1, Tp + 2, N_MELS + 2, device=dev, dtype=self.dt)
         if self.f64:
             ops.mel_image64(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)

@@ -245,24 +245,31 @@ def test_filtfilt_golden(ops, golden):
     np.testing.assert_allclose(out64.cpu().numpy(), g["y"], rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("f64", [False, True])
 @pytest.mark.parametrize("Ci,Co,H,W", [(32, 32, 40, 24), (256, 256, 12, 8), (16, 16, 30, 20)])
-def test_conv2d_bordered_image_writes_zero_border(ops, engine, Ci, Co, H, W):
-    """RMVPE's 3x3 conv on a zero-bordered [C][H+2][W+2] image (1-D engine, 9 tap offsets): the
-    interior matches F.conv2d(pad 1) and the border is written as exactly 0, so the output buffer needs
-    no zero-fill (the 256-channel case runs split-K, whose reduce stores the border)."""
+def test_conv2d_bordered_image_writes_zero_border(ops, engine, Ci, Co, H, W, f64):
+    """RMVPE's 3x3 conv on a zero-bordered [C][H+2][W+2] image (1-D engine, 9 tap offsets; the f32 engines and
+    the f64 one of the f64 RMVPE): the interior matches F.conv2d(pad 1) and the border is written as exactly 0,
+    so the output buffer needs no zero-fill (the 256-channel case runs split-K, whose reduce stores the border)."""
     from rvc_amd.rmvpe import _Conv2d
+    if f64 and engine != "x6":
+        pytest.skip("one engine for f64")
     g = gen(11)
-    w = torch.randn(Co, Ci, 3, 3, generator=g) / math.sqrt(9 * Ci)
-    b = torch.randn(Co, generator=g) * 0.1
-    x = torch.randn(Ci, H, W, generator=g)
-    xb = F.pad(x, (1, 1, 1, 1))
-    conv = _Conv2d(w, b, DEV)
-    out = torch.full((Co, H + 2, W + 2), float("nan"), device=DEV)
+    w = torch.randn(Co, Ci, 3, 3, generator=g, dtype=torch.float64) / math.sqrt(9 * Ci)
+    b = torch.randn(Co, generator=g, dtype=torch.float64) * 0.1
+    x = torch.randn(Ci, H, W, generator=g, dtype=torch.float64)
+    dt = torch.float64 if f64 else torch.float32
+    xb = F.pad(x.to(dt), (1, 1, 1, 1))
+    conv = _Conv2d(w if f64 else w.float(), b if f64 else b.float(), DEV, f64=f64)
+    out = torch.full((Co, H + 2, W + 2), float("nan"), device=DEV, dtype=dt)
     conv(xb.to(DEV).contiguous(), H, W, out)
     torch.cuda.synchronize()
     o = out.cpu()
-    ref = F.conv2d(x.unsqueeze(0).double(), w.double(), b.double(), padding=1)[0]
-    close(o[:, 1:-1, 1:-1], ref)
+    ref = F.conv2d(x.to(dt).double().unsqueeze(0), w.to(dt).double(), b.to(dt).double(), padding=1)[0]
+    if f64:
+        assert (o[:, 1:-1, 1:-1] - ref).abs().max().item() <= 1e-13 * max(1.0, ref.abs().max().item())
+    else:
+        close(o[:, 1:-1, 1:-1], ref)
     border = torch.ones(H + 2, W + 2, dtype=torch.bool)
     border[1:-1, 1:-1] = False
     assert torch.equal(o[:, border], torch.zeros(Co, int(border.sum())))
