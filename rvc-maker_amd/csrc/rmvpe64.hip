@@ -17,6 +17,7 @@
 // cycles, so the staging work per chunk is small beside the 4 x FM x FN MFMAs it feeds.
 #include "rvc_common.h"
 #include <stdlib.h>
+#include <algorithm>
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
@@ -37,6 +38,13 @@ RVC_DEV double act64(double v, int act, double slope) {
 
 constexpr int KC = 16;  // flattened k per chunk (4 MFMA k-steps)
 
+// scripts/conv64_dbg.hip builds this file with C64_DBG bits set to take parts of the main loop out (timing
+// only; the results are then wrong): 1 = no global staging loads, 2 = no LDS staging stores, 4 = no barrier,
+// 8 = no LDS operand reads
+#ifndef C64_DBG
+#define C64_DBG 0
+#endif
+
 // staged input doubles per thread (rows * span <= 256 * NB): 12 for the 512-column tile (3 channel rows of a
 // 3x3 conv's 774-wide span), 8 otherwise (a K = 1 chunk's 16 rows of 128)
 template <int BN>
@@ -49,7 +57,7 @@ struct C64 {
     const double* res;
     double* y;
     float* yf;
-    double* ws;  // split-K partials [ksplit][B][Co][Lout]
+    double* ws;  // split-K partials [ksplit][B][Co][nout]
     int64_t B, Ci, Co, Lin, Lout;
     int64_t x_bs, y_bs, res_bs;
     int K, pad, out_act, wrap;
@@ -57,6 +65,10 @@ struct C64 {
     int ntoff;
     int toff[16];
     int span, span_s, rows_max, ksplit, cps;  // cps = chunks per split
+    // compact form (2-D images with a narrow width): the GEMM's columns are the H x W interior cells only, not
+    // the (H + 2) x (W + 2) bordered image (whose border columns are 2 / W of the work at W = 4, the 512-channel
+    // layers); cw = W (0: bordered form), chh = H, nout = the column count either way
+    int cw, chh, nout;
 };
 
 RVC_DEV int tap64(const C64& p, int t) { return p.ntoff ? p.toff[t] : t; }
@@ -85,7 +97,31 @@ RVC_DEV void store64(const C64& p, double acc, int b, int m, int t) {
     else p.y[b * p.y_bs + o] = v;
 }
 
-template <int FM, int FN, int WM, int WN>
+// compact form: interior cell n = h W + w sits at (h + 1)(W + 2) + w + 1 of the bordered image
+RVC_DEV int cpos64(const C64& p, int n) { return n + 2 * (n / p.cw) + p.cw + 3; }
+
+// ... and the cells on the image's edge also write the border cells beside them (0), corners included
+RVC_DEV void border64(const C64& p, int b, int m, int n) {
+    const int W = p.cw, R = W + 2;
+    const int h = n / W, w = n - h * W;
+    const int po = n + 2 * h + R + 1;
+    const bool l = w == 0, r = w == W - 1;
+    auto zero = [&](int o) { store64(p, 0.0, b, m, -o - 2); };
+    if (l) zero(po - 1);
+    if (r) zero(po + 1);
+    if (h == 0) {
+        zero(po - R);
+        if (l) zero(po - R - 1);
+        if (r) zero(po - R + 1);
+    }
+    if (h == p.chh - 1) {
+        zero(po + R);
+        if (l) zero(po + R - 1);
+        if (r) zero(po + R + 1);
+    }
+}
+
+template <int FM, int FN, int WM, int WN, bool CMP>
 __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
@@ -110,8 +146,18 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
     const int nch = (kmax + KC - 1) / KC;
     const int ch_beg = split * p.cps;
     const int ch_end = min(nch, ch_beg + p.cps);
-    const int base = n0 - p.pad;
+    const int h0 = CMP ? n0 / p.cw : 0;
+    // the staged tile's first input position: column n0's (bordered) output position - pad
+    const int base = CMP ? n0 + 2 * h0 + p.cw + 3 - p.pad : n0 - p.pad;
     const int lin = (int)p.Lin;
+    const int lk = lane >> 4, ln = lane & 15;
+    // this lane's B-operand column offsets into the staged tile (compact form: + 2 per image row crossed)
+    int xo[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int nl = wn * 16 * FN + j * 16 + ln;
+        xo[j] = CMP ? nl + 2 * ((n0 + nl) / p.cw - h0) : nl;
+    }
 
     // per-thread staging slots of the rows x span input tile (the same for every chunk)
     int bslot[NB64];
@@ -189,7 +235,6 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
 
-    const int lk = lane >> 4, ln = lane & 15;
     if (ch_beg < ch_end) {
         gload(ch_beg);
         sstore(ch_beg, 0);
@@ -198,9 +243,9 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
     for (int ch = ch_beg; ch < ch_end; ++ch) {
         const int cur = (ch - ch_beg) & 1;
         const bool more = ch + 1 < ch_end;
-        if (more) gload(ch + 1);
+        if (more && !(C64_DBG & 1)) gload(ch + 1);
         const double* Ws = Wsb + cur * KC * WS + wm * 16 * FM + ln;
-        const double* Xs = Xsb + cur * xs_n + wn * 16 * FN + ln;
+        const double* Xs = Xsb + cur * xs_n;
         // the chunk's tap offsets first (one LDS read per k-step, all issued together), then the operands
         // of k-step ks + 1 are read while k-step ks's MFMAs run (register double buffer)
         int ko[KC / 4];
@@ -210,28 +255,28 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) a[0][i] = Ws[lk * WS + i * 16];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bv[0][j] = Xs[ko[0] + j * 16];
+        for (int j = 0; j < FN; ++j) bv[0][j] = Xs[ko[0] + xo[j]];
 #pragma unroll
         for (int ks = 0; ks < KC / 4; ++ks) {
-            const int q = ks & 1;
-            if (ks + 1 < KC / 4) {
+            const int q = (C64_DBG & 8) ? 0 : ks & 1;
+            if (ks + 1 < KC / 4 && !(C64_DBG & 8)) {
                 const int kk = (ks + 1) * 4 + lk;
 #pragma unroll
                 for (int i = 0; i < FM; ++i) a[q ^ 1][i] = Ws[kk * WS + i * 16];
 #pragma unroll
-                for (int j = 0; j < FN; ++j) bv[q ^ 1][j] = Xs[ko[ks + 1] + j * 16];
+                for (int j = 0; j < FN; ++j) bv[q ^ 1][j] = Xs[ko[ks + 1] + xo[j]];
             }
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) acc[i][j] = mfma64(a[q][i], bv[q][j], acc[i][j]);
         }
-        if (more) sstore(ch + 1, cur ^ 1);
-        __syncthreads();
+        if (more && !(C64_DBG & 2)) sstore(ch + 1, cur ^ 1);
+        if (!(C64_DBG & 4)) __syncthreads();
     }
 
     if (p.ksplit > 1) {
-        double* wsb = p.ws + ((int64_t)split * p.B + b) * p.Co * p.Lout;
+        double* wsb = p.ws + ((int64_t)split * p.B + b) * p.Co * p.nout;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -240,14 +285,15 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
                     const int n = n0 + wn * 16 * FN + j * 16 + ln;
-                    if (m < Co && n < (int)p.Lout) wsb[(int64_t)m * p.Lout + n] = acc[i][j][r];
+                    if (m < Co && n < p.nout) wsb[(int64_t)m * p.nout + n] = acc[i][j][r];
                 }
             }
         return;
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-        const int t = opos64(p, n0 + wn * 16 * FN + j * 16 + ln);
+        const int n = n0 + wn * 16 * FN + j * 16 + ln;
+        const int t = CMP ? (n < p.nout ? cpos64(p, n) : -1) : opos64(p, n);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -256,25 +302,143 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
                 if (m < Co) store64(p, acc[i][j][r], b, m, t);
             }
     }
+    if (CMP) {  // the border cells beside this tile's edge cells (after the values: no accumulator is live)
+        for (int j = 0; j < FN; ++j) {
+            const int n = n0 + wn * 16 * FN + j * 16 + ln;
+            if (n >= p.nout) continue;
+            for (int i = 0; i < FM; ++i)
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + wm * 16 * FM + i * 16 + lk + 4 * r;
+                    if (m < Co) border64(p, b, m, n);
+                }
+        }
+    }
 }
 
 // split-K: the partials summed in split order, then the epilogue
 __global__ void conv64_splitk_reduce(C64 p) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     const int m = blockIdx.y, b = blockIdx.z;
-    if (n >= (int)p.Lout) return;
-    const int64_t sstride = p.B * p.Co * p.Lout;
-    const double* src = p.ws + ((int64_t)b * p.Co + m) * p.Lout + n;
+    if (n >= p.nout) return;
+    const int64_t sstride = p.B * p.Co * p.nout;
+    const double* src = p.ws + ((int64_t)b * p.Co + m) * p.nout + n;
     double s = 0.0;
     for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
-    store64(p, s, b, m, opos64(p, n));
+    if (p.cw) {
+        store64(p, s, b, m, cpos64(p, n));
+        border64(p, b, m, n);
+    } else {
+        store64(p, s, b, m, opos64(p, n));
+    }
 }
 
 struct Cfg64 {
     int FM, FN, WM, WN;
 };
 
-int plan64(const rvc_conv64_args* a, C64& p, Cfg64& cfg, dim3& grid, size_t& lds) {
+// the tiles the planner chooses from (BM x BN = 16 FM WM x 16 FN WN)
+constexpr int N_TILES64 = 8;
+constexpr Cfg64 kTiles64[N_TILES64] = {
+    {1, 8, 1, 4},  // 16 x 512
+    {1, 4, 1, 4},  // 16 x 256
+    {2, 4, 1, 4},  // 32 x 256
+    {2, 2, 1, 4},  // 32 x 128
+    {2, 4, 2, 2},  // 64 x 128
+    {2, 2, 2, 2},  // 64 x 64
+    {4, 4, 2, 2},  // 128 x 128
+    {4, 2, 2, 2},  // 128 x 64
+};
+
+// the compact form of the 128 x 128 tile spills (its per-lane column offsets on top of 255 VGPRs): not built
+constexpr bool has_cmp64(int t) { return t != 6; }
+
+template <int T, bool CMP>
+const void* kernel64() {
+    constexpr Cfg64 c = kTiles64[T];
+    if constexpr (CMP && !has_cmp64(T)) return nullptr;
+    else return reinterpret_cast<const void*>(&conv64_kernel<c.FM, c.FN, c.WM, c.WN, CMP>);
+}
+
+template <int T>
+void launch64t(const C64& p, dim3 grid, size_t lds, hipStream_t s) {
+    constexpr Cfg64 c = kTiles64[T];
+    if constexpr (has_cmp64(T)) {
+        if (p.cw) {
+            hipLaunchKernelGGL((conv64_kernel<c.FM, c.FN, c.WM, c.WN, true>), grid, dim3(256), lds, s, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((conv64_kernel<c.FM, c.FN, c.WM, c.WN, false>), grid, dim3(256), lds, s, p);
+}
+
+void launch64(int tile, const C64& p, dim3 grid, size_t lds, hipStream_t s) {
+    switch (tile) {
+        case 0: launch64t<0>(p, grid, lds, s); break;
+        case 1: launch64t<1>(p, grid, lds, s); break;
+        case 2: launch64t<2>(p, grid, lds, s); break;
+        case 3: launch64t<3>(p, grid, lds, s); break;
+        case 4: launch64t<4>(p, grid, lds, s); break;
+        case 5: launch64t<5>(p, grid, lds, s); break;
+        case 6: launch64t<6>(p, grid, lds, s); break;
+        default: launch64t<7>(p, grid, lds, s); break;
+    }
+}
+
+// blocks of a tile resident per CU by its registers (the runtime's occupancy answer, asked once per tile)
+int occ64(int tile, bool cmp) {
+    static int cache[N_TILES64][2];
+    int& o = cache[tile][cmp];
+    if (o == 0) {
+        const void* k = nullptr;
+        switch (tile) {
+            case 0: k = cmp ? kernel64<0, true>() : kernel64<0, false>(); break;
+            case 1: k = cmp ? kernel64<1, true>() : kernel64<1, false>(); break;
+            case 2: k = cmp ? kernel64<2, true>() : kernel64<2, false>(); break;
+            case 3: k = cmp ? kernel64<3, true>() : kernel64<3, false>(); break;
+            case 4: k = cmp ? kernel64<4, true>() : kernel64<4, false>(); break;
+            case 5: k = cmp ? kernel64<5, true>() : kernel64<5, false>(); break;
+            case 6: k = cmp ? kernel64<6, true>() : kernel64<6, false>(); break;
+            default: k = cmp ? kernel64<7, true>() : kernel64<7, false>(); break;
+        }
+        int n = 0;
+        if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, 0) != hipSuccess || n < 1) n = 1;
+        o = n;
+    }
+    return o;
+}
+
+// forced plan (rvc_conv64_set_plan; diagnostics and sweeps): tile, split-K, compact (-1 = the planner's)
+int g_force_tile = -1, g_force_ks = -1, g_force_cmp = -1;
+
+struct Plan64 {
+    int tile, ks, cmp;
+    double cost_ns;
+};
+
+// The planner's time model (ns) of one (tile, split-K, form) choice, fitted (least squares, median error 8.5 %)
+// to every forced plan on RMVPE's U-Net shapes (scripts/conv64_sweep.py, profiles/r4_conv64_sweep.json): blocks
+// are dealt evenly over 256 CUs and run `occ` at a time; a block's MFMAs (MFMA_NS each per SIMD, the chip's
+// measured f64 rate) cost SHARED of that when its CU holds other blocks too and LONE when it runs alone; every
+// 16-deep chunk of every block costs CHUNK_NS of its CU's time (staging, barrier); a split adds the partials'
+// round trip (RED_BPNS bytes per ns) and the reduce launch.
+constexpr double MFMA_NS = 44.6, SHARED = 0.753, LONE = 1.026, CHUNK_NS = 593.0, RED_BPNS = 7700.0,
+                 RED_FIX_NS = 1630.0;
+
+double cost64(int FM, int FN, int64_t nblk, int cps, int occ) {
+    const double bt = cps * FM * FN * 4 * MFMA_NS;
+    const int64_t per_cu = (nblk + 255) / 256;
+    const int64_t full = per_cu / occ, rem = per_cu % occ;
+    const int64_t shared = (occ > 1 ? full * occ : 0) + (rem > 1 ? rem : 0);
+    const int64_t lone = (occ == 1 ? full : 0) + (rem == 1 ? 1 : 0);
+    return bt * (SHARED * shared + LONE * lone) + CHUNK_NS * cps * per_cu;
+}
+
+// the staged tile's width (columns + tap halo) for a tile of BN columns
+int span64(int BN, int maxoff, int cw) {
+    return cw ? BN + 2 * ((cw + BN - 2) / cw) + maxoff : BN + maxoff;
+}
+
+int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds) {
     RVC_CHECK_ARG(a && a->x && a->w && a->y, "conv64: null pointer");
     RVC_CHECK_ARG(a->B > 0 && a->Ci > 0 && a->Co > 0 && a->K > 0 && a->Lin > 0 && a->Lout > 0,
                   "conv64: bad sizes B=%lld Ci=%lld Co=%lld K=%d Lin=%lld Lout=%lld", (long long)a->B,
@@ -286,7 +450,8 @@ int plan64(const rvc_conv64_args* a, C64& p, Cfg64& cfg, dim3& grid, size_t& lds
     RVC_CHECK_ARG(a->out_act == RVC_ACT_NONE || a->out_act == RVC_ACT_RELU || a->out_act == RVC_ACT_SIGMOID ||
                       a->out_act == RVC_ACT_LOGCLAMP,
                   "conv64: out_act %d (NONE, RELU, SIGMOID, LOGCLAMP)", a->out_act);
-    RVC_CHECK_ARG(a->wrap == 0 || (a->wrap >= 3 && a->Lout % a->wrap == 0), "conv64: Lout must be rows x wrap");
+    RVC_CHECK_ARG(a->wrap == 0 || (a->wrap >= 3 && a->Lout % a->wrap == 0 && a->Lout / a->wrap >= 3),
+                  "conv64: Lout must be rows x wrap");
     int maxoff = a->ntoff ? 0 : a->K - 1;
     for (int i = 0; i < a->ntoff; ++i) {
         RVC_CHECK_ARG(a->toff[i] >= 0, "conv64: negative tap offset");
@@ -304,51 +469,53 @@ int plan64(const rvc_conv64_args* a, C64& p, Cfg64& cfg, dim3& grid, size_t& lds
     p.ntoff = a->ntoff;
     for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff && i < a->ntoff ? a->toff[i] : 0;
 
-    if (a->Co <= 16) cfg = {1, 8, 1, 4};       // 16 x 512
-    else if (a->Co <= 32) cfg = {2, 4, 1, 4};  // 32 x 256
-    else if (a->Co <= 64) cfg = {2, 4, 2, 2};  // 64 x 128
-    else cfg = {4, 4, 2, 2};                   // 128 x 128
     int rows_max = (KC % a->K == 0) ? KC / a->K : (KC - 1) / a->K + 2;
     if (rows_max > a->Ci) rows_max = (int)a->Ci;
-    int BN = 16 * cfg.FN * cfg.WN;
-    // a wide tile whose staged rows x span exceed its per-thread budget (K = 1 / 2-tap convs over many rows)
-    // takes the 64 x 128 tile instead
-    if ((int64_t)rows_max * (BN + maxoff) > 256 * (BN >= 512 ? 12 : 8)) {
-        cfg = {2, 4, 2, 2};
-        BN = 128;
+    const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
+    const int W = a->wrap ? (int)a->wrap - 2 : 0, H = a->wrap ? (int)(a->Lout / a->wrap) - 2 : 0;
+    const int64_t ncols[2] = {a->Lout, (int64_t)H * W};
+
+    Plan64 best = {-1, 1, 0, 1e300};
+    for (int cmp = 0; cmp < (a->wrap ? 2 : 1); ++cmp) {
+        if (g_force_cmp >= 0 && cmp != g_force_cmp) continue;
+        for (int t = 0; t < N_TILES64; ++t) {
+            if ((g_force_tile >= 0 && t != g_force_tile) || (cmp && !has_cmp64(t))) continue;
+            const Cfg64 c = kTiles64[t];
+            const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN;
+            const int span = span64(BN, maxoff, cmp ? W : 0);
+            if ((int64_t)rows_max * span > 256 * (BN >= 512 ? 12 : 8) || span >= 65536) continue;
+            const size_t l = (size_t)(2 * KC * (BM + 4) + 2 * (rows_max * (span + 1) + 1)) * 8 + 2 * KC * 4;
+            if (l > 160 * 1024) continue;
+            const int occ = std::max(1, std::min(occ64(t, cmp), (int)(160 * 1024 / l)));
+            const int64_t tiles = (a->Co + BM - 1) / BM * cdiv(ncols[cmp], BN) * a->B;
+            const int ks_max = std::max(1, std::min(32, nch / 2));
+            for (int ks = 1; ks <= ks_max; ++ks) {
+                if (g_force_ks >= 1 && ks != std::min(g_force_ks, ks_max)) continue;
+                const int cps = (nch + ks - 1) / ks;
+                const int kse = (nch + cps - 1) / cps;
+                if (kse != ks) continue;
+                double cost = cost64(c.FM, c.FN, tiles * kse, cps, occ);
+                if (kse > 1) cost += (double)kse * a->B * a->Co * ncols[cmp] * 16 / RED_BPNS + RED_FIX_NS;
+                if (cost < best.cost_ns) best = {t, kse, cmp, cost};
+            }
+        }
     }
-    const int BM = 16 * cfg.FM * cfg.WM;
-    p.span = BN + maxoff;
+    RVC_CHECK_ARG(best.tile >= 0, "conv64: no tile stages rows %d x span of K %d (maxoff %d)", rows_max, a->K, maxoff);
+    tile = best.tile;
+    const Cfg64 c = kTiles64[tile];
+    const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN;
+    p.cw = best.cmp ? W : 0;
+    p.chh = best.cmp ? H : 0;
+    p.nout = (int)ncols[best.cmp];
+    p.span = span64(BN, maxoff, p.cw);
     p.span_s = p.span + 1;
     p.rows_max = rows_max;
-    RVC_CHECK_ARG((int64_t)rows_max * p.span <= 256 * 8 && p.span < 65536 || (BN >= 512 && rows_max * p.span <= 256 * 12),
-                  "conv64: staged tile too large (rows %d x span %d)", rows_max, p.span);
-    const int mt = (int)((a->Co + BM - 1) / BM);
-    const int64_t tiles = (int64_t)mt * cdiv(a->Lout, BN) * a->B;
-    const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
-    // split-K while the grid underfills the chip (2 blocks per CU): the partials go to a workspace and are
-    // summed in split order by conv64_splitk_reduce
-    static const int target = getenv("RVC_C64_SPLITK_TILES") ? atoi(getenv("RVC_C64_SPLITK_TILES")) : 512;
-    int ks = 1;
-    if (tiles < target && nch >= 4) {
-        ks = (int)((target + tiles - 1) / tiles);
-        if (ks > 16) ks = 16;
-        if (ks > nch / 2) ks = nch / 2;
-        if (ks < 1) ks = 1;
-    }
-    p.cps = (nch + ks - 1) / ks;
+    p.cps = (nch + best.ks - 1) / best.ks;
     p.ksplit = (nch + p.cps - 1) / p.cps;
-    const int WS = BM + 4;
-    lds = (size_t)(2 * KC * WS + 2 * (rows_max * p.span_s + 1)) * 8 + 2 * KC * 4;
-    RVC_CHECK_ARG(lds <= 160 * 1024, "conv64: LDS %zu too large", lds);
-    grid = dim3(cdiv(a->Lout, BN), (unsigned)mt, (unsigned)(a->B * p.ksplit));
+    lds = (size_t)(2 * KC * (BM + 4) + 2 * (rows_max * p.span_s + 1)) * 8 + 2 * KC * 4;
+    grid = dim3(cdiv(p.nout, BN), (unsigned)((a->Co + BM - 1) / BM), (unsigned)(a->B * p.ksplit));
     RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv64: grid too large");
     return RVC_OK;
-}
-
-template <int FM, int FN, int WM, int WN>
-void launch64(const C64& p, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((conv64_kernel<FM, FN, WM, WN>), grid, dim3(256), lds, s, p);
 }
 
 // ---------------------------------------------------------------- f64 image / sequence glue (rmvpe.hip's f32 forms)
@@ -556,34 +723,56 @@ constexpr int G_B_MAX = 16;  // sequences per launch (32 co-resident workgroups 
 
 extern "C" int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a) {
     C64 p;
-    Cfg64 cfg;
+    int tile;
     dim3 grid;
     size_t lds;
-    if (plan64(a, p, cfg, grid, lds) != RVC_OK) return -1;
-    return p.ksplit > 1 ? (int64_t)p.ksplit * p.B * p.Co * p.Lout * 8 : 0;
+    if (plan64(a, p, tile, grid, lds) != RVC_OK) return -1;
+    return p.ksplit > 1 ? (int64_t)p.ksplit * p.B * p.Co * p.nout * 8 : 0;
+}
+
+extern "C" int rvc_conv64_set_plan(int tile, int ksplit, int compact) {
+    RVC_CHECK_ARG(tile >= -1 && tile < N_TILES64 && ksplit >= -1 && ksplit <= 32 && compact >= -1 && compact <= 1,
+                  "conv64_set_plan: tile %d (-1..%d), ksplit %d (-1..32), compact %d (-1..1)", tile, N_TILES64 - 1,
+                  ksplit, compact);
+    g_force_tile = tile;
+    g_force_ks = ksplit;
+    g_force_cmp = compact;
+    return RVC_OK;
+}
+
+extern "C" int rvc_conv64_plan(const rvc_conv64_args* a, int* out) {
+    C64 p;
+    int tile;
+    dim3 grid;
+    size_t lds;
+    const int rc = plan64(a, p, tile, grid, lds);
+    if (rc != RVC_OK) return rc;
+    RVC_CHECK_ARG(out, "conv64_plan: null out");
+    out[0] = tile;
+    out[1] = p.ksplit;
+    out[2] = p.cw != 0;
+    out[3] = (int)(grid.x * grid.y * grid.z);
+    return RVC_OK;
 }
 
 extern "C" int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
     C64 p;
-    Cfg64 cfg;
+    int tile;
     dim3 grid;
     size_t lds;
-    const int rc = plan64(a, p, cfg, grid, lds);
+    const int rc = plan64(a, p, tile, grid, lds);
     if (rc != RVC_OK) return rc;
     if (p.ksplit > 1) {
-        const int64_t need = (int64_t)p.ksplit * p.B * p.Co * p.Lout * 8;
+        const int64_t need = (int64_t)p.ksplit * p.B * p.Co * p.nout * 8;
         RVC_CHECK_ARG(ws && ws_bytes >= need, "conv64: split-K needs %lld B of workspace (got %lld)", (long long)need,
                       (long long)ws_bytes);
         p.ws = (double*)ws;
     }
     hipStream_t s = (hipStream_t)stream;
-    if (cfg.FM == 1) launch64<1, 8, 1, 4>(p, grid, lds, s);
-    else if (cfg.WM == 1) launch64<2, 4, 1, 4>(p, grid, lds, s);
-    else if (cfg.FM == 2) launch64<2, 4, 2, 2>(p, grid, lds, s);
-    else launch64<4, 4, 2, 2>(p, grid, lds, s);
+    launch64(tile, p, grid, lds, s);
     RVC_HIP(hipGetLastError());
     if (p.ksplit > 1) {
-        hipLaunchKernelGGL(conv64_splitk_reduce, dim3(cdiv(p.Lout, 256), (unsigned)p.Co, (unsigned)p.B), dim3(256), 0,
+        hipLaunchKernelGGL(conv64_splitk_reduce, dim3(cdiv(p.nout, 256), (unsigned)p.Co, (unsigned)p.B), dim3(256), 0,
                            s, p);
         RVC_HIP(hipGetLastError());
     }

@@ -17,8 +17,9 @@ void rvc_set_error(const char* fmt, ...) {
 extern "C" const char* rvc_last_error(void) { return g_err; }
 extern "C" int rvc_version(void) { return 1; }
 
-// A stream whose kernels may only use the CUs set in mask (nwords 32-bit words, bit i = CU i; hipExtStreamCreate-
-// WithCUMask).  The clip stream gives its synthesizer stream one, leaving a few CUs to the latency-bound front end.
+// A stream whose kernels may only use the CUs set in mask (nwords 32-bit words; hipExtStreamCreateWithCUMask).
+// Measured (scripts/cu_mask_probe.hip): bit i lands on XCD i mod 8, and a mask naming every CU of one XCD is not
+// applied at all.  The clip stream can give its synthesizer stream one (VC.BACK_CU_MASK; off by default).
 extern "C" int rvc_stream_create_cu_mask(const uint32_t* mask, int nwords, rvc_stream_t* out) {
     if (!mask || nwords <= 0 || !out) {
         rvc_set_error("stream_create_cu_mask: bad args");

@@ -158,6 +158,8 @@ SIGNATURES = {
                           c_void_p],
     "rvc_conv64": [POINTER(Conv64Args), c_void_p, c_int64, c_void_p],
     "rvc_conv64_workspace_bytes": [POINTER(Conv64Args)],
+    "rvc_conv64_plan": [POINTER(Conv64Args), POINTER(c_int)],
+    "rvc_conv64_set_plan": [c_int, c_int, c_int],
     "rvc_stft_mag64": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_int, c_int64, c_int64,
                        c_void_p],
     "rvc_mel_image64": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_double, c_double, c_int64, c_int64,

@@ -568,9 +568,10 @@ class Conv64:
 
 
 def conv64(x, w, Ci, Co, K, *, bias=None, pad=0, Lout=None, out=None, res=None, out_act=ACT_NONE, out_slope=0.0,
-           B=None, Lin=None, x_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, out_f32=False):
+           B=None, Lin=None, x_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, out_f32=False, plan=False):
     """The f64 conv (rvc_conv64): x [B][Ci][Lin] f64, y f64 (or f32 when ``out_f32``), stride 1, K taps at
-    ``toff`` (or 0..K-1), 2-D border masking with ``wrap``; see include/rvc_amd.h."""
+    ``toff`` (or 0..K-1), 2-D border masking with ``wrap``; see include/rvc_amd.h.  ``plan=True`` launches
+    nothing and returns the planner's choice (rvc_conv64_plan): (tile, split-K, compact, blocks)."""
     if B is None:
         B, Cx, Lx = _shape3(x)
         if Lin is None:
@@ -610,12 +611,21 @@ def conv64(x, w, Ci, Co, K, *, bias=None, pad=0, Lout=None, out=None, res=None, 
             a.toff[i] = int(v)
     a.wrap = wrap
     lib = _lib.load()
+    if plan:
+        res4 = (ctypes.c_int * 4)()
+        check(lib.rvc_conv64_plan(ctypes.byref(a), res4), "conv64_plan")
+        return tuple(res4)
     need = lib.rvc_conv64_workspace_bytes(ctypes.byref(a))
     if need < 0:
         raise RuntimeError(f"rvc_amd: conv64 plan failed: {lib.rvc_last_error().decode()}")
     ws = _workspace(out.device, need, "c64") if need else None
     check(lib.rvc_conv64(ctypes.byref(a), _p(ws), need, _stream()), "conv64")
     return out
+
+
+def conv64_set_plan(tile=-1, ksplit=-1, compact=-1):
+    """Force the f64 conv planner's choice (rvc_conv64_set_plan; -1 = the planner's): sweeps and tests."""
+    check(_lib.load().rvc_conv64_set_plan(tile, ksplit, compact), "conv64_set_plan")
 
 
 def _bs(t, nd):

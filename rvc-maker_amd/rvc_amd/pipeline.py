@@ -502,9 +502,11 @@ class VC:
     # leave 4 CUs on each XCD (28 of 32 used per XCD).  The default "mod:8:7" is therefore an unmasked stream of
     # default priority on a hardware queue of its own; that is what the round-3 numbers measured (986-990 xRT
     # against 899-1003 for the high-priority back stream, "none"), while the real 4-CU-per-XCD mask ("top:32")
-    # ran 798-801.  The stream is its own
-    # pooled stream, apart from the per-call side stream (sharing it: 805 -> 650 xRT per call).
-    BACK_CU_MASK = os.environ.get("RVC_BACK_CU_MASK", "mod:8:7")
+    # ran 798-801.  With the f64 RMVPE (round 4, interleaved on one box, 2 runs each): "none" 861 / 861,
+    # "mod:8:7" 842 / 842, "none" at normal back priority 669 / 667 -- so the default is now the plain
+    # high-priority back stream.  A masked stream is its own pooled stream, apart from the per-call side stream
+    # (sharing it: 805 -> 650 xRT per call).
+    BACK_CU_MASK = os.environ.get("RVC_BACK_CU_MASK", "none")
 
     @staticmethod
     def _cu_mask_words(device, spec):

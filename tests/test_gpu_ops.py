@@ -275,6 +275,52 @@ def test_conv2d_bordered_image_writes_zero_border(ops, engine, Ci, Co, H, W, f64
     assert torch.equal(o[:, border], torch.zeros(Co, int(border.sum())))
 
 
+@pytest.mark.parametrize("Ci,Co,H,W,B,k", [(64, 128, 9, 4, 1, 3), (24, 40, 7, 5, 2, 3), (16, 16, 11, 3, 1, 3),
+                                           (48, 72, 6, 4, 2, 1)])
+def test_conv64_every_plan(ops, Ci, Co, H, W, B, k):
+    """The f64 conv engine under every plan its planner can choose (rvc_conv64_set_plan: the 8 tiles, split-K
+    1..8, bordered and compact forms -- the compact one's GEMM columns are the H x W interior cells, and its
+    epilogue writes the border cells beside the image's edge cells): interior = F.conv2d in f64 to 1e-13, border
+    exactly 0, over a NaN-filled output, batched (batch strides) and not."""
+    g = gen(12)
+    w = torch.randn(Co, Ci, k, k, generator=g, dtype=torch.float64) / math.sqrt(k * k * Ci)
+    b = torch.randn(Co, generator=g, dtype=torch.float64) * 0.1
+    x = torch.randn(B, Ci, H, W, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, w, b, padding=k // 2)
+    wrap = W + 2
+    L = (H + 2) * wrap
+    toff = [dy * wrap + dx for dy in range(k) for dx in range(k)]
+    wkm = ops.pack_km(w.reshape(Co, Ci, k * k)).to(DEV)
+    xb = F.pad(x, (1, 1, 1, 1)).to(DEV).contiguous()
+    border = torch.ones(H + 2, W + 2, dtype=torch.bool)
+    border[1:-1, 1:-1] = False
+    seen = set()
+    try:
+        for tile in range(8):
+            for cmp in (0, 1):
+                for ks in (1, 2, 3, 8):
+                    try:
+                        ops.conv64_set_plan(tile, ks, cmp)
+                        out = torch.full((B, Co, H + 2, W + 2), float("nan"), device=DEV, dtype=torch.float64)
+                        kw = dict(bias=b.to(DEV), pad=(wrap + 1) if k == 3 else 0, Lin=L, Lout=L, toff=toff,
+                                  wrap=wrap, B=B, x_bstride=Ci * L, y_bstride=Co * L)
+                        plan = ops.conv64(xb, wkm, Ci, Co, k * k, out=out, plan=True, **kw)
+                        ops.conv64(xb, wkm, Ci, Co, k * k, out=out, **kw)
+                    except RuntimeError:
+                        continue  # a plan the planner refuses for this shape (staging budget / split count)
+                    torch.cuda.synchronize()
+                    seen.add(tuple(plan[:3]))
+                    o = out.cpu()
+                    err = (o[:, :, 1:-1, 1:-1] - ref).abs().max().item()
+                    assert err <= 1e-13 * max(1.0, ref.abs().max().item()), (plan, err)
+                    assert torch.equal(o[:, :, border], torch.zeros(B, Co, int(border.sum()), dtype=o.dtype)), plan
+    finally:
+        ops.conv64_set_plan()
+    # (a K = 1 chunk stages 16 channel rows: only the narrower tiles fit it, and 3 chunks allow no split)
+    assert len({p[0] for p in seen}) >= (6 if k == 3 else 4) and {p[2] for p in seen} == {0, 1}, seen
+    assert k == 1 or max(p[1] for p in seen) >= 3, seen
+
+
 F16_CASES = [c for c in CONV_CASES if c[6] == 1 and c[2] <= 64 and (c[3] == 1 or (c[3] == 2 and c[0] >= 32))]
 
 
