@@ -285,10 +285,10 @@ typedef struct rvc_conv64_args {
 /* split-K workspace (bytes; 0 = none, -1 = bad args), as rvc_conv1d_workspace_bytes */
 int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a);
 /* the planner's choice for a (diagnostics): out[0] tile (0..7: 16x512, 16x256, 32x256, 32x128, 64x128, 64x64,
- * 128x128, 128x64), out[1] split-K, out[2] compact form (wrap > 0: the H x W interior cells as the GEMM's
+ * 128x128, 128x64 with 16-deep k chunks; 8..12: 16x256, 32x128, 64x128, 64x64, 128x64 with 32-deep), out[1] split-K, out[2] compact form (wrap > 0: the H x W interior cells as the GEMM's
  * columns instead of the bordered image), out[3] blocks of the conv launch */
 int rvc_conv64_plan(const rvc_conv64_args* a, int* out);
-/* force the planner (process-wide; sweeps and tests): tile -1..7, ksplit -1..32, compact -1..1 (-1 = planner's) */
+/* force the planner (process-wide; sweeps and tests): tile -1..12, ksplit -1..32, compact -1..1 (-1 = planner's) */
 int rvc_conv64_set_plan(int tile, int ksplit, int compact);
 int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* stft_mag64: rvc_stft_mag with the f64 magnitudes unrounded */

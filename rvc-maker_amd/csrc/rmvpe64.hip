@@ -18,6 +18,7 @@
 #include "rvc_common.h"
 #include <stdlib.h>
 #include <algorithm>
+#include <utility>
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
@@ -25,6 +26,22 @@ namespace {
 
 // v_mfma_f64_16x16x4_f64: lane l holds A[l&15][l>>4], B[l>>4][l&15]; C/D: col = l&15, row = (l>>4) + 4 r
 RVC_DEV doublex4 mfma64(double a, double b, doublex4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+
+// The same 16 x 16 x 4 product as four v_mfma_f64_4x4x4f64 (4 blocks of 4x4x4 per wave), 1.5x the f64 rate of the
+// 16x16x4 form on gfx950 (72 against 47 TFLOP/s, scripts/bigru64_bench.hip).  Its lane layout, found by
+// experiment (scripts/mfma64_layout.hip): block b = (l & 15) >> 2; A: row l & 3, k = l >> 4; B: col l & 3,
+// k = l >> 4; D: col l & 3, row l >> 4.  With B as the 16x16x4 form's B (block b = columns 4b..4b+3) and, for
+// component r, A = rows 4r..4r+3 replicated over the blocks (lane l: A[4r + (l & 3)][l >> 4]), D lane l is
+// row 4r + (l >> 4), col l & 15: the 16x16x4 form's component r, so the epilogue is the same.  (The f64 form
+// has no A broadcast: its CBSZ / ABID bits are modifiers, and ABID is ignored -- measured.)
+RVC_DEV double mfma64q(double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0); }
+
+// Measured (scripts/conv64_dbg.hip, round 4): no faster inside the conv engine than the 16x16x4 form (the MFMA-only
+// loop 45-50 us either way on RMVPE's levels) while the 4 A values per fragment cost VGPRs and occupancy, so it
+// is off; C64_M4=1 builds it.
+#ifndef C64_M4
+#define C64_M4 0
+#endif
 
 // the activations RMVPE's f64 network uses (plan64 refuses the others)
 RVC_DEV double act64(double v, int act, double slope) {
@@ -36,7 +53,6 @@ RVC_DEV double act64(double v, int act, double slope) {
     }
 }
 
-constexpr int KC = 16;  // flattened k per chunk (4 MFMA k-steps)
 
 // scripts/conv64_dbg.hip builds this file with C64_DBG bits set to take parts of the main loop out (timing
 // only; the results are then wrong): 1 = no global staging loads, 2 = no LDS staging stores, 4 = no barrier,
@@ -121,8 +137,9 @@ RVC_DEV void border64(const C64& p, int b, int m, int n) {
     }
 }
 
-template <int FM, int FN, int WM, int WN, bool CMP>
+template <int FM, int FN, int WM, int WN, bool CMP, int KC_>
 __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
+    constexpr int KC = KC_;
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
     constexpr int NB64 = nb64<BN>();
@@ -244,16 +261,20 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
         const int cur = (ch - ch_beg) & 1;
         const bool more = ch + 1 < ch_end;
         if (more && !(C64_DBG & 1)) gload(ch + 1);
-        const double* Ws = Wsb + cur * KC * WS + wm * 16 * FM + ln;
+        // 16x16x4 form: lane reads A[m0 + (l & 15)][k]; 4x4x4 form: A[m0 + 4r + (l & 3)][k], r = 0..3
+        const double* Ws = Wsb + cur * KC * WS + wm * 16 * FM + (C64_M4 ? (lane & 3) : ln);
         const double* Xs = Xsb + cur * xs_n;
+        constexpr int NR = C64_M4 ? 4 : 1;
         // the chunk's tap offsets first (one LDS read per k-step, all issued together), then the operands
         // of k-step ks + 1 are read while k-step ks's MFMAs run (register double buffer)
         int ko[KC / 4];
 #pragma unroll
         for (int ks = 0; ks < KC / 4; ++ks) ko[ks] = koffb[cur * KC + ks * 4 + lk];
-        double a[2][FM], bv[2][FN];
+        double a[2][FM][NR], bv[2][FN];
 #pragma unroll
-        for (int i = 0; i < FM; ++i) a[0][i] = Ws[lk * WS + i * 16];
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) a[0][i][r] = Ws[lk * WS + i * 16 + 4 * r];
 #pragma unroll
         for (int j = 0; j < FN; ++j) bv[0][j] = Xs[ko[0] + xo[j]];
 #pragma unroll
@@ -262,14 +283,23 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
             if (ks + 1 < KC / 4 && !(C64_DBG & 8)) {
                 const int kk = (ks + 1) * 4 + lk;
 #pragma unroll
-                for (int i = 0; i < FM; ++i) a[q ^ 1][i] = Ws[kk * WS + i * 16];
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) a[q ^ 1][i][r] = Ws[kk * WS + i * 16 + 4 * r];
 #pragma unroll
                 for (int j = 0; j < FN; ++j) bv[q ^ 1][j] = Xs[ko[ks + 1] + xo[j]];
             }
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < FN; ++j) acc[i][j] = mfma64(a[q][i], bv[q][j], acc[i][j]);
+                for (int j = 0; j < FN; ++j) {
+                    if constexpr (C64_M4) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[i][j][r] = mfma64q(a[q][i][r], bv[q][j], acc[i][j][r]);
+                    } else {
+                        acc[i][j] = mfma64(a[q][i][0], bv[q][j], acc[i][j]);
+                    }
+                }
         }
         if (more && !(C64_DBG & 2)) sstore(ch + 1, cur ^ 1);
         if (!(C64_DBG & 4)) __syncthreads();
@@ -333,30 +363,38 @@ __global__ void conv64_splitk_reduce(C64 p) {
 }
 
 struct Cfg64 {
-    int FM, FN, WM, WN;
+    int FM, FN, WM, WN, KC;
 };
 
-// the tiles the planner chooses from (BM x BN = 16 FM WM x 16 FN WN)
-constexpr int N_TILES64 = 8;
+// the tiles the planner chooses from (BM x BN = 16 FM WM x 16 FN WN, k chunk KC): the 32-deep chunks halve the
+// barriers and staging rounds per k and pay where the tile's registers and LDS leave room (scripts/conv64_dbg.hip:
+// 32 x 128 tiles 15-20 % faster, 32 x 256 ones slower)
+constexpr int N_TILES64 = 13;
 constexpr Cfg64 kTiles64[N_TILES64] = {
-    {1, 8, 1, 4},  // 16 x 512
-    {1, 4, 1, 4},  // 16 x 256
-    {2, 4, 1, 4},  // 32 x 256
-    {2, 2, 1, 4},  // 32 x 128
-    {2, 4, 2, 2},  // 64 x 128
-    {2, 2, 2, 2},  // 64 x 64
-    {4, 4, 2, 2},  // 128 x 128
-    {4, 2, 2, 2},  // 128 x 64
+    {1, 8, 1, 4, 16},  // 0: 16 x 512
+    {1, 4, 1, 4, 16},  // 1: 16 x 256
+    {2, 4, 1, 4, 16},  // 2: 32 x 256
+    {2, 2, 1, 4, 16},  // 3: 32 x 128
+    {2, 4, 2, 2, 16},  // 4: 64 x 128
+    {2, 2, 2, 2, 16},  // 5: 64 x 64
+    {4, 4, 2, 2, 16},  // 6: 128 x 128
+    {4, 2, 2, 2, 16},  // 7: 128 x 64
+    {1, 4, 1, 4, 32},  // 8: 16 x 256, KC 32
+    {2, 2, 1, 4, 32},  // 9: 32 x 128, KC 32
+    {2, 4, 2, 2, 32},  // 10: 64 x 128, KC 32
+    {2, 2, 2, 2, 32},  // 11: 64 x 64, KC 32
+    {4, 2, 2, 2, 32},  // 12: 128 x 64, KC 32
 };
 
-// the compact form of the 128 x 128 tile spills (its per-lane column offsets on top of 255 VGPRs): not built
+// the compact form of the 128 x 128 tile spills (its per-lane column offsets on top of 255 VGPRs): not built;
+// with the 4x4x4 MFMA form (4 A values per fragment) the bordered one spills too and the planner skips it
 constexpr bool has_cmp64(int t) { return t != 6; }
 
 template <int T, bool CMP>
 const void* kernel64() {
     constexpr Cfg64 c = kTiles64[T];
     if constexpr (CMP && !has_cmp64(T)) return nullptr;
-    else return reinterpret_cast<const void*>(&conv64_kernel<c.FM, c.FN, c.WM, c.WN, CMP>);
+    else return reinterpret_cast<const void*>(&conv64_kernel<c.FM, c.FN, c.WM, c.WN, CMP, c.KC>);
 }
 
 template <int T>
@@ -364,24 +402,27 @@ void launch64t(const C64& p, dim3 grid, size_t lds, hipStream_t s) {
     constexpr Cfg64 c = kTiles64[T];
     if constexpr (has_cmp64(T)) {
         if (p.cw) {
-            hipLaunchKernelGGL((conv64_kernel<c.FM, c.FN, c.WM, c.WN, true>), grid, dim3(256), lds, s, p);
+            hipLaunchKernelGGL((conv64_kernel<c.FM, c.FN, c.WM, c.WN, true, c.KC>), grid, dim3(256), lds, s, p);
             return;
         }
     }
-    hipLaunchKernelGGL((conv64_kernel<c.FM, c.FN, c.WM, c.WN, false>), grid, dim3(256), lds, s, p);
+    hipLaunchKernelGGL((conv64_kernel<c.FM, c.FN, c.WM, c.WN, false, c.KC>), grid, dim3(256), lds, s, p);
+}
+
+template <int... T>
+void launch64_any(int tile, const C64& p, dim3 grid, size_t lds, hipStream_t s, std::integer_sequence<int, T...>) {
+    ((tile == T ? launch64t<T>(p, grid, lds, s) : void()), ...);
 }
 
 void launch64(int tile, const C64& p, dim3 grid, size_t lds, hipStream_t s) {
-    switch (tile) {
-        case 0: launch64t<0>(p, grid, lds, s); break;
-        case 1: launch64t<1>(p, grid, lds, s); break;
-        case 2: launch64t<2>(p, grid, lds, s); break;
-        case 3: launch64t<3>(p, grid, lds, s); break;
-        case 4: launch64t<4>(p, grid, lds, s); break;
-        case 5: launch64t<5>(p, grid, lds, s); break;
-        case 6: launch64t<6>(p, grid, lds, s); break;
-        default: launch64t<7>(p, grid, lds, s); break;
-    }
+    launch64_any(tile, p, grid, lds, s, std::make_integer_sequence<int, N_TILES64>{});
+}
+
+template <int... T>
+const void* kernel64_any(int tile, bool cmp, std::integer_sequence<int, T...>) {
+    const void* k = nullptr;
+    ((tile == T ? (void)(k = cmp ? kernel64<T, true>() : kernel64<T, false>()) : void()), ...);
+    return k;
 }
 
 // blocks of a tile resident per CU by its registers (the runtime's occupancy answer, asked once per tile)
@@ -389,17 +430,7 @@ int occ64(int tile, bool cmp) {
     static int cache[N_TILES64][2];
     int& o = cache[tile][cmp];
     if (o == 0) {
-        const void* k = nullptr;
-        switch (tile) {
-            case 0: k = cmp ? kernel64<0, true>() : kernel64<0, false>(); break;
-            case 1: k = cmp ? kernel64<1, true>() : kernel64<1, false>(); break;
-            case 2: k = cmp ? kernel64<2, true>() : kernel64<2, false>(); break;
-            case 3: k = cmp ? kernel64<3, true>() : kernel64<3, false>(); break;
-            case 4: k = cmp ? kernel64<4, true>() : kernel64<4, false>(); break;
-            case 5: k = cmp ? kernel64<5, true>() : kernel64<5, false>(); break;
-            case 6: k = cmp ? kernel64<6, true>() : kernel64<6, false>(); break;
-            default: k = cmp ? kernel64<7, true>() : kernel64<7, false>(); break;
-        }
+        const void* k = kernel64_any(tile, cmp, std::make_integer_sequence<int, N_TILES64>{});
         int n = 0;
         if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, 0) != hipSuccess || n < 1) n = 1;
         o = n;
@@ -415,22 +446,24 @@ struct Plan64 {
     double cost_ns;
 };
 
-// The planner's time model (ns) of one (tile, split-K, form) choice, fitted (least squares, median error 8.5 %)
-// to every forced plan on RMVPE's U-Net shapes (scripts/conv64_sweep.py, profiles/r4_conv64_sweep.json): blocks
-// are dealt evenly over 256 CUs and run `occ` at a time; a block's MFMAs (MFMA_NS each per SIMD, the chip's
-// measured f64 rate) cost SHARED of that when its CU holds other blocks too and LONE when it runs alone; every
-// 16-deep chunk of every block costs CHUNK_NS of its CU's time (staging, barrier); a split adds the partials'
-// round trip (RED_BPNS bytes per ns) and the reduce launch.
-constexpr double MFMA_NS = 44.6, SHARED = 0.753, LONE = 1.026, CHUNK_NS = 593.0, RED_BPNS = 7700.0,
-                 RED_FIX_NS = 1630.0;
+// The planner's time model (ns) of one (tile, split-K, form) choice, fitted (least squares weighted to the fast
+// plans, median error 5.8 %) to every forced plan on RMVPE's U-Net shapes (scripts/conv64_sweep.py,
+// profiles/r4_conv64_sweep.json): blocks are dealt evenly over 256 CUs and run `occ` at a time; a block's MFMAs
+// (MFMA_NS each per SIMD, the chip's measured f64 rate) cost SHARED of that when its CU holds other blocks too
+// and LONE when it runs alone; every k chunk of every block costs CHUNK_NS plus STAGE_NS per byte it stages
+// (input rows with their halo, weights); a split adds the partials' round trip (RED_BPNS bytes per ns) and the
+// reduce launch.  The fit leaves the MFMA terms small: on these shapes the staging, not the f64 MFMA rate, sets
+// the time (scripts/conv64_dbg.hip: the MFMA-only loop runs 45-50 us where the whole kernel takes 55-60).
+constexpr double MFMA_NS = 44.6, SHARED = 0.156, LONE = 0.247, CHUNK_NS = 287.6, STAGE_NS = 0.0247,
+                 RED_BPNS = 8770.0, RED_FIX_NS = 7890.0;
 
-double cost64(int FM, int FN, int64_t nblk, int cps, int occ) {
-    const double bt = cps * FM * FN * 4 * MFMA_NS;
+double cost64(int FM, int FN, int KC, int64_t nblk, int cps, int occ, int64_t stage_bytes) {
+    const double bt = cps * FM * FN * KC * MFMA_NS;
     const int64_t per_cu = (nblk + 255) / 256;
     const int64_t full = per_cu / occ, rem = per_cu % occ;
     const int64_t shared = (occ > 1 ? full * occ : 0) + (rem > 1 ? rem : 0);
     const int64_t lone = (occ == 1 ? full : 0) + (rem == 1 ? 1 : 0);
-    return bt * (SHARED * shared + LONE * lone) + CHUNK_NS * cps * per_cu;
+    return bt * (SHARED * shared + LONE * lone) + (CHUNK_NS + STAGE_NS * stage_bytes) * cps * per_cu;
 }
 
 // the staged tile's width (columns + tap halo) for a tile of BN columns
@@ -469,9 +502,10 @@ int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds)
     p.ntoff = a->ntoff;
     for (int i = 0; i < 16; ++i) p.toff[i] = a->ntoff && i < a->ntoff ? a->toff[i] : 0;
 
-    int rows_max = (KC % a->K == 0) ? KC / a->K : (KC - 1) / a->K + 2;
-    if (rows_max > a->Ci) rows_max = (int)a->Ci;
-    const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
+    auto rows_of = [&](int kc) {
+        const int r = (kc % a->K == 0) ? kc / a->K : (kc - 1) / a->K + 2;
+        return r > a->Ci ? (int)a->Ci : r;
+    };
     const int W = a->wrap ? (int)a->wrap - 2 : 0, H = a->wrap ? (int)(a->Lout / a->wrap) - 2 : 0;
     const int64_t ncols[2] = {a->Lout, (int64_t)H * W};
 
@@ -479,9 +513,13 @@ int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds)
     for (int cmp = 0; cmp < (a->wrap ? 2 : 1); ++cmp) {
         if (g_force_cmp >= 0 && cmp != g_force_cmp) continue;
         for (int t = 0; t < N_TILES64; ++t) {
-            if ((g_force_tile >= 0 && t != g_force_tile) || (cmp && !has_cmp64(t))) continue;
+            if ((g_force_tile >= 0 && t != g_force_tile) || (cmp && !has_cmp64(t)) || (C64_M4 && t == 6)) continue;
+            // the 16 x 512 tile lost to 16 x 256 on every shape of the sweep (occupancy 2 against 4): forced only
+            if (t == 0 && g_force_tile != 0) continue;
             const Cfg64 c = kTiles64[t];
-            const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN;
+            const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN, KC = c.KC;
+            const int rows_max = rows_of(KC);
+            const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
             const int span = span64(BN, maxoff, cmp ? W : 0);
             if ((int64_t)rows_max * span > 256 * (BN >= 512 ? 12 : 8) || span >= 65536) continue;
             const size_t l = (size_t)(2 * KC * (BM + 4) + 2 * (rows_max * (span + 1) + 1)) * 8 + 2 * KC * 4;
@@ -494,16 +532,18 @@ int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds)
                 const int cps = (nch + ks - 1) / ks;
                 const int kse = (nch + cps - 1) / cps;
                 if (kse != ks) continue;
-                double cost = cost64(c.FM, c.FN, tiles * kse, cps, occ);
+                double cost = cost64(c.FM, c.FN, KC, tiles * kse, cps, occ, ((int64_t)rows_max * span + KC * BM) * 8);
                 if (kse > 1) cost += (double)kse * a->B * a->Co * ncols[cmp] * 16 / RED_BPNS + RED_FIX_NS;
                 if (cost < best.cost_ns) best = {t, kse, cmp, cost};
             }
         }
     }
-    RVC_CHECK_ARG(best.tile >= 0, "conv64: no tile stages rows %d x span of K %d (maxoff %d)", rows_max, a->K, maxoff);
+    RVC_CHECK_ARG(best.tile >= 0, "conv64: no tile stages the rows x span of K %d (maxoff %d)", a->K, maxoff);
     tile = best.tile;
     const Cfg64 c = kTiles64[tile];
-    const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN;
+    const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN, KC = c.KC;
+    const int rows_max = rows_of(KC);
+    const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
     p.cw = best.cmp ? W : 0;
     p.chh = best.cmp ? H : 0;
     p.nout = (int)ncols[best.cmp];

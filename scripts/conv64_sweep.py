@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "rvc-maker_amd")]
 from rvc_amd import ops  # noqa: E402
 
-TILES = ["16x512", "16x256", "32x256", "32x128", "64x128", "64x64", "128x128", "128x64"]
+TILES = ["16x512", "16x256", "32x256", "32x128", "64x128", "64x64", "128x128", "128x64", "16x256/32", "32x128/32",
+         "64x128/32", "64x64/32", "128x64/32"]
 # (Ci, Co, H, W): one 3x3 conv per U-Net level (every level's convs are 1.77 GFLOP), the encoder's first conv
 SHAPES = [(16, 16, 3008, 128), (32, 32, 1504, 64), (64, 64, 752, 32), (128, 128, 376, 16), (256, 256, 188, 8),
           (512, 512, 94, 4), (256, 512, 94, 4), (1, 16, 3008, 128)]
@@ -66,7 +67,7 @@ def main():
                "forced": []}
         best = (us, plan)
         kss = [1, 2, 4, 8, 16, 32] if quick else [1, 2, 3, 4, 6, 8, 12, 16, 21, 24, 32]
-        for t in range(8):
+        for t in range(len(TILES)):
             for cmp in (0, 1):
                 for ks in kss:
                     try:
