@@ -41,6 +41,7 @@ def run(x, w, b, Ci, Co, H, W, out, reps):
 def main():
     path = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else "gpurun_out/conv64_sweep.json"
     quick = "--quick" in sys.argv
+    planner_only = "--planner-only" in sys.argv
     torch.manual_seed(0)
     rows = []
     for Ci, Co, H, W in SHAPES:
@@ -66,6 +67,9 @@ def main():
         row = {"Ci": Ci, "Co": Co, "H": H, "W": W, "planner": list(plan), "us": us, "err": err, "border": border,
                "forced": []}
         best = (us, plan)
+        if planner_only:
+            rows.append(row)
+            continue
         kss = [1, 2, 4, 8, 16, 32] if quick else [1, 2, 3, 4, 6, 8, 12, 16, 21, 24, 32]
         for t in range(len(TILES)):
             for cmp in (0, 1):
