@@ -281,6 +281,9 @@ typedef struct rvc_conv64_args {
     double out_slope;
     int ntoff, wrap;
     int toff[16];
+    /* per-batch weights: batch b uses w + (b % w_bmod) * w_bstride (w_bmod 0: every batch the same w) */
+    int64_t w_bstride;
+    int w_bmod, _pad0;
 } rvc_conv64_args;
 /* split-K workspace (bytes; 0 = none, -1 = bad args), as rvc_conv1d_workspace_bytes */
 int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a);
@@ -291,6 +294,24 @@ int rvc_conv64_plan(const rvc_conv64_args* a, int* out);
 /* force the planner (process-wide; sweeps and tests): tile -1..12, ksplit -1..32, compact -1..1 (-1 = planner's) */
 int rvc_conv64_set_plan(int tile, int ksplit, int compact);
 int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
+/* Winograd F(4x4, 3x3) f64 conv for RMVPE's deep levels (3x3 pad 1 on bordered [C][H+2][W+2] images, as
+ * conv64 with wrap): y = act(conv(x) + bias) (+ res), border cells 0.  v = rvc_wino64_weights(KM w [Ci*9][Co])
+ * = the 36 transformed weight matrices [36][Ci][Co] (G g G^T).  rvc_wino64_use(Ci, Co): whether the f64 RMVPE
+ * takes this form for a Ci -> Co conv (>= 64 channels each; RVC_RMVPE_WINO=0 turns it off). */
+typedef struct rvc_wino64_args {
+    const double* x;
+    const double* v;
+    const double* bias;
+    const double* res;
+    void* y;
+    int64_t B, Ci, Co, H, W;
+    int64_t x_bstride, y_bstride, res_bstride;
+    int out_act, y_f32;
+} rvc_wino64_args;
+int rvc_wino64_use(int64_t Ci, int64_t Co);
+int rvc_wino64_weights(const double* w, double* v, int64_t Ci, int64_t Co, rvc_stream_t stream);
+int64_t rvc_wino64_workspace_bytes(const rvc_wino64_args* a);
+int rvc_wino64_conv(const rvc_wino64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* stft_mag64: rvc_stft_mag with the f64 magnitudes unrounded */
 int rvc_stft_mag64(const float* x, const float* win, double* mag, int64_t B, int64_t N, int64_t F, int nfft, int hop,
                    int64_t x_bstride, int64_t mag_bstride, rvc_stream_t stream);

@@ -17,6 +17,7 @@
 // cycles, so the staging work per chunk is small beside the 4 x FM x FN MFMAs it feeds.
 #include "rvc_common.h"
 #include <stdlib.h>
+#include <string.h>
 #include <algorithm>
 #include <utility>
 
@@ -85,6 +86,9 @@ struct C64 {
     // the (H + 2) x (W + 2) bordered image (whose border columns are 2 / W of the work at W = 4, the 512-channel
     // layers); cw = W (0: bordered form), chh = H, nout = the column count either way
     int cw, chh, nout;
+    // per-batch weights (the Winograd GEMMs): batch b uses w + (b % w_bmod) * w_bs (w_bmod 0: one weight)
+    int64_t w_bs;
+    int w_bmod;
 };
 
 RVC_DEV int tap64(const C64& p, int t) { return p.ntoff ? p.toff[t] : t; }
@@ -159,6 +163,7 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
     const int n0 = blockIdx.x * BN;
     const int Co = (int)p.Co, Ci = (int)p.Ci, K = p.K;
     const double* xb = p.x + b * p.x_bs;
+    const double* wb = p.w + (p.w_bmod ? (int64_t)(b % p.w_bmod) * p.w_bs : 0);
     const int kmax = Ci * K;
     const int nch = (kmax + KC - 1) / KC;
     const int ch_beg = split * p.cps;
@@ -195,7 +200,7 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
             const int idx = tid + 256 * i;
             const int kk = idx / BM, m = idx % BM;
             const bool ok = k0 + kk < kmax && m0 + m < Co;
-            ra[i] = p.w[ok ? (int64_t)(k0 + kk) * Co + m0 + m : 0];
+            ra[i] = wb[ok ? (int64_t)(k0 + kk) * Co + m0 + m : 0];
         }
         const int c_lo = k0 / K;
         const int rows = min((k0 + KC - 1) / K, Ci - 1) - c_lo + 1;
@@ -490,7 +495,10 @@ int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds)
         RVC_CHECK_ARG(a->toff[i] >= 0, "conv64: negative tap offset");
         maxoff = a->toff[i] > maxoff ? a->toff[i] : maxoff;
     }
+    RVC_CHECK_ARG(a->w_bmod >= 0 && (a->w_bmod == 0 || a->w_bstride >= a->Ci * a->K * a->Co), "conv64: bad w_bmod / w_bstride");
     p.x = a->x; p.w = a->w; p.bias = a->bias; p.res = a->res;
+    p.w_bs = a->w_bstride;
+    p.w_bmod = a->w_bmod;
     p.y = a->y_f32 ? nullptr : (double*)a->y;
     p.yf = a->y_f32 ? (float*)a->y : nullptr;
     p.ws = nullptr;
@@ -615,6 +623,142 @@ __global__ void img_to_seq64_kernel(const double* img, double* x, int C, int64_t
     const int c = cf / W, f = cf - c * W;
     x[(int64_t)cf * H + t] = img[(int64_t)c * (H + 2) * (W + 2) + (t + 1) * (W + 2) + f + 1];
 }
+
+// ---------------------------------------------------------------- f64 Winograd F(4x4, 3x3) for the deep U-Net levels
+// The f64 matrix cores are power-bound chip-wide: the conv engine's MFMA-only loop runs ~36-39 TFLOP/s on every
+// RMVPE level whatever the tile, split or MFMA form, and per SIMD at near the nominal rate only while <= ~96 CUs
+// run (scripts/conv64_dbg.hip, round 4) -- so the lever is fewer MFMA FLOPs.  Winograd F(4x4, 3x3) (Lavin & Gray)
+// computes each 4 x 4 output tile from a 6 x 6 input tile with 36 products per (ci, co) instead of 144:
+//   Y = A^T [ sum_ci (G g G^T)[co][ci] (.) (B^T d B)[ci] ] A
+// as (1) an input transform U[36][Ci][P] (P = output tiles), (2) 36 GEMMs M[x] = V[x]^T U[x] on the conv engine
+// (K = 1, per-batch weights), (3) an output transform with the bias / activation / residual epilogue and the
+// zero border.  In f64 the transforms cost ~1e-14 relative (numpy: 1.1e-14 at 512 channels vs 1e-15 direct),
+// 7 orders below the f0 decisions' 1e-7 scale.  Used where the GEMMs dominate the transforms' HBM traffic
+// (2.25x the input and output): >= 64 channels in and out (rvc_wino64_use).
+namespace {
+// B^T d (6 -> 6) for one column / row
+RVC_DEV void wbt(const double* d, double* o) {
+    o[0] = 4.0 * d[0] - 5.0 * d[2] + d[4];
+    o[1] = -4.0 * d[1] - 4.0 * d[2] + d[3] + d[4];
+    o[2] = 4.0 * d[1] - 4.0 * d[2] - d[3] + d[4];
+    o[3] = -2.0 * d[1] - d[2] + 2.0 * d[3] + d[4];
+    o[4] = 2.0 * d[1] - d[2] - 2.0 * d[3] + d[4];
+    o[5] = 4.0 * d[1] - 5.0 * d[3] + d[5];
+}
+// A^T m (6 -> 4)
+RVC_DEV void wat(const double* m, double* o) {
+    o[0] = m[0] + m[1] + m[2] + m[3] + m[4];
+    o[1] = m[1] - m[2] + 2.0 * m[3] - 2.0 * m[4];
+    o[2] = m[1] + m[2] + 4.0 * m[3] + 4.0 * m[4];
+    o[3] = m[1] - m[2] + 8.0 * m[3] - 8.0 * m[4] + m[5];
+}
+// G g (3 -> 6)
+RVC_DEV void wg(const double* g, double* o) {
+    o[0] = g[0] / 4.0;
+    o[1] = -(g[0] + g[1] + g[2]) / 6.0;
+    o[2] = -(g[0] - g[1] + g[2]) / 6.0;
+    o[3] = g[0] / 24.0 + g[1] / 12.0 + g[2] / 6.0;
+    o[4] = g[0] / 24.0 - g[1] / 12.0 + g[2] / 6.0;
+    o[5] = g[2];
+}
+
+// KM weights w[(ci * 9 + dy * 3 + dx)][co] -> V[36][ci][co]
+__global__ void wino_w64_kernel(const double* w, double* v, int Ci, int Co) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Ci * Co) return;
+    const int ci = (int)(i / Co), co = (int)(i - (int64_t)ci * Co);
+    double g[3][3], t[6][3], col[3], o6[6];
+    for (int k = 0; k < 9; ++k) g[k / 3][k % 3] = w[(int64_t)(ci * 9 + k) * Co + co];
+    for (int c = 0; c < 3; ++c) {  // G g: columns
+        for (int r = 0; r < 3; ++r) col[r] = g[r][c];
+        wg(col, o6);
+        for (int r = 0; r < 6; ++r) t[r][c] = o6[r];
+    }
+    for (int r = 0; r < 6; ++r) {  // (G g) G^T: rows
+        wg(t[r], o6);
+        for (int c = 0; c < 6; ++c) v[((int64_t)(r * 6 + c) * Ci + ci) * Co + co] = o6[c];
+    }
+}
+
+// bordered x [B][C][(H+2)(W+2)] -> U [B][36][C][P], tile p = (th, tw): bordered rows 4 th .. 4 th + 5, cols 4 tw ..
+// 4 tw + 5 (past the bordered image: 0)
+__global__ void wino_in64_kernel(const double* x, double* u, int C, int H, int W, int TW, int P, int64_t x_bs,
+                                 int64_t u_bs) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y, b = blockIdx.z;
+    if (p >= P) return;
+    const int th = p / TW, tw = p - th * TW;
+    const int R = W + 2;
+    const double* xc = x + b * x_bs + (int64_t)c * (H + 2) * R;
+    double d[6][6], t[6][6], col[6], o6[6];
+    for (int r = 0; r < 6; ++r) {
+        const int y = 4 * th + r;
+        for (int q = 0; q < 6; ++q) {
+            const int xx = 4 * tw + q;
+            d[r][q] = (y < H + 2 && xx < R) ? xc[(int64_t)y * R + xx] : 0.0;
+        }
+    }
+    for (int q = 0; q < 6; ++q) {  // B^T d: columns
+        for (int r = 0; r < 6; ++r) col[r] = d[r][q];
+        wbt(col, o6);
+        for (int r = 0; r < 6; ++r) t[r][q] = o6[r];
+    }
+    double* ub = u + b * u_bs + (int64_t)c * P + p;
+    for (int r = 0; r < 6; ++r) {  // (B^T d) B: rows
+        wbt(t[r], o6);
+        for (int q = 0; q < 6; ++q) ub[(int64_t)(r * 6 + q) * C * P] = o6[q];
+    }
+}
+
+// M [B][36][Co][P] -> bordered y [B][Co][(H+2)(W+2)]: act(A^T m A + bias) (+ res), the tile's border cells 0
+__global__ void wino_out64_kernel(const double* m, double* y, float* yf, const double* bias, const double* res, int Co,
+                                  int H, int W, int TW, int P, int act, int64_t m_bs, int64_t y_bs, int64_t res_bs) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int co = blockIdx.y, b = blockIdx.z;
+    if (p >= P) return;
+    const int th = p / TW, tw = p - th * TW;
+    const int R = W + 2;
+    const double* mb = m + b * m_bs + (int64_t)co * P + p;
+    double mm[6][6], t[4][6], col[6], o4[4];
+    for (int r = 0; r < 6; ++r)
+        for (int q = 0; q < 6; ++q) mm[r][q] = mb[(int64_t)(r * 6 + q) * Co * P];
+    for (int q = 0; q < 6; ++q) {  // A^T m: columns
+        for (int r = 0; r < 6; ++r) col[r] = mm[r][q];
+        wat(col, o4);
+        for (int r = 0; r < 4; ++r) t[r][q] = o4[r];
+    }
+    const int64_t ybase = b * y_bs + (int64_t)co * (H + 2) * R;
+    const double bv = bias ? bias[co] : 0.0;
+    auto put = [&](int yy, int xx, double v) {
+        const int64_t o = ybase + (int64_t)yy * R + xx;
+        if (yf) yf[o] = (float)v;
+        else y[o] = v;
+    };
+    for (int r = 0; r < 4; ++r) {  // (A^T m) A: rows
+        wat(t[r], o4);
+        const int oy = 4 * th + r;
+        if (oy >= H) break;
+        for (int q = 0; q < 4; ++q) {
+            const int ox = 4 * tw + q;
+            if (ox >= W) break;
+            double v = act64(o4[q] + bv, act, 0.0);
+            if (res) v += res[b * res_bs + (int64_t)co * (H + 2) * R + (int64_t)(oy + 1) * R + ox + 1];
+            put(oy + 1, ox + 1, v);
+        }
+    }
+    // border cells beside this tile: top / bottom rows (with the corners) and left / right columns
+    const int x0 = 4 * tw + 1, x1 = min(4 * tw + 4, W), y0 = 4 * th + 1, y1 = min(4 * th + 4, H);
+    const int cx0 = tw == 0 ? 0 : x0, cx1 = tw == TW - 1 ? W + 1 : x1;
+    if (th == 0)
+        for (int xx = cx0; xx <= cx1; ++xx) put(0, xx, 0.0);
+    if (th == (H + 3) / 4 - 1)
+        for (int xx = cx0; xx <= cx1; ++xx) put(H + 1, xx, 0.0);
+    if (tw == 0)
+        for (int yy = y0; yy <= y1; ++yy) put(yy, 0, 0.0);
+    if (tw == TW - 1)
+        for (int yy = y0; yy <= y1; ++yy) put(yy, W + 1, 0.0);
+}
+}  // namespace
 
 // ---------------------------------------------------------------- f64 bidirectional GRU recurrence
 // rmvpe.hip's bigru_kernel in f64: 16 workgroups per direction, 16 hidden units each, W_hh rows in registers
@@ -809,6 +953,9 @@ extern "C" int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, 
         p.ws = (double*)ws;
     }
     hipStream_t s = (hipStream_t)stream;
+    // RVC_F64_ABLATE bit 1: no conv launches (timing ablation only: the output is then wrong)
+    static const int ablate = getenv("RVC_F64_ABLATE") ? atoi(getenv("RVC_F64_ABLATE")) : 0;
+    if (ablate & 2) return RVC_OK;
     launch64(tile, p, grid, lds, s);
     RVC_HIP(hipGetLastError());
     if (p.ksplit > 1) {
@@ -873,6 +1020,9 @@ extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double
     RVC_CHECK_ARG(B == 1 || (gi_bs >= 2 * 3 * G_H * T && y_bs >= 2 * G_H * T), "bigru64: batch strides too small");
     hipStream_t s = (hipStream_t)stream;
     const unsigned spin = rvc_bigru_set_spin_limit(0);
+    // RVC_F64_ABLATE bit 0: a 1-step recurrence (timing ablation only: the output is then wrong)
+    static const int ablate = getenv("RVC_F64_ABLATE") ? atoi(getenv("RVC_F64_ABLATE")) : 0;
+    if (ablate & 1) T = 1;
     for (int64_t b0 = 0; b0 < B; b0 += G_B_MAX) {
         const int64_t nb = B - b0 < G_B_MAX ? B - b0 : G_B_MAX;
         RVC_HIP(hipMemsetAsync(gran_ws, 0, (size_t)nb * RVC_BIGRU64_GRAN_BYTES, s));
@@ -880,5 +1030,91 @@ extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double
                            y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
         RVC_HIP(hipGetLastError());
     }
+    return RVC_OK;
+}
+
+// ---------------------------------------------------------------- Winograd F(4x4, 3x3) entry points
+extern "C" int rvc_wino64_use(int64_t Ci, int64_t Co) {
+    static const int on = getenv("RVC_RMVPE_WINO") ? atoi(getenv("RVC_RMVPE_WINO")) : 1;
+    return on && Ci >= 64 && Co >= 64;
+}
+
+extern "C" int rvc_wino64_weights(const double* w, double* v, int64_t Ci, int64_t Co, rvc_stream_t stream) {
+    RVC_CHECK_ARG(w && v && Ci > 0 && Co > 0 && Ci * Co * 36 < (1ll << 31), "wino64_weights: bad args");
+    hipLaunchKernelGGL(wino_w64_kernel, dim3(cdiv(Ci * Co, 256)), dim3(256), 0, (hipStream_t)stream, w, v, (int)Ci,
+                       (int)Co);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}
+
+namespace {
+struct Wino64 {
+    int64_t P, TW, u_n, m_n;  // tiles, tile columns, U / M doubles per image
+    rvc_conv64_args g;        // the 36-batch GEMM
+};
+
+int wino64_plan(const rvc_wino64_args* a, Wino64& w) {
+    RVC_CHECK_ARG(a && a->x && a->v && a->y && a->B > 0 && a->Ci > 0 && a->Co > 0 && a->H > 0 && a->W > 0,
+                  "wino64: bad args");
+    w.TW = (a->W + 3) / 4;
+    w.P = ((a->H + 3) / 4) * w.TW;
+    w.u_n = 36 * a->Ci * w.P;
+    w.m_n = 36 * a->Co * w.P;
+    RVC_CHECK_ARG(a->B * w.u_n < (1ll << 40) && w.P < (1 << 30), "wino64: too large");
+    memset(&w.g, 0, sizeof(w.g));
+    w.g.w = a->v;
+    w.g.B = a->B * 36;
+    w.g.Ci = a->Ci;
+    w.g.Co = a->Co;
+    w.g.Lin = w.P;
+    w.g.Lout = w.P;
+    w.g.K = 1;
+    w.g.out_act = RVC_ACT_NONE;
+    w.g.w_bstride = a->Ci * a->Co;
+    w.g.w_bmod = 36;
+    w.g.x = a->v;  // placeholders for planning (the workspace pointers are set at launch)
+    w.g.y = (void*)a->v;
+    return RVC_OK;
+}
+}  // namespace
+
+extern "C" int64_t rvc_wino64_workspace_bytes(const rvc_wino64_args* a) {
+    Wino64 w;
+    if (wino64_plan(a, w) != RVC_OK) return -1;
+    const int64_t g = rvc_conv64_workspace_bytes(&w.g);
+    if (g < 0) return -1;
+    return (a->B * (w.u_n + w.m_n)) * 8 + g;
+}
+
+extern "C" int rvc_wino64_conv(const rvc_wino64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
+    Wino64 w;
+    const int rc = wino64_plan(a, w);
+    if (rc != RVC_OK) return rc;
+    const int64_t g = rvc_conv64_workspace_bytes(&w.g);
+    RVC_CHECK_ARG(g >= 0, "wino64: GEMM plan failed");
+    const int64_t need = a->B * (w.u_n + w.m_n) * 8 + g;
+    RVC_CHECK_ARG(ws && ws_bytes >= need, "wino64: needs %lld B of workspace (got %lld)", (long long)need,
+                  (long long)ws_bytes);
+    double* u = (double*)ws;
+    double* m = u + a->B * w.u_n;
+    void* gws = g ? (void*)(m + a->B * w.m_n) : nullptr;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t img_i = a->Ci * (a->H + 2) * (a->W + 2), img_o = a->Co * (a->H + 2) * (a->W + 2);
+    const int64_t x_bs = a->x_bstride ? a->x_bstride : img_i, y_bs = a->y_bstride ? a->y_bstride : img_o;
+    const int64_t r_bs = a->res_bstride ? a->res_bstride : img_o;
+    RVC_CHECK_ARG(a->B < 65536 && a->Ci < 65536 && a->Co < 65536, "wino64: too many images / channels");
+    hipLaunchKernelGGL(wino_in64_kernel, dim3(cdiv(w.P, 64), (unsigned)a->Ci, (unsigned)a->B), dim3(64), 0, s, a->x, u,
+                       (int)a->Ci, (int)a->H, (int)a->W, (int)w.TW, (int)w.P, x_bs, w.u_n);
+    RVC_HIP(hipGetLastError());
+    w.g.x = u;
+    w.g.y = m;
+    w.g.x_bstride = a->Ci * w.P;
+    w.g.y_bstride = a->Co * w.P;
+    const int rg = rvc_conv64(&w.g, gws, g, stream);
+    if (rg != RVC_OK) return rg;
+    hipLaunchKernelGGL(wino_out64_kernel, dim3(cdiv(w.P, 64), (unsigned)a->Co, (unsigned)a->B), dim3(64), 0, s, m,
+                       a->y_f32 ? nullptr : (double*)a->y, a->y_f32 ? (float*)a->y : nullptr, a->bias, a->res,
+                       (int)a->Co, (int)a->H, (int)a->W, (int)w.TW, (int)w.P, a->out_act, w.m_n, y_bs, r_bs);
+    RVC_HIP(hipGetLastError());
     return RVC_OK;
 }

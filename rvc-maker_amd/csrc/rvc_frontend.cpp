@@ -22,6 +22,7 @@ struct W64 {
     int K = 0;
     double* w = nullptr;
     double* b = nullptr;
+    double* v = nullptr;  // the Winograd F(4x4, 3x3) weights [36][Ci][Co] (rvc_wino64_use), else null
 };
 
 // ConvBlockRes (RMVPE.py:11-44) with BatchNorm folded: conv.0 -> ReLU, conv.3 -> ReLU + shortcut
@@ -223,6 +224,12 @@ int make_w64(Rmvpe& M, const HostT& w, int64_t Co, int64_t Ci, int K, const std:
     if (bias) {
         MCHECK((int64_t)bias->size() == Co, "rvc_load_rmvpe: bias size %zu != %lld", bias->size(), (long long)Co);
         MTRY(upload64(M, *bias, &cw.b));
+    }
+    // the deep levels' 3x3 convs as Winograd F(4x4, 3x3), the same rule and transform as rmvpe.py's _Conv2d
+    if (K == 9 && rvc_wino64_use(Ci, Co)) {
+        MTRY(dev_alloc(M, (size_t)36 * Ci * Co * 8, (void**)&cw.v));
+        MTRY(rvc_wino64_weights(cw.w, cw.v, Ci, Co, nullptr));
+        MHIP(hipStreamSynchronize(nullptr));
     }
     return RVC_OK;
 }
@@ -493,6 +500,25 @@ int conv64(Rmvpe& M, const W64& cw, const double* x, int64_t Lin, void* y, const
 // _Conv2d.__call__ (f64) on bordered [C][H+2][W+2] images
 int conv2d64(Rmvpe& M, const W64& cw, const double* x, int64_t H, int64_t W, double* out, int out_act,
              const double* res, hipStream_t s) {
+    if (cw.v) {
+        rvc_wino64_args a;
+        memset(&a, 0, sizeof(a));
+        a.x = x;
+        a.v = cw.v;
+        a.bias = cw.b;
+        a.res = res;
+        a.y = out;
+        a.B = 1;
+        a.Ci = cw.Ci;
+        a.Co = cw.Co;
+        a.H = H;
+        a.W = W;
+        a.out_act = out_act;
+        const int64_t need = rvc_wino64_workspace_bytes(&a);
+        if (need < 0) return RVC_EINVAL;
+        MTRY(ensure_ws(M, need, s));
+        return rvc_wino64_conv(&a, M.ws, need, s);
+    }
     const int64_t wrap = W + 2, L = (H + 2) * wrap;
     C64Opts o;
     o.Lout = L;

@@ -36,7 +36,16 @@ class Conv64Args(ctypes.Structure):
                 ("B", c_int64), ("Ci", c_int64), ("Co", c_int64), ("Lin", c_int64), ("Lout", c_int64),
                 ("x_bstride", c_int64), ("y_bstride", c_int64), ("res_bstride", c_int64),
                 ("K", c_int), ("pad", c_int), ("out_act", c_int), ("y_f32", c_int), ("out_slope", c_double),
-                ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16)]
+                ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16),
+                ("w_bstride", c_int64), ("w_bmod", c_int), ("_pad0", c_int)]
+
+
+class Wino64Args(ctypes.Structure):
+    """rvc_wino64_args: the f64 Winograd F(4x4, 3x3) conv of RMVPE's deep levels (rmvpe64.hip)."""
+    _fields_ = [("x", c_void_p), ("v", c_void_p), ("bias", c_void_p), ("res", c_void_p), ("y", c_void_p),
+                ("B", c_int64), ("Ci", c_int64), ("Co", c_int64), ("H", c_int64), ("W", c_int64),
+                ("x_bstride", c_int64), ("y_bstride", c_int64), ("res_bstride", c_int64),
+                ("out_act", c_int), ("y_f32", c_int)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -159,6 +168,10 @@ SIGNATURES = {
     "rvc_conv64": [POINTER(Conv64Args), c_void_p, c_int64, c_void_p],
     "rvc_conv64_workspace_bytes": [POINTER(Conv64Args)],
     "rvc_conv64_plan": [POINTER(Conv64Args), POINTER(c_int)],
+    "rvc_wino64_use": [c_int64, c_int64],
+    "rvc_wino64_weights": [c_void_p, c_void_p, c_int64, c_int64, c_void_p],
+    "rvc_wino64_workspace_bytes": [POINTER(Wino64Args)],
+    "rvc_wino64_conv": [POINTER(Wino64Args), c_void_p, c_int64, c_void_p],
     "rvc_conv64_set_plan": [c_int, c_int, c_int],
     "rvc_stft_mag64": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int, c_int, c_int64, c_int64,
                        c_void_p],
@@ -230,7 +243,7 @@ SIGNATURES = {
                         c_void_p, c_void_p],
 }
 _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_int64, "rvc_conv1d_x6_bytes": c_int64,
-             "rvc_conv64_workspace_bytes": c_int64,
+             "rvc_conv64_workspace_bytes": c_int64, "rvc_wino64_workspace_bytes": c_int64,
              "rvc_conv1d_f16_bytes": c_int64, "rvc_pm_frames": c_int64, "rvc_pm_work_bytes": c_int64,
              "rvc_filtfilt_work_bytes": c_int64, "rvc_attention_workspace_bytes": c_int64,
              "rvc_ivf_coarse_ws_bytes": c_int64, "rvc_crepe_decode_ws_bytes": c_int64,

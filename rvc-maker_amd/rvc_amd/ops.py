@@ -623,6 +623,49 @@ def conv64(x, w, Ci, Co, K, *, bias=None, pad=0, Lout=None, out=None, res=None, 
     return out
 
 
+def wino64_use(Ci, Co):
+    """Whether the f64 RMVPE takes the Winograd F(4x4, 3x3) form for a Ci -> Co 3x3 conv (rvc_wino64_use)."""
+    return bool(_lib.load().rvc_wino64_use(Ci, Co))
+
+
+def wino64_weights(w_km, Ci, Co):
+    """KM f64 3x3 weights [Ci*9][Co] -> the 36 Winograd weight matrices [36][Ci][Co] (rvc_wino64_weights)."""
+    v = torch.empty(36, Ci, Co, dtype=torch.float64, device=w_km.device)
+    check(_lib.load().rvc_wino64_weights(_pd(w_km), _pd(v), Ci, Co, _stream()), "wino64_weights")
+    return v
+
+
+def wino64(x, v, Ci, Co, H, W, *, bias=None, res=None, out=None, out_act=ACT_NONE, B=1, x_bstride=0, y_bstride=0,
+           res_bstride=0, out_f32=False):
+    """The f64 Winograd F(4x4, 3x3) conv (rvc_wino64_conv) on bordered [Ci][H+2][W+2] images (or B of them with
+    batch strides): y = act(conv3x3(x) + bias) (+ res), border cells 0."""
+    L = (H + 2) * (W + 2)
+    ydt = torch.float32 if out_f32 else torch.float64
+    if out is None:
+        out = torch.empty(*((B,) if B > 1 else ()), Co, H + 2, W + 2, device=x.device, dtype=ydt)
+    elif out.dtype != ydt or _room(out) < (B - 1) * (y_bstride or Co * L) + Co * L:
+        raise ValueError("wino64: output buffer too small or of the wrong dtype")
+    if _room(x) < (B - 1) * (x_bstride or Ci * L) + Ci * L or x.dtype != torch.float64:
+        raise ValueError("wino64: f64 input of [B][Ci][H+2][W+2] expected")
+    if res is not None and _room(res) < (B - 1) * (res_bstride or Co * L) + Co * L:
+        raise ValueError("wino64: residual too small")
+    if v.numel() < 36 * Ci * Co or v.dtype != torch.float64:
+        raise ValueError("wino64: f64 weights [36][Ci][Co] expected")
+    a = _lib.Wino64Args()
+    a.x, a.v, a.bias, a.res = _pd(x), _pd(v), _pd(bias), _pd(res)
+    a.y = _p(out) if out_f32 else _pd(out)
+    a.B, a.Ci, a.Co, a.H, a.W = B, Ci, Co, H, W
+    a.x_bstride, a.y_bstride, a.res_bstride = x_bstride, y_bstride, res_bstride
+    a.out_act, a.y_f32 = out_act, int(bool(out_f32))
+    lib = _lib.load()
+    need = lib.rvc_wino64_workspace_bytes(ctypes.byref(a))
+    if need < 0:
+        raise RuntimeError(f"rvc_amd: wino64 plan failed: {lib.rvc_last_error().decode()}")
+    ws = _workspace(out.device, need, "w64")
+    check(lib.rvc_wino64_conv(ctypes.byref(a), _p(ws), need, _stream()), "wino64")
+    return out
+
+
 def conv64_set_plan(tile=-1, ksplit=-1, compact=-1):
     """Force the f64 conv planner's choice (rvc_conv64_set_plan; -1 = the planner's): sweeps and tests."""
     check(_lib.load().rvc_conv64_set_plan(tile, ksplit, compact), "conv64_set_plan")

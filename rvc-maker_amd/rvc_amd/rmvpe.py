@@ -69,9 +69,13 @@ class _Conv2d:
     def __init__(self, w, b, device, f64=True):
         Co, Ci, kh, kw = w.shape
         self.Co, self.Ci, self.k, self.f64 = Co, Ci, kh, f64
+        self.v = None
         if f64:
             self.w = pack_km(w.reshape(Co, Ci, kh * kw).double()).to(device)
             self.b = b.double().to(device) if b is not None else None
+            # the deep levels' 3x3 convs as Winograd F(4x4, 3x3) (rmvpe64.hip: 4x fewer f64 MFMA FLOPs)
+            if kh == 3 and ops.wino64_use(Ci, Co):
+                self.v = ops.wino64_weights(self.w, Ci, Co)
         else:
             self.w = pack_km(w.reshape(Co, Ci, kh * kw).float()).to(device)
             self.b = b.float().to(device) if b is not None else None
@@ -86,6 +90,8 @@ class _Conv2d:
             pad = wrap + 1
         else:
             toff, pad = [0], 0
+        if self.v is not None:
+            return ops.wino64(x, self.v, self.Ci, self.Co, H, W, bias=self.b, out=out, **_batch_kw(x, out, kw), **kw)
         if self.f64:
             return ops.conv64(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L,
                               out=out, toff=toff, wrap=wrap, **_batch_kw(x, out, kw), **kw)

@@ -321,6 +321,36 @@ def test_conv64_every_plan(ops, Ci, Co, H, W, B, k):
     assert k == 1 or max(p[1] for p in seen) >= 3, seen
 
 
+@pytest.mark.parametrize("Ci,Co,H,W,B", [(64, 64, 12, 8, 1), (128, 96, 10, 4, 2), (72, 64, 9, 5, 1), (512, 512, 94, 4, 1)])
+def test_wino64_conv(ops, Ci, Co, H, W, B):
+    """The f64 Winograd F(4x4, 3x3) conv of RMVPE's deep levels (rmvpe64.hip): input transform, 36 GEMMs on the
+    conv engine with per-batch weights, output transform with bias, ReLU, residual and the zero border -- against
+    F.conv2d in f64 (1e-12 relative: the transforms cost ~1e-14) over a NaN-filled output, ragged tiles (H, W not
+    multiples of 4) and batch strides included."""
+    g = gen(13)
+    w = torch.randn(Co, Ci, 3, 3, generator=g, dtype=torch.float64) / math.sqrt(9 * Ci)
+    b = torch.randn(Co, generator=g, dtype=torch.float64) * 0.1
+    x = torch.randn(B, Ci, H, W, generator=g, dtype=torch.float64)
+    r = torch.randn(B, Co, H, W, generator=g, dtype=torch.float64)
+    ref = torch.relu(F.conv2d(x, w, b, padding=1)) + r
+    wkm = ops.pack_km(w.reshape(Co, Ci, 9)).to(DEV)
+    v = ops.wino64_weights(wkm, Ci, Co)
+    xb = F.pad(x, (1, 1, 1, 1)).to(DEV).contiguous()
+    rb = F.pad(r, (1, 1, 1, 1)).to(DEV).contiguous()
+    L = (H + 2) * (W + 2)
+    out = torch.full((B, Co, H + 2, W + 2), float("nan"), device=DEV, dtype=torch.float64)
+    ops.wino64(xb, v, Ci, Co, H, W, bias=b.to(DEV), res=rb, out=out, out_act=ops.ACT_RELU, B=B, x_bstride=Ci * L,
+               y_bstride=Co * L, res_bstride=Co * L)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    err = (o[:, :, 1:-1, 1:-1] - ref).abs().max().item()
+    assert err <= 1e-12 * max(1.0, ref.abs().max().item()), err
+    border = torch.ones(H + 2, W + 2, dtype=torch.bool)
+    border[1:-1, 1:-1] = False
+    assert torch.equal(o[:, :, border], torch.zeros(B, Co, int(border.sum()), dtype=o.dtype))
+    assert ops.wino64_use(Ci, Co)
+
+
 F16_CASES = [c for c in CONV_CASES if c[6] == 1 and c[2] <= 64 and (c[3] == 1 or (c[3] == 2 and c[0] >= 32))]
 
 
