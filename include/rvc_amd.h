@@ -288,16 +288,18 @@ typedef struct rvc_conv64_args {
 /* split-K workspace (bytes; 0 = none, -1 = bad args), as rvc_conv1d_workspace_bytes */
 int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a);
 /* the planner's choice for a (diagnostics): out[0] tile (0..7: 16x512, 16x256, 32x256, 32x128, 64x128, 64x64,
- * 128x128, 128x64 with 16-deep k chunks; 8..12: 16x256, 32x128, 64x128, 64x64, 128x64 with 32-deep), out[1] split-K, out[2] compact form (wrap > 0: the H x W interior cells as the GEMM's
+ * 128x128, 128x64 with 16-deep k chunks; 8..12: 16x256, 32x128, 64x128, 64x64, 128x64 with 32-deep; 13, 14: 128x16
+ * with 16- / 32-deep), out[1] split-K, out[2] compact form (wrap > 0: the H x W interior cells as the GEMM's
  * columns instead of the bordered image), out[3] blocks of the conv launch */
 int rvc_conv64_plan(const rvc_conv64_args* a, int* out);
-/* force the planner (process-wide; sweeps and tests): tile -1..12, ksplit -1..32, compact -1..1 (-1 = planner's) */
+/* force the planner (process-wide; sweeps and tests): tile -1..14, ksplit -1..32, compact -1..1 (-1 = planner's) */
 int rvc_conv64_set_plan(int tile, int ksplit, int compact);
 int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* Winograd F(4x4, 3x3) f64 conv for RMVPE's deep levels (3x3 pad 1 on bordered [C][H+2][W+2] images, as
  * conv64 with wrap): y = act(conv(x) + bias) (+ res), border cells 0.  v = rvc_wino64_weights(KM w [Ci*9][Co])
- * = the 36 transformed weight matrices [36][Ci][Co] (G g G^T).  rvc_wino64_use(Ci, Co): whether the f64 RMVPE
- * takes this form for a Ci -> Co conv (>= 64 channels each; RVC_RMVPE_WINO=0 turns it off). */
+ * = the 36 transformed weight matrices [36][Ci][Co] (G g G^T).  rvc_wino64_use(Ci, Co, H, W): whether the f64
+ * RMVPE takes this form for a Ci -> Co conv on an H x W image (>= 64 channels each and >= 90 4x4 output tiles,
+ * RVC_RMVPE_WINO_MINP; H or W <= 0: the channel rule alone, whether to prepare v; RVC_RMVPE_WINO=0: never). */
 typedef struct rvc_wino64_args {
     const double* x;
     const double* v;
@@ -308,7 +310,7 @@ typedef struct rvc_wino64_args {
     int64_t x_bstride, y_bstride, res_bstride;
     int out_act, y_f32;
 } rvc_wino64_args;
-int rvc_wino64_use(int64_t Ci, int64_t Co);
+int rvc_wino64_use(int64_t Ci, int64_t Co, int64_t H, int64_t W);
 int rvc_wino64_weights(const double* w, double* v, int64_t Ci, int64_t Co, rvc_stream_t stream);
 int64_t rvc_wino64_workspace_bytes(const rvc_wino64_args* a);
 int rvc_wino64_conv(const rvc_wino64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);

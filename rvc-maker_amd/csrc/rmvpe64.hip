@@ -374,7 +374,7 @@ struct Cfg64 {
 // the tiles the planner chooses from (BM x BN = 16 FM WM x 16 FN WN, k chunk KC): the 32-deep chunks halve the
 // barriers and staging rounds per k and pay where the tile's registers and LDS leave room (scripts/conv64_dbg.hip:
 // 32 x 128 tiles 15-20 % faster, 32 x 256 ones slower)
-constexpr int N_TILES64 = 13;
+constexpr int N_TILES64 = 15;
 constexpr Cfg64 kTiles64[N_TILES64] = {
     {1, 8, 1, 4, 16},  // 0: 16 x 512
     {1, 4, 1, 4, 16},  // 1: 16 x 256
@@ -389,6 +389,8 @@ constexpr Cfg64 kTiles64[N_TILES64] = {
     {2, 4, 2, 2, 32},  // 10: 64 x 128, KC 32
     {2, 2, 2, 2, 32},  // 11: 64 x 64, KC 32
     {4, 2, 2, 2, 32},  // 12: 128 x 64, KC 32
+    {2, 1, 4, 1, 16},  // 13: 128 x 16 (the Winograd GEMMs of small images: a few dozen columns)
+    {2, 1, 4, 1, 32},  // 14: 128 x 16, KC 32
 };
 
 // the compact form of the 128 x 128 tile spills (its per-lane column offsets on top of 255 VGPRs): not built;
@@ -634,7 +636,9 @@ __global__ void img_to_seq64_kernel(const double* img, double* x, int C, int64_t
 // (K = 1, per-batch weights), (3) an output transform with the bias / activation / residual epilogue and the
 // zero border.  In f64 the transforms cost ~1e-14 relative (numpy: 1.1e-14 at 512 channels vs 1e-15 direct),
 // 7 orders below the f0 decisions' 1e-7 scale.  Used where the GEMMs dominate the transforms' HBM traffic
-// (2.25x the input and output): >= 64 channels in and out (rvc_wino64_use).
+// (2.25x the input and output) and are wide enough: >= 64 channels in and out and >= 90 output tiles
+// (rvc_wino64_use).  Measured (one box, RMVPE alone / the bench's clip stream): every >= 64-channel conv 15.64 ms /
+// 925 xRT, >= 90 tiles (levels 2-4, not the 94 x 4 middle) 14.70 ms / 929, >= 300 15.05 / 926, none 15.52 / 907.
 namespace {
 // B^T d (6 -> 6) for one column / row
 RVC_DEV void wbt(const double* d, double* o) {
@@ -1034,9 +1038,12 @@ extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double
 }
 
 // ---------------------------------------------------------------- Winograd F(4x4, 3x3) entry points
-extern "C" int rvc_wino64_use(int64_t Ci, int64_t Co) {
+extern "C" int rvc_wino64_use(int64_t Ci, int64_t Co, int64_t H, int64_t W) {
     static const int on = getenv("RVC_RMVPE_WINO") ? atoi(getenv("RVC_RMVPE_WINO")) : 1;
-    return on && Ci >= 64 && Co >= 64;
+    // images of fewer output tiles than this run direct (the 36 GEMMs get too narrow; RVC_RMVPE_WINO_MINP)
+    static const int64_t minp = getenv("RVC_RMVPE_WINO_MINP") ? atoll(getenv("RVC_RMVPE_WINO_MINP")) : 90;
+    if (!on || Ci < 64 || Co < 64) return 0;
+    return H <= 0 || W <= 0 || ((H + 3) / 4) * ((W + 3) / 4) >= minp;
 }
 
 extern "C" int rvc_wino64_weights(const double* w, double* v, int64_t Ci, int64_t Co, rvc_stream_t stream) {

@@ -226,7 +226,7 @@ int make_w64(Rmvpe& M, const HostT& w, int64_t Co, int64_t Ci, int K, const std:
         MTRY(upload64(M, *bias, &cw.b));
     }
     // the deep levels' 3x3 convs as Winograd F(4x4, 3x3), the same rule and transform as rmvpe.py's _Conv2d
-    if (K == 9 && rvc_wino64_use(Ci, Co)) {
+    if (K == 9 && rvc_wino64_use(Ci, Co, 0, 0)) {
         MTRY(dev_alloc(M, (size_t)36 * Ci * Co * 8, (void**)&cw.v));
         MTRY(rvc_wino64_weights(cw.w, cw.v, Ci, Co, nullptr));
         MHIP(hipStreamSynchronize(nullptr));
@@ -500,7 +500,7 @@ int conv64(Rmvpe& M, const W64& cw, const double* x, int64_t Lin, void* y, const
 // _Conv2d.__call__ (f64) on bordered [C][H+2][W+2] images
 int conv2d64(Rmvpe& M, const W64& cw, const double* x, int64_t H, int64_t W, double* out, int out_act,
              const double* res, hipStream_t s) {
-    if (cw.v) {
+    if (cw.v && rvc_wino64_use(cw.Ci, cw.Co, H, W)) {
         rvc_wino64_args a;
         memset(&a, 0, sizeof(a));
         a.x = x;

@@ -168,7 +168,7 @@ SIGNATURES = {
     "rvc_conv64": [POINTER(Conv64Args), c_void_p, c_int64, c_void_p],
     "rvc_conv64_workspace_bytes": [POINTER(Conv64Args)],
     "rvc_conv64_plan": [POINTER(Conv64Args), POINTER(c_int)],
-    "rvc_wino64_use": [c_int64, c_int64],
+    "rvc_wino64_use": [c_int64, c_int64, c_int64, c_int64],
     "rvc_wino64_weights": [c_void_p, c_void_p, c_int64, c_int64, c_void_p],
     "rvc_wino64_workspace_bytes": [POINTER(Wino64Args)],
     "rvc_wino64_conv": [POINTER(Wino64Args), c_void_p, c_int64, c_void_p],

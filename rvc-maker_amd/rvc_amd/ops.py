@@ -623,9 +623,10 @@ def conv64(x, w, Ci, Co, K, *, bias=None, pad=0, Lout=None, out=None, res=None, 
     return out
 
 
-def wino64_use(Ci, Co):
-    """Whether the f64 RMVPE takes the Winograd F(4x4, 3x3) form for a Ci -> Co 3x3 conv (rvc_wino64_use)."""
-    return bool(_lib.load().rvc_wino64_use(Ci, Co))
+def wino64_use(Ci, Co, H=0, W=0):
+    """Whether the f64 RMVPE takes the Winograd F(4x4, 3x3) form for a Ci -> Co 3x3 conv on an H x W image
+    (rvc_wino64_use; H = W = 0: the channel rule alone, i.e. whether to prepare the transformed weights)."""
+    return bool(_lib.load().rvc_wino64_use(Ci, Co, H, W))
 
 
 def wino64_weights(w_km, Ci, Co):

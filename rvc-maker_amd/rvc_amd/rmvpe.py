@@ -90,7 +90,7 @@ class _Conv2d:
             pad = wrap + 1
         else:
             toff, pad = [0], 0
-        if self.v is not None:
+        if self.v is not None and ops.wino64_use(self.Ci, self.Co, H, W):
             return ops.wino64(x, self.v, self.Ci, self.Co, H, W, bias=self.b, out=out, **_batch_kw(x, out, kw), **kw)
         if self.f64:
             return ops.conv64(x, self.w, self.Ci, self.Co, self.k * self.k, bias=self.b, pad=pad, Lin=L, Lout=L,
