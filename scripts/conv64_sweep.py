@@ -19,6 +19,10 @@ TILES = ["16x512", "16x256", "32x256", "32x128", "64x128", "64x64", "128x128", "
 # (Ci, Co, H, W): one 3x3 conv per U-Net level (every level's convs are 1.77 GFLOP), the encoder's first conv
 SHAPES = [(16, 16, 3008, 128), (32, 32, 1504, 64), (64, 64, 752, 32), (128, 128, 376, 16), (256, 256, 188, 8),
           (512, 512, 94, 4), (256, 512, 94, 4), (1, 16, 3008, 128)]
+# --direct: the convs the f64 RMVPE still runs direct on a 30 s clip after filtfilt / t_pad (mel image 3232 x 128;
+# levels >= 2 of >= 64 channels go Winograd): encoder, decoder (concat input) and the 512-channel middle
+SHAPES_DIRECT = [(1, 16, 3232, 128), (16, 16, 3232, 128), (32, 16, 3232, 128), (16, 32, 1616, 64), (32, 32, 1616, 64),
+                 (64, 32, 1616, 64), (32, 64, 808, 32), (512, 512, 101, 4), (256, 512, 101, 4), (512, 256, 101, 4)]
 
 
 def run(x, w, b, Ci, Co, H, W, out, reps):
@@ -44,7 +48,7 @@ def main():
     planner_only = "--planner-only" in sys.argv
     torch.manual_seed(0)
     rows = []
-    for Ci, Co, H, W in SHAPES:
+    for Ci, Co, H, W in (SHAPES_DIRECT if "--direct" in sys.argv else SHAPES):
         L = (H + 2) * (W + 2)
         x = torch.zeros(Ci, H + 2, W + 2, dtype=torch.float64, device="cuda")
         x[:, 1:-1, 1:-1] = torch.randn(Ci, H, W, dtype=torch.float64, device="cuda")
