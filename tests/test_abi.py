@@ -99,7 +99,9 @@ def test_struct_layouts_match_c_compiler(tmp_path):
               "rvc_synth_cfg": [f[0] for f in _lib.SynthCfg._fields_],
               "rvc_contentvec_cfg": [f[0] for f in _lib.ContentVecCfg._fields_],
               "rvc_vc_args": [f[0] for f in _lib.VcArgs._fields_],
-              "rvc_ivf_index": [f[0] for f in _lib.IvfIndex._fields_]}
+              "rvc_ivf_index": [f[0] for f in _lib.IvfIndex._fields_],
+              "rvc_conv64_args": [f[0] for f in _lib.Conv64Args._fields_],
+              "rvc_wino64_args": [f[0] for f in _lib.Wino64Args._fields_]}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rvc_amd.h"', "int main(void){"]
     for st, fs in fields.items():
         lines.append(f'printf("%zu\\n", sizeof({st}));')
@@ -112,7 +114,8 @@ def test_struct_layouts_match_c_compiler(tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = []
-    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs, _lib.Param, _lib.SynthCfg, _lib.ContentVecCfg, _lib.VcArgs, _lib.IvfIndex):
+    for cls in (_lib.Conv1dArgs, _lib.AttnArgs, _lib.F0Post, _lib.DenoiseArgs, _lib.Param, _lib.SynthCfg, _lib.ContentVecCfg,
+                _lib.VcArgs, _lib.IvfIndex, _lib.Conv64Args, _lib.Wino64Args):
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f[0]).offset for f in cls._fields_]
     assert got == want
