@@ -684,83 +684,276 @@ __global__ void wino_w64_kernel(const double* w, double* v, int Ci, int Co) {
     }
 }
 
+// Both transforms stage a band of RT tile rows through LDS (one block: 256 threads, one channel, RT tile rows, all
+// tile columns): the image rows are read / written whole and coalesced, each thread transforms tiles out of LDS.
+// RT = the tile rows that make ~256 tiles (rows of W / 4 tiles each).
+inline int wino_rt(int W) {
+    const int tw = (W + 3) / 4;
+    return tw >= 256 ? 1 : 256 / tw;
+}
+
 // bordered x [B][C][(H+2)(W+2)] -> U [B][36][C][P], tile p = (th, tw): bordered rows 4 th .. 4 th + 5, cols 4 tw ..
 // 4 tw + 5 (past the bordered image: 0)
-__global__ void wino_in64_kernel(const double* x, double* u, int C, int H, int W, int TW, int P, int64_t x_bs,
-                                 int64_t u_bs) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void wino_in64_kernel(const double* x, double* u, int C, int H, int W, int TW,
+                                                        int P, int RT, int64_t x_bs, int64_t u_bs) {
+    extern __shared__ double band[];  // [4 RT + 2][W + 2]
     const int c = blockIdx.y, b = blockIdx.z;
-    if (p >= P) return;
-    const int th = p / TW, tw = p - th * TW;
+    const int th0 = blockIdx.x * RT;
+    const int TH = (H + 3) / 4;
+    const int nth = min(RT, TH - th0);
     const int R = W + 2;
+    const int rows = 4 * nth + 2;
     const double* xc = x + b * x_bs + (int64_t)c * (H + 2) * R;
-    double d[6][6], t[6][6], col[6], o6[6];
-    for (int r = 0; r < 6; ++r) {
-        const int y = 4 * th + r;
-        for (int q = 0; q < 6; ++q) {
-            const int xx = 4 * tw + q;
-            d[r][q] = (y < H + 2 && xx < R) ? xc[(int64_t)y * R + xx] : 0.0;
+    for (int i = threadIdx.x; i < rows * R; i += 256) {
+        const int r = i / R, q = i - r * R;
+        const int y = 4 * th0 + r;
+        band[i] = y < H + 2 ? xc[(int64_t)y * R + q] : 0.0;
+    }
+    __syncthreads();
+    double* ub = u + b * u_bs + (int64_t)c * P;
+    for (int t = threadIdx.x; t < nth * TW; t += 256) {
+        const int tr = t / TW, tw = t - tr * TW;
+        double d[6][6], tt[6][6], col[6], o6[6];
+        for (int r = 0; r < 6; ++r)
+            for (int q = 0; q < 6; ++q) {
+                const int xx = 4 * tw + q;
+                d[r][q] = xx < R ? band[(4 * tr + r) * R + xx] : 0.0;
+            }
+        for (int q = 0; q < 6; ++q) {  // B^T d: columns
+            for (int r = 0; r < 6; ++r) col[r] = d[r][q];
+            wbt(col, o6);
+            for (int r = 0; r < 6; ++r) tt[r][q] = o6[r];
         }
-    }
-    for (int q = 0; q < 6; ++q) {  // B^T d: columns
-        for (int r = 0; r < 6; ++r) col[r] = d[r][q];
-        wbt(col, o6);
-        for (int r = 0; r < 6; ++r) t[r][q] = o6[r];
-    }
-    double* ub = u + b * u_bs + (int64_t)c * P + p;
-    for (int r = 0; r < 6; ++r) {  // (B^T d) B: rows
-        wbt(t[r], o6);
-        for (int q = 0; q < 6; ++q) ub[(int64_t)(r * 6 + q) * C * P] = o6[q];
+        const int p = (th0 + tr) * TW + tw;
+        for (int r = 0; r < 6; ++r) {  // (B^T d) B: rows
+            wbt(tt[r], o6);
+            for (int q = 0; q < 6; ++q) ub[(int64_t)(r * 6 + q) * C * P + p] = o6[q];
+        }
     }
 }
 
-// M [B][36][Co][P] -> bordered y [B][Co][(H+2)(W+2)]: act(A^T m A + bias) (+ res), the tile's border cells 0
-__global__ void wino_out64_kernel(const double* m, double* y, float* yf, const double* bias, const double* res, int Co,
-                                  int H, int W, int TW, int P, int act, int64_t m_bs, int64_t y_bs, int64_t res_bs) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// M [B][36][Co][P] -> bordered y [B][Co][(H+2)(W+2)]: act(A^T m A + bias) (+ res), the band's border cells 0
+__global__ __launch_bounds__(256) void wino_out64_kernel(const double* m, double* y, float* yf, const double* bias,
+                                                         const double* res, int Co, int H, int W, int TW, int P, int RT,
+                                                         int act, int64_t m_bs, int64_t y_bs, int64_t res_bs) {
+    extern __shared__ double band[];  // [4 RT][W] transformed outputs
     const int co = blockIdx.y, b = blockIdx.z;
-    if (p >= P) return;
-    const int th = p / TW, tw = p - th * TW;
+    const int th0 = blockIdx.x * RT;
+    const int TH = (H + 3) / 4;
+    const int nth = min(RT, TH - th0);
     const int R = W + 2;
-    const double* mb = m + b * m_bs + (int64_t)co * P + p;
-    double mm[6][6], t[4][6], col[6], o4[4];
-    for (int r = 0; r < 6; ++r)
-        for (int q = 0; q < 6; ++q) mm[r][q] = mb[(int64_t)(r * 6 + q) * Co * P];
-    for (int q = 0; q < 6; ++q) {  // A^T m: columns
-        for (int r = 0; r < 6; ++r) col[r] = mm[r][q];
-        wat(col, o4);
-        for (int r = 0; r < 4; ++r) t[r][q] = o4[r];
-    }
-    const int64_t ybase = b * y_bs + (int64_t)co * (H + 2) * R;
-    const double bv = bias ? bias[co] : 0.0;
-    auto put = [&](int yy, int xx, double v) {
-        const int64_t o = ybase + (int64_t)yy * R + xx;
-        if (yf) yf[o] = (float)v;
-        else y[o] = v;
-    };
-    for (int r = 0; r < 4; ++r) {  // (A^T m) A: rows
-        wat(t[r], o4);
-        const int oy = 4 * th + r;
-        if (oy >= H) break;
-        for (int q = 0; q < 4; ++q) {
-            const int ox = 4 * tw + q;
-            if (ox >= W) break;
-            double v = act64(o4[q] + bv, act, 0.0);
-            if (res) v += res[b * res_bs + (int64_t)co * (H + 2) * R + (int64_t)(oy + 1) * R + ox + 1];
-            put(oy + 1, ox + 1, v);
+    const int W4 = 4 * TW;
+    const double* mb = m + b * m_bs + (int64_t)co * P;
+    for (int t = threadIdx.x; t < nth * TW; t += 256) {
+        const int tr = t / TW, tw = t - tr * TW;
+        const int p = (th0 + tr) * TW + tw;
+        double mm[6][6], tt[4][6], col[6], o4[4];
+        for (int r = 0; r < 6; ++r)
+            for (int q = 0; q < 6; ++q) mm[r][q] = mb[(int64_t)(r * 6 + q) * Co * P + p];
+        for (int q = 0; q < 6; ++q) {  // A^T m: columns
+            for (int r = 0; r < 6; ++r) col[r] = mm[r][q];
+            wat(col, o4);
+            for (int r = 0; r < 4; ++r) tt[r][q] = o4[r];
+        }
+        for (int r = 0; r < 4; ++r) {  // (A^T m) A: rows
+            wat(tt[r], o4);
+            for (int q = 0; q < 4; ++q) band[(4 * tr + r) * W4 + 4 * tw + q] = o4[q];
         }
     }
-    // border cells beside this tile: top / bottom rows (with the corners) and left / right columns
-    const int x0 = 4 * tw + 1, x1 = min(4 * tw + 4, W), y0 = 4 * th + 1, y1 = min(4 * th + 4, H);
-    const int cx0 = tw == 0 ? 0 : x0, cx1 = tw == TW - 1 ? W + 1 : x1;
-    if (th == 0)
-        for (int xx = cx0; xx <= cx1; ++xx) put(0, xx, 0.0);
-    if (th == (H + 3) / 4 - 1)
-        for (int xx = cx0; xx <= cx1; ++xx) put(H + 1, xx, 0.0);
-    if (tw == 0)
-        for (int yy = y0; yy <= y1; ++yy) put(yy, 0, 0.0);
-    if (tw == TW - 1)
-        for (int yy = y0; yy <= y1; ++yy) put(yy, W + 1, 0.0);
+    __syncthreads();
+    const int64_t ybase = b * y_bs + (int64_t)co * (H + 2) * R;
+    const double* rb = res ? res + b * res_bs + (int64_t)co * (H + 2) * R : nullptr;
+    const double bv = bias ? bias[co] : 0.0;
+    auto put = [&](int64_t o, double v) {
+        if (yf) yf[ybase + o] = (float)v;
+        else y[ybase + o] = v;
+    };
+    const int oy0 = 4 * th0, ny = min(4 * nth, H - oy0);
+    // the band's output rows with their left / right border cells, row-contiguous
+    for (int i = threadIdx.x; i < ny * R; i += 256) {
+        const int r = i / R, q = i - r * R;
+        const int64_t o = (int64_t)(oy0 + r + 1) * R + q;
+        if (q == 0 || q == R - 1) {
+            put(o, 0.0);
+        } else {
+            double v = act64(band[r * W4 + q - 1] + bv, act, 0.0);
+            if (rb) v += rb[o];
+            put(o, v);
+        }
+    }
+    if (th0 == 0)
+        for (int q = threadIdx.x; q < R; q += 256) put(q, 0.0);
+    if (th0 + nth == TH)
+        for (int q = threadIdx.x; q < R; q += 256) put((int64_t)(H + 1) * R + q, 0.0);
+}
+
+// Fused Winograd for the small-channel levels (Ci in {16, 32, 64}, Co in {16, 32}: U-Net levels 0-1), where the
+// separate transforms' 2.25x HBM traffic would cost more than the 4x fewer MFMA FLOPs save.  Measured no faster
+// than the direct engine (its per-thread 6x6 patch reads and 4-wide output writes are strided, 25 % of each
+// access used), so off by default (RVC_RMVPE_WINO=3 turns it on; correct either way, tests/test_gpu_ops.py).  One block = 16
+// consecutive output tiles (P order) of one image, all Co: per 16-channel input chunk the threads transform their
+// (channel, tile) 6x6 patches (read from the bordered image, L1 / L2 resident across the overlapping patches)
+// into U [36][16 ci][16 tiles] in LDS, and each wave accumulates XI of the 36 products M[x] += V[x]^T U[x]
+// (v_mfma_f64_16x16x4: V from global, L2 resident, U from LDS); at the end M goes through LDS, 16 output
+// channels at a time, to the output transform with the bias / activation / residual epilogue and the zero border.
+// Nothing but x, v and y touches HBM.  Waves: 36 / XI (XI = 9 at Co 16: 4 waves; 6 at Co 32: 6 waves, which
+// keeps the accumulators at 48 doubles per lane).
+template <int CI, int CO>
+__global__ __launch_bounds__(64 * (CO == 16 ? 4 : 6), CO == 16 ? 2 : 1) void wino_fused64_kernel(
+    const double* x, const double* v, const double* bias, const double* res, double* y, float* yf, int H, int W,
+    int TW, int P, int act, int64_t x_bs, int64_t y_bs, int64_t res_bs) {
+    constexpr int XI = CO == 16 ? 9 : 6;  // products per wave
+    constexpr int NW = 36 / XI;
+    constexpr int NT = 64 * NW;
+    constexpr int CB = CO / 16;           // 16-channel output blocks
+    extern __shared__ double sm[];         // [36][16][16]: U chunk, then M (16 output channels at a time)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.y;
+    const int p0 = blockIdx.x * 16;
+    const int R = W + 2;
+    const double* xb = x + b * x_bs;
+    doublex4 acc[XI][CB];
+#pragma unroll
+    for (int i = 0; i < XI; ++i)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) acc[i][c] = doublex4{0.0, 0.0, 0.0, 0.0};
+    const int lk = lane >> 4, ln = lane & 15;
+#pragma unroll 1
+    for (int c0 = 0; c0 < CI; c0 += 16) {
+        // input transform of (channel c0 + t / 16, tile p0 + t % 16)
+        for (int t = tid; t < 256; t += NT) {
+            const int cl = t >> 4, j = t & 15, p = p0 + j;
+            double d[6][6];
+            if (p < P) {
+                const int th = p / TW, tw = p - th * TW;
+                const double* xc = xb + (int64_t)(c0 + cl) * (H + 2) * R;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const int yy = 4 * th + r;
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) {
+                        const int xx = 4 * tw + q;
+                        d[r][q] = (yy < H + 2 && xx < R) ? xc[(int64_t)yy * R + xx] : 0.0;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 6; ++r)
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) d[r][q] = 0.0;
+            }
+            double o6[6], col[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {  // d B: rows, in place
+                wbt(d[r], o6);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) d[r][q] = o6[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {  // B^T (d B): columns
+#pragma unroll
+                for (int r = 0; r < 6; ++r) col[r] = d[r][q];
+                wbt(col, o6);
+#pragma unroll
+                for (int r = 0; r < 6; ++r) sm[((r * 6 + q) * 16 + cl) * 16 + j] = o6[r];
+            }
+        }
+        __syncthreads();
+        // products: M[x][co][tile] += sum_ci V[x][ci][co] U[x][ci][tile], 4 k-steps of 4 channels
+#pragma unroll
+        for (int i = 0; i < XI; ++i) {
+            const int xi = wave * XI + i;
+            const double* vx = v + ((int64_t)xi * CI + c0) * CO;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const double bop = sm[(xi * 16 + ks * 4 + lk) * 16 + ln];
+#pragma unroll
+                for (int c = 0; c < CB; ++c)
+                    acc[i][c] = mfma64(vx[(ks * 4 + lk) * CO + c * 16 + ln], bop, acc[i][c]);
+            }
+        }
+        __syncthreads();
+    }
+    const double* rb = res ? res + b * res_bs : nullptr;
+    const int64_t ybase = b * y_bs;
+    auto put = [&](int64_t o, double val) {
+        if (yf) yf[ybase + o] = (float)val;
+        else y[ybase + o] = val;
+    };
+    const int TH = (H + 3) / 4;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+        // this wave's M[x][co][tile] (D layout: col = tile = l & 15, row = co = (l >> 4) + 4 r) -> LDS
+#pragma unroll
+        for (int i = 0; i < XI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm[((wave * XI + i) * 16 + lk + 4 * r) * 16 + ln] = acc[i][c][r];
+        __syncthreads();
+        for (int t = tid; t < 256; t += NT) {
+            const int cl = t >> 4, j = t & 15, p = p0 + j;
+            if (p >= P) continue;
+            const int co = c * 16 + cl;
+            const int th = p / TW, tw = p - th * TW;
+            double mm[6][6], o4[4], col[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int q = 0; q < 6; ++q) mm[r][q] = sm[((r * 6 + q) * 16 + cl) * 16 + j];
+            double tt[4][6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {  // A^T m: columns
+#pragma unroll
+                for (int r = 0; r < 6; ++r) col[r] = mm[r][q];
+                wat(col, o4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tt[r][q] = o4[r];
+            }
+            const int64_t cbase = (int64_t)co * (H + 2) * R;
+            const double bv = bias ? bias[co] : 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // (A^T m) A: rows
+                wat(tt[r], o4);
+                const int oy = 4 * th + r;
+                if (oy < H) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int ox = 4 * tw + q;
+                        if (ox < W) {
+                            const int64_t o = cbase + (int64_t)(oy + 1) * R + ox + 1;
+                            double val = act64(o4[q] + bv, act, 0.0);
+                            if (rb) val += rb[o];
+                            put(o, val);
+                        }
+                    }
+                }
+            }
+            // border cells beside this tile: top / bottom rows (with the corners) and left / right columns
+            const int x0 = 4 * tw + 1, x1 = min(4 * tw + 4, W), y0 = 4 * th + 1, y1 = min(4 * th + 4, H);
+            const int cx0 = tw == 0 ? 0 : x0, cx1 = tw == TW - 1 ? W + 1 : x1;
+            if (th == 0)
+                for (int xx = cx0; xx <= cx1; ++xx) put(cbase + xx, 0.0);
+            if (th == TH - 1)
+                for (int xx = cx0; xx <= cx1; ++xx) put(cbase + (int64_t)(H + 1) * R + xx, 0.0);
+            if (tw == 0)
+                for (int yy = y0; yy <= y1; ++yy) put(cbase + (int64_t)yy * R, 0.0);
+            if (tw == TW - 1)
+                for (int yy = y0; yy <= y1; ++yy) put(cbase + (int64_t)yy * R + W + 1, 0.0);
+        }
+        __syncthreads();
+    }
+}
+
+template <int CI, int CO>
+void launch_wino_fused(const rvc_wino64_args* a, int TW, int P, int64_t x_bs, int64_t y_bs, int64_t r_bs,
+                       hipStream_t s) {
+    constexpr int NT = 64 * (CO == 16 ? 4 : 6);
+    hipLaunchKernelGGL((wino_fused64_kernel<CI, CO>), dim3(cdiv(P, 16), (unsigned)a->B), dim3(NT), 36 * 256 * 8, s,
+                       a->x, a->v, a->bias, a->res, a->y_f32 ? nullptr : (double*)a->y,
+                       a->y_f32 ? (float*)a->y : nullptr, (int)a->H, (int)a->W, TW, P, a->out_act, x_bs, y_bs, r_bs);
+}
+
+bool wino_fused_shape(int64_t Ci, int64_t Co) {
+    return (Ci == 16 || Ci == 32 || Ci == 64) && (Co == 16 || Co == 32);
 }
 }  // namespace
 
@@ -776,7 +969,6 @@ __global__ void wino_out64_kernel(const double* m, double* y, float* yf, const d
 // (exp64: Cody-Waite reduction, degree-12 Taylor, ~1 ulp) and a Newton-refined reciprocal, and r and z are
 // evaluated at once on two lanes of the unit's 16-lane group (lane 0: r, lane 1: z), n after r on lane 0.
 constexpr int G_H = 256;
-constexpr int G_WG = 16;
 
 RVC_DEV double exp64(double x) {
     x = fmin(fmax(x, -700.0), 700.0);
@@ -807,17 +999,21 @@ RVC_DEV double rcp64(double d) {  // 1 / d for d >= 1: hardware estimate + 2 New
     return fma(y, e, y);
 }
 
-__global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const double* whh, const double* bhh,
-                                                      double* y, unsigned long long* gran, int* err, int64_t T,
-                                                      unsigned spin_limit, int64_t gi_bs, int64_t y_bs) {
+// NWG workgroups per direction (16: 256 threads, 16 units each; 8: 512 threads, 32 units each -- half the CUs held
+// for the whole recurrence; RVC_BIGRU64_WG=8).  Measured: 8 costs the clip stream 5 % (876 vs 921 xRT): 16.
+template <int NWG>
+__global__ __launch_bounds__(4096 / NWG) void bigru64_kernel(const double* gi, const double* whh, const double* bhh,
+                                                             double* y, unsigned long long* gran, int* err, int64_t T,
+                                                             unsigned spin_limit, int64_t gi_bs, int64_t y_bs) {
+    constexpr int UPW = G_H / NWG;  // hidden units per workgroup
     gi += (int64_t)blockIdx.y * gi_bs;
     y += (int64_t)blockIdx.y * y_bs;
     gran += (int64_t)blockIdx.y * 2 * 2 * G_H * 2;
-    const int d = blockIdx.x / G_WG;
-    const int j = blockIdx.x % G_WG;
+    const int d = blockIdx.x / NWG;
+    const int j = blockIdx.x % NWG;
     const int tid = threadIdx.x;
     const int ul = tid >> 4, s = tid & 15;
-    const int u = j * 16 + ul;
+    const int u = j * UPW + ul;
     __shared__ double hs[2][G_H];
     __shared__ int abort_flag;
     if (tid == 0) abort_flag = 0;
@@ -841,27 +1037,29 @@ __global__ __launch_bounds__(256) void bigru64_kernel(const double* gi, const do
         gxg = G[(int64_t)(gsel * G_H + u) * T + tau0];
         gxn = G[(int64_t)(2 * G_H + u) * T + tau0];
     }
-    hs[0][tid] = 0.0;
+    if (tid < G_H) hs[0][tid] = 0.0;
     __syncthreads();
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     for (int64_t t = 0; t < T; ++t) {
         const int64_t tau = d ? T - 1 - t : t;
         const int cur = (int)(t & 1);
         if (t > 0) {
-            const unsigned long long* g = GR + ((t - 1) & 1) * G_H * 2 + 2 * tid;
-            u64x2 v;
-            unsigned spins = 0;
-            for (;;) {
-                asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(g) : "memory");
-                if ((uint32_t)(v.x >> 32) == (uint32_t)t && (uint32_t)(v.y >> 32) == (uint32_t)t) break;
-                if (++spins > spin_limit) {
-                    atomicExch(err, 1);
-                    abort_flag = 1;
-                    break;
+            if (tid < G_H) {  // (wave-uniform) one granule per thread of the first 4 waves
+                const unsigned long long* g = GR + ((t - 1) & 1) * G_H * 2 + 2 * tid;
+                u64x2 v;
+                unsigned spins = 0;
+                for (;;) {
+                    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(g) : "memory");
+                    if ((uint32_t)(v.x >> 32) == (uint32_t)t && (uint32_t)(v.y >> 32) == (uint32_t)t) break;
+                    if (++spins > spin_limit) {
+                        atomicExch(err, 1);
+                        abort_flag = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                hs[cur][tid] = __hiloint2double((int)(uint32_t)v.y, (int)(uint32_t)v.x);
             }
-            hs[cur][tid] = __hiloint2double((int)(uint32_t)v.y, (int)(uint32_t)v.x);
             __syncthreads();
             if (abort_flag) break;
         }
@@ -1030,8 +1228,13 @@ extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double
     for (int64_t b0 = 0; b0 < B; b0 += G_B_MAX) {
         const int64_t nb = B - b0 < G_B_MAX ? B - b0 : G_B_MAX;
         RVC_HIP(hipMemsetAsync(gran_ws, 0, (size_t)nb * RVC_BIGRU64_GRAN_BYTES, s));
-        hipLaunchKernelGGL(bigru64_kernel, dim3(2 * G_WG, (unsigned)nb), dim3(256), 0, s, gi + b0 * gi_bs, whh, bhh,
-                           y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
+        static const int nwg = getenv("RVC_BIGRU64_WG") && atoi(getenv("RVC_BIGRU64_WG")) == 8 ? 8 : 16;
+        if (nwg == 8)
+            hipLaunchKernelGGL(bigru64_kernel<8>, dim3(2 * 8, (unsigned)nb), dim3(512), 0, s, gi + b0 * gi_bs, whh, bhh,
+                               y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
+        else
+            hipLaunchKernelGGL(bigru64_kernel<16>, dim3(2 * 16, (unsigned)nb), dim3(256), 0, s, gi + b0 * gi_bs, whh,
+                               bhh, y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
         RVC_HIP(hipGetLastError());
     }
     return RVC_OK;
@@ -1042,7 +1245,11 @@ extern "C" int rvc_wino64_use(int64_t Ci, int64_t Co, int64_t H, int64_t W) {
     static const int on = getenv("RVC_RMVPE_WINO") ? atoi(getenv("RVC_RMVPE_WINO")) : 1;
     // images of fewer output tiles than this run direct (the 36 GEMMs get too narrow; RVC_RMVPE_WINO_MINP)
     static const int64_t minp = getenv("RVC_RMVPE_WINO_MINP") ? atoll(getenv("RVC_RMVPE_WINO_MINP")) : 90;
-    if (!on || Ci < 64 || Co < 64) return 0;
+    if (!on) return 0;
+    // the fused small-channel form only on request (RVC_RMVPE_WINO=3): measured no faster than the direct engine
+    // (16 -> 16 at 3232 x 128: 74 us vs 70-80; 32 -> 32 at 1616 x 64: 99 vs 57-81; clip stream 921 vs 927 xRT)
+    if (wino_fused_shape(Ci, Co)) return on == 3;
+    if (Ci < 64 || Co < 64) return 0;
     return H <= 0 || W <= 0 || ((H + 3) / 4) * ((W + 3) / 4) >= minp;
 }
 
@@ -1088,6 +1295,7 @@ int wino64_plan(const rvc_wino64_args* a, Wino64& w) {
 extern "C" int64_t rvc_wino64_workspace_bytes(const rvc_wino64_args* a) {
     Wino64 w;
     if (wino64_plan(a, w) != RVC_OK) return -1;
+    if (wino_fused_shape(a->Ci, a->Co)) return 0;
     const int64_t g = rvc_conv64_workspace_bytes(&w.g);
     if (g < 0) return -1;
     return (a->B * (w.u_n + w.m_n)) * 8 + g;
@@ -1097,6 +1305,25 @@ extern "C" int rvc_wino64_conv(const rvc_wino64_args* a, void* ws, int64_t ws_by
     Wino64 w;
     const int rc = wino64_plan(a, w);
     if (rc != RVC_OK) return rc;
+    if (wino_fused_shape(a->Ci, a->Co)) {
+        const int64_t img_i = a->Ci * (a->H + 2) * (a->W + 2), img_o = a->Co * (a->H + 2) * (a->W + 2);
+        const int64_t x_bs = a->x_bstride ? a->x_bstride : img_i, y_bs = a->y_bstride ? a->y_bstride : img_o;
+        const int64_t r_bs = a->res_bstride ? a->res_bstride : img_o;
+        RVC_CHECK_ARG(a->B < 65536, "wino64: too many images");
+        hipStream_t s = (hipStream_t)stream;
+        const int TW = (int)w.TW, P = (int)w.P;
+        if (a->Co == 16) {
+            if (a->Ci == 16) launch_wino_fused<16, 16>(a, TW, P, x_bs, y_bs, r_bs, s);
+            else if (a->Ci == 32) launch_wino_fused<32, 16>(a, TW, P, x_bs, y_bs, r_bs, s);
+            else launch_wino_fused<64, 16>(a, TW, P, x_bs, y_bs, r_bs, s);
+        } else {
+            if (a->Ci == 16) launch_wino_fused<16, 32>(a, TW, P, x_bs, y_bs, r_bs, s);
+            else if (a->Ci == 32) launch_wino_fused<32, 32>(a, TW, P, x_bs, y_bs, r_bs, s);
+            else launch_wino_fused<64, 32>(a, TW, P, x_bs, y_bs, r_bs, s);
+        }
+        RVC_HIP(hipGetLastError());
+        return RVC_OK;
+    }
     const int64_t g = rvc_conv64_workspace_bytes(&w.g);
     RVC_CHECK_ARG(g >= 0, "wino64: GEMM plan failed");
     const int64_t need = a->B * (w.u_n + w.m_n) * 8 + g;
@@ -1110,8 +1337,12 @@ extern "C" int rvc_wino64_conv(const rvc_wino64_args* a, void* ws, int64_t ws_by
     const int64_t x_bs = a->x_bstride ? a->x_bstride : img_i, y_bs = a->y_bstride ? a->y_bstride : img_o;
     const int64_t r_bs = a->res_bstride ? a->res_bstride : img_o;
     RVC_CHECK_ARG(a->B < 65536 && a->Ci < 65536 && a->Co < 65536, "wino64: too many images / channels");
-    hipLaunchKernelGGL(wino_in64_kernel, dim3(cdiv(w.P, 64), (unsigned)a->Ci, (unsigned)a->B), dim3(64), 0, s, a->x, u,
-                       (int)a->Ci, (int)a->H, (int)a->W, (int)w.TW, (int)w.P, x_bs, w.u_n);
+    const int RT = wino_rt((int)a->W);
+    const unsigned nband = cdiv((a->H + 3) / 4, RT);
+    const size_t lds_in = (size_t)(4 * RT + 2) * (a->W + 2) * 8, lds_out = (size_t)(4 * RT) * (4 * w.TW) * 8;
+    RVC_CHECK_ARG(lds_in <= 64 * 1024 && lds_out <= 64 * 1024, "wino64: image too wide (W %lld)", (long long)a->W);
+    hipLaunchKernelGGL(wino_in64_kernel, dim3(nband, (unsigned)a->Ci, (unsigned)a->B), dim3(256), lds_in, s, a->x, u,
+                       (int)a->Ci, (int)a->H, (int)a->W, (int)w.TW, (int)w.P, RT, x_bs, w.u_n);
     RVC_HIP(hipGetLastError());
     w.g.x = u;
     w.g.y = m;
@@ -1119,9 +1350,9 @@ extern "C" int rvc_wino64_conv(const rvc_wino64_args* a, void* ws, int64_t ws_by
     w.g.y_bstride = a->Co * w.P;
     const int rg = rvc_conv64(&w.g, gws, g, stream);
     if (rg != RVC_OK) return rg;
-    hipLaunchKernelGGL(wino_out64_kernel, dim3(cdiv(w.P, 64), (unsigned)a->Co, (unsigned)a->B), dim3(64), 0, s, m,
+    hipLaunchKernelGGL(wino_out64_kernel, dim3(nband, (unsigned)a->Co, (unsigned)a->B), dim3(256), lds_out, s, m,
                        a->y_f32 ? nullptr : (double*)a->y, a->y_f32 ? (float*)a->y : nullptr, a->bias, a->res,
-                       (int)a->Co, (int)a->H, (int)a->W, (int)w.TW, (int)w.P, a->out_act, w.m_n, y_bs, r_bs);
+                       (int)a->Co, (int)a->H, (int)a->W, (int)w.TW, (int)w.P, RT, a->out_act, w.m_n, y_bs, r_bs);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }

@@ -321,12 +321,15 @@ def test_conv64_every_plan(ops, Ci, Co, H, W, B, k):
     assert k == 1 or max(p[1] for p in seen) >= 3, seen
 
 
-@pytest.mark.parametrize("Ci,Co,H,W,B", [(64, 64, 12, 8, 1), (128, 96, 10, 4, 2), (72, 64, 9, 5, 1), (512, 512, 94, 4, 1)])
+@pytest.mark.parametrize("Ci,Co,H,W,B", [(64, 64, 12, 8, 1), (128, 96, 10, 4, 2), (72, 64, 9, 5, 1), (512, 512, 94, 4, 1),
+                                         (16, 16, 12, 8, 1), (32, 16, 9, 5, 2), (64, 32, 10, 6, 1), (16, 32, 7, 4, 1),
+                                         (32, 32, 33, 17, 1), (64, 16, 6, 70, 1)])
 def test_wino64_conv(ops, Ci, Co, H, W, B):
-    """The f64 Winograd F(4x4, 3x3) conv of RMVPE's deep levels (rmvpe64.hip): input transform, 36 GEMMs on the
-    conv engine with per-batch weights, output transform with bias, ReLU, residual and the zero border -- against
-    F.conv2d in f64 (1e-12 relative: the transforms cost ~1e-14) over a NaN-filled output, ragged tiles (H, W not
-    multiples of 4) and batch strides included."""
+    """The f64 Winograd F(4x4, 3x3) conv of RMVPE (rmvpe64.hip): for >= 64 channels the input transform, 36 GEMMs
+    on the conv engine with per-batch weights and the output transform; for 16 / 32 / 64 -> 16 / 32 channels the
+    fused kernel (transforms in LDS) -- each with bias, ReLU, residual and the zero border, against F.conv2d in
+    f64 (1e-12 relative: the transforms cost ~1e-14) over a NaN-filled output, ragged tiles (H, W not multiples
+    of 4) and batch strides included."""
     g = gen(13)
     w = torch.randn(Co, Ci, 3, 3, generator=g, dtype=torch.float64) / math.sqrt(9 * Ci)
     b = torch.randn(Co, generator=g, dtype=torch.float64) * 0.1
@@ -348,7 +351,9 @@ def test_wino64_conv(ops, Ci, Co, H, W, B):
     border = torch.ones(H + 2, W + 2, dtype=torch.bool)
     border[1:-1, 1:-1] = False
     assert torch.equal(o[:, :, border], torch.zeros(B, Co, int(border.sum()), dtype=o.dtype))
-    assert ops.wino64_use(Ci, Co) and not ops.wino64_use(Ci, Co, 94, 4) and ops.wino64_use(Ci, Co, 188, 8)
+    assert ops.wino64_use(Ci, Co) == (Ci >= 64 and Co >= 64)  # the fused small-channel form: tested, off by default
+    if Ci >= 64 and Co >= 64:
+        assert not ops.wino64_use(Ci, Co, 94, 4) and ops.wino64_use(Ci, Co, 188, 8)
 
 
 F16_CASES = [c for c in CONV_CASES if c[6] == 1 and c[2] <= 64 and (c[3] == 1 or (c[3] == 2 and c[0] >= 32))]
