@@ -299,7 +299,10 @@ int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_
  * conv64 with wrap): y = act(conv(x) + bias) (+ res), border cells 0.  v = rvc_wino64_weights(KM w [Ci*9][Co])
  * = the 36 transformed weight matrices [36][Ci][Co] (G g G^T).  rvc_wino64_use(Ci, Co, H, W): whether the f64
  * RMVPE takes this form for a Ci -> Co conv on an H x W image (>= 64 channels each and >= 90 4x4 output tiles,
- * RVC_RMVPE_WINO_MINP; H or W <= 0: the channel rule alone, whether to prepare v; RVC_RMVPE_WINO=0: never). */
+ * RVC_RMVPE_WINO_MINP; H or W <= 0: the channel rule alone, whether to prepare v; RVC_RMVPE_WINO=0: never).
+ * rvc_wino64_conv itself takes any channel counts: 16 / 32 / 64 -> 16 / 32 channels run one fused kernel (transforms
+ * in LDS, no workspace; measured no faster than conv64, so rvc_wino64_use leaves those shapes to conv64 unless
+ * RVC_RMVPE_WINO=3), the rest the three-step form with its workspace. */
 typedef struct rvc_wino64_args {
     const double* x;
     const double* v;
