@@ -903,10 +903,15 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
 // per-thread override of the split-K target grid (rvc_conv1d_set_splitk_target; -1 = the process default)
 static thread_local int g_splitk_target = -1;
 
-void split_k(ConvParams& p, int64_t tiles, int nch) {
-    // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU
+void split_k(ConvParams& p, int64_t tiles, int nch, int per_cu = 2) {
+    // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU.  A kernel of which only one block fits
+    // a CU (the 8-compute-wave x6 tiles: 768 threads) targets 256: past one round of blocks a split only adds
+    // rounds (ContentVec's K = 1 GEMMs, 30 s: 2304 x 768 x 1599 76 -> 49 us unsplit, 3072 x 768 95 -> 89;
+    // RVC_X6_SPLIT_OCC=0 restores 512 for every tile)
     static const int env_target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
-    const int target = g_splitk_target >= 0 ? g_splitk_target : env_target;
+    static const int occ_aware = getenv("RVC_X6_SPLIT_OCC") ? atoi(getenv("RVC_X6_SPLIT_OCC")) : 1;
+    int target = g_splitk_target >= 0 ? g_splitk_target : env_target;
+    if (occ_aware && per_cu == 1 && g_splitk_target < 0) target /= 2;
     int ks = 1;
     if (tiles < target && nch >= 4) {
         ks = (int)((target + tiles - 1) / tiles);
@@ -935,6 +940,9 @@ constexpr int X6_K_MAX = 64;
 // and the operand reads of even positions are 2-way bank conflicted
 bool x6_eligible(const rvc_conv1d_args* a) {
     static const int s2 = getenv("RVC_X6_STRIDE2") ? atoi(getenv("RVC_X6_STRIDE2")) : 1;
+    // RVC_X6_K1=0: the K = 1 GEMMs (ContentVec / TextEncoder linears) on the f32 MFMA engine instead (A/B switch)
+    static const int k1 = getenv("RVC_X6_K1") ? atoi(getenv("RVC_X6_K1")) : 1;
+    if (a->K == 1 && !k1) return false;
     return a->wx && a->Lin < (1 << 24) &&
            (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
            a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= X6_K_MAX &&
@@ -998,7 +1006,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         p.wx_nch = (int)((Cig + 31) / 32);
         p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
         const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
-        split_k(p, tiles, p.wx_nch);
+        split_k(p, tiles, p.wx_nch, cfg.WM * cfg.WN == 8 ? 1 : 2);
         lds = (size_t)2 * (p.wx_passes == 6 || p.wx_passes == RVC_ARITH_FP32_SA ? 3 : (p.wx_passes == 1 ? 1 : 2)) *
               p.span * 64 + 16;  // + the split-fp16 tile |max|
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
