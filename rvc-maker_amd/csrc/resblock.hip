@@ -48,9 +48,14 @@ constexpr int RB_MAXSPAN = 64; // (K - 1) * dil bound (generator: 10 * 5 = 50)
 
 template <int C>
 struct RbGeom {
+    // C = 128 (round 4): 2 row fragments per compute wave, so the 8 waves are 4 row groups x 2 column groups and
+    // a tile is 112 outputs (not 48); its residual rows are read from x in the epilogue instead of LDS (the X and
+    // T tiles alone take 157 KB at 2 split planes), and only the 1- and 2-plane pass sets fit (<= 3 passes)
+    static constexpr int FM = C >= 128 ? 2 : RB_FM;
+    static constexpr bool RLDS = C <= 64;        // residual rows staged in LDS
     static constexpr int RF = C / 16;            // row fragments
     static constexpr int NCH = C / 32;           // 32-channel chunks
-    static constexpr int RG = RF / RB_FM;        // row groups
+    static constexpr int RG = RF / FM;           // row groups
     static constexpr int CG = 8 / RG;            // column groups (RG x CG = 8 compute waves)
     static constexpr int NF1 = CG * RB_FN;       // c1 column fragments: T holds 16 NF1 positions
     static constexpr int NF2 = NF1 - 1;          // c2 column fragments
@@ -65,7 +70,7 @@ size_t rb_lds_bytes(int K, int dil) {
     using G = RbGeom<C>;
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     const int Wx = G::TW + (K - 1) * dil;
-    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (size_t)C * G::RSTR * 4 + 64;  // + split-fp16 scale slots
+    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (G::RLDS ? (size_t)C * G::RSTR * 4 : 0) + 64;  // + fp16 scales
 }
 
 // F16 (with NP = 3): split-fp16 operands (x6_common.h split2h).  The loader waves take each staged x tile's
@@ -78,7 +83,9 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     static_assert(!F16 || NP == 3, "split-fp16: 3 passes");
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int N = G::N, TW = G::TW, NCH = G::NCH, NF1 = G::NF1, NF2 = G::NF2, RSTR = G::RSTR;
-    constexpr int FM = RB_FM, FN = RB_FN;
+    constexpr int FM = G::FM, FN = RB_FN;
+    constexpr bool YREG = RB_YREG && C <= 64;  // C = 128: no register room for the accumulate operands
+    static_assert(G::RLDS || NP <= 3, "C = 128: at most 2 split planes fit LDS");
     extern __shared__ uint4 lds[];
     const int K = p.K, d = p.dil, L = p.L;
     const int hk = (K - 1) / 2;
@@ -86,8 +93,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     const int Wx = TW + (K - 1) * d;
     uint4* Xs = lds;                          // [NCH][Wx][NPL][4]
     uint4* Ts = Xs + NCH * Wx * NPL * 4;      // [NCH][TW][NPL][4]
-    float* Rs = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [C][RSTR]
-    float* xmax = Rs + C * RSTR;  // F16: [2 tile parities][4 loader waves] x tile |max|
+    float* Rs = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [C][RSTR] (C <= 64)
+    float* xmax = Rs + (G::RLDS ? C * RSTR : 0);  // F16: [2 tile parities][4 loader waves] x tile |max|
     float* tmaxs = xmax + 8;      // F16: [8 compute waves] T tile |max|
     const int ntc = (L + N - 1) / N;  // time tiles per clip
     const int ntiles = p.B * ntc;
@@ -167,6 +174,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             }
         };
         auto rstore = [&]() __attribute__((always_inline)) {  // raw residual rows of the staged tile
+            if constexpr (!G::RLDS) return;
 #pragma unroll
             for (int it = 0; it < G::NI; ++it) {
                 if (ltid + 256 * it < nitems) {
@@ -256,7 +264,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #ifndef RB_PD2
 #define RB_PD2 2
 #endif
-    constexpr int PD = NPL == 3 ? RB_PD3 : (NPL == 2 ? RB_PD2 : 4);
+    constexpr int PD = C >= 128 ? (NPL == 2 ? 1 : 2) : (NPL == 3 ? RB_PD3 : (NPL == 2 ? RB_PD2 : 4));
     constexpr int NB = PD + 1;            // ring slots: k-step S uses slot S % NB (compile-time below)
     uint4 abuf[NB][NPL][FM];
     // k-step decode by counters stepped once per k-step (tap, chunk, conv), for the prefetch (PD ahead) and the
@@ -279,9 +287,10 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     }
     bool two = false;  // the computing k-step: conv, chunk, tap, and its tile
     int ch = 0, t = 0, k = 0;
-    float yold[FM][FN][4];
+    float yold[YREG ? FM : 1][YREG ? FN : 1][4];
     int n0 = 0;
     float* yb = p.y;  // the current tile's clip
+    const float* xres = p.x;  // C = 128: the current tile's clip of x, the residual
     // F16: row reciprocal scales of both images (after each image), the x tile's and T tile's reciprocals
     const float* rs1 = reinterpret_cast<const float*>(p.w1x + (int64_t)K * NCH * p.nmf1 * 3 * 64);
     const float* rs2 = reinterpret_cast<const float*>(p.w2x + (int64_t)K * NCH * p.nmf2 * 3 * 64);
@@ -304,6 +313,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                     const int cb = g / ntc;
                     n0 = (g - cb * ntc) * N;
                     yb = p.y + (int64_t)cb * C * L;
+                    xres = p.x + (int64_t)cb * C * L;
                     __syncthreads();  // S0(k)
 #pragma unroll
                     for (int i = 0; i < FM; ++i)
@@ -384,7 +394,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                         }
                     }
                     __syncthreads();  // S1(k): T written; X free for the loaders
-                    if (RB_YREG && p.accumulate) {
+                    if (YREG && p.accumulate) {
 #pragma unroll
                         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -410,8 +420,9 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
                                     float v = (F16 ? acc[i][j][r] * (rs2[m0 + r] * t_rs) : acc[i][j][r]) + p.b2[m0 + r];
-                                    v = v + Rs[(m0 + r) * RSTR + col];
-                                    if (p.accumulate) v += RB_YREG ? yold[i][j][r] : yb[(int64_t)(m0 + r) * L + q];
+                                    if constexpr (G::RLDS) v = v + Rs[(m0 + r) * RSTR + col];
+                                    else v = v + xres[(int64_t)(m0 + r) * L + q];
+                                    if (p.accumulate) v += YREG ? yold[i][j][r] : yb[(int64_t)(m0 + r) * L + q];
                                     yb[(int64_t)(m0 + r) * L + q] = v;
                                 }
                             }
@@ -459,7 +470,8 @@ int launch_rb(const RbParams& p, hipStream_t s) {
 
 int rb_check(const rvc_resblock_args* a) {
     RVC_CHECK_ARG(a && a->x && a->y && a->w1x && a->w2x && a->b1 && a->b2, "resblock: null pointer");
-    RVC_CHECK_ARG(a->C == 32 || a->C == 64, "resblock: C must be 32 or 64 (got %lld)", (long long)a->C);
+    RVC_CHECK_ARG(a->C == 32 || a->C == 64 || a->C == 128, "resblock: C must be 32, 64 or 128 (got %lld)", (long long)a->C);
+    RVC_CHECK_ARG(a->C != 128 || a->passes != 6, "resblock: C = 128 takes at most 2 split planes (passes 3, 1, F16X3)");
     RVC_CHECK_ARG(a->L > 0 && a->C * a->L < (1ll << 31), "resblock: bad length");
     RVC_CHECK_ARG(a->B >= 0 && (int64_t)(a->B > 1 ? a->B : 1) * ((a->L + 15) / 16) < (1ll << 31), "resblock: bad B");
     RVC_CHECK_ARG(a->K >= 1 && a->K % 2 == 1 && a->K <= 15 && a->dil >= 1 && (a->K - 1) * a->dil <= RB_MAXSPAN,
@@ -479,6 +491,7 @@ extern "C" int64_t rvc_resblock_lds_bytes(int64_t C, int K, int dil, int passes)
                                                                                 : rb_lds_bytes<32, 1>(K, dil);
     if (C == 64) return passes == 6 ? rb_lds_bytes<64, 6>(K, dil) : passes == 3 ? rb_lds_bytes<64, 3>(K, dil)
                                                                                 : rb_lds_bytes<64, 1>(K, dil);
+    if (C == 128) return passes == 6 ? -1 : passes == 3 ? rb_lds_bytes<128, 3>(K, dil) : rb_lds_bytes<128, 1>(K, dil);
     return -1;
 }
 
@@ -506,6 +519,11 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
         if (a->passes == 6) return launch_rb<32, 6>(p, s);
         if (a->passes == 3) return launch_rb<32, 3>(p, s);
         return launch_rb<32, 1>(p, s);
+    }
+    if (a->C == 128) {
+        if (a->passes == RVC_ARITH_F16X3) return launch_rb<128, 3, true>(p, s);
+        if (a->passes == 3) return launch_rb<128, 3>(p, s);
+        return launch_rb<128, 1>(p, s);
     }
     if (a->passes == RVC_ARITH_F16X3) return launch_rb<64, 3, true>(p, s);
     if (a->passes == 6) return launch_rb<64, 6>(p, s);

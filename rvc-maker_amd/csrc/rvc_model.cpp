@@ -69,9 +69,13 @@ int rb_passes(const rvc_ctx* c, int K) {
 bool rb_pass_ok(int passes) { return passes == 6 || passes == 3 || passes == 1 || passes == RVC_ARITH_F16X3; }
 
 bool resblock_fusable(const rvc_ctx* c, const ConvW& c1, const ConvW& c2, int d) {
-    return c->fused_rb && rb_pass_ok(rb_passes(c, c1.K)) && c1.wx_bf && c2.wx_bf && c1.Ci == c1.Co &&
-           c1.Co == c2.Ci && c2.Ci == c2.Co &&
-           (c1.Co == 32 || c1.Co == 64) && c1.K == c2.K && c1.K % 2 == 1 && c1.K <= 15 && (c1.K - 1) * d <= 64;
+    // the 128-channel pair only at <= 2 split planes (passes 3, 1, F16X3: what fits its LDS) and on request
+    // (RVC_AMD_FUSED_RB128=1: measured slower in the clip stream), as ops.py
+    static const bool rb128 = getenv("RVC_AMD_FUSED_RB128") && atoi(getenv("RVC_AMD_FUSED_RB128")) != 0;
+    const int passes = rb_passes(c, c1.K);
+    const bool chans = c1.Co == 32 || c1.Co == 64 || (c1.Co == 128 && rb128 && passes != 6);
+    return c->fused_rb && rb_pass_ok(passes) && c1.wx_bf && c2.wx_bf && c1.Ci == c1.Co && c2.Ci == c2.Co &&
+           c1.Co == c2.Co && chans && c1.K == c2.K && c1.K % 2 == 1 && c1.K <= 15 && (c1.K - 1) * d <= 64;
 }
 
 

@@ -338,10 +338,18 @@ def rb_passes(K):
     return PASSES[_PRECISION]
 
 
+# the 128-channel fused pair (round 4; <= 2 split planes fit LDS: pass sets 3, 1, F16X3): correct (bit-identical to
+# two launches, tests/test_gpu_resblock.py) but measured slower in the clip stream (893 vs 920 xRT), so only on
+# request: RVC_AMD_FUSED_RB128=1
+FUSED_RB128 = os.environ.get("RVC_AMD_FUSED_RB128", "0") != "0"
+
+
 def resblock_fusable(c1: "Conv", c2: "Conv", dil: int) -> bool:
-    return (FUSED_RB and rb_passes(c1.K) in RB_PASSES and c1.wx is not None and c2.wx is not None
+    passes = rb_passes(c1.K)
+    chans = c1.Co in (32, 64) or (c1.Co == 128 and FUSED_RB128 and passes in (3, 1, F16X3))
+    return (FUSED_RB and passes in RB_PASSES and c1.wx is not None and c2.wx is not None
             and c1.Ci == c1.Co == c2.Ci == c2.Co
-            and c1.Co in (32, 64) and c1.K == c2.K and c1.K % 2 == 1 and c1.K <= 15 and (c1.K - 1) * dil <= 64)
+            and chans and c1.K == c2.K and c1.K % 2 == 1 and c1.K <= 15 and (c1.K - 1) * dil <= 64)
 
 
 def resblock_pair(x, y, c1: "Conv", c2: "Conv", dil: int, slope: float, accumulate: bool = False):

@@ -37,14 +37,19 @@ def torch_ref(x, w, K, d):
     return (xt + x[None])[0]
 
 
-@pytest.mark.parametrize("C", [32, 64])
+@pytest.mark.parametrize("C", [32, 64, 128])
 @pytest.mark.parametrize("K,d", [(3, 1), (3, 5), (7, 3), (11, 1), (11, 5)])
 @pytest.mark.parametrize("precision", ["fp32x6", "bf16x3", "bf16"])
 def test_fused_pair_bit_identical_to_two_launches(C, K, d, precision):
+    """C = 128 (round 4): 2 row fragments per wave, residual read from x; at <= 2 split planes only (the 6-pass
+    pair does not fit LDS), and against a two-launch form without split-K (its per-conv k-order)."""
+    if C == 128 and precision == "fp32x6":
+        pytest.skip("the 128-channel pair takes <= 2 split planes")
     w, c1, c2 = make_pair(C, K, seed=C * 100 + K * 10 + d)
     L = 5003  # several tiles and a partial one
     x = torch.randn(C, L, generator=torch.Generator().manual_seed(K + d)).to(DEV)
-    with ops.precision(precision):
+    with ops.precision(precision), ops.splitk_target(0):
+        assert C == 128 or ops.resblock_fusable(c1, c2, d)
         ref = two_launch(x, c1, c2, K, d)
         y = torch.full_like(x, float("nan"))
         ops.resblock_pair(x, y, c1, c2, d, 0.1)
@@ -89,7 +94,7 @@ def test_fused_pair_rejects_bad_args():
         ops.resblock_pair(x16, torch.empty_like(x16), c16a, c16b, 1, 0.1)
 
 
-@pytest.mark.parametrize("C", [32, 64])
+@pytest.mark.parametrize("C", [32, 64, 128])
 @pytest.mark.parametrize("K,d", [(3, 1), (7, 3), (11, 5)])
 @pytest.mark.parametrize("scale", [1.0, 1e-4, 1e4])
 def test_fused_pair_f16x3(C, K, d, scale):
@@ -100,7 +105,7 @@ def test_fused_pair_f16x3(C, K, d, scale):
     L = 5003
     x = (torch.randn(C, L, generator=torch.Generator().manual_seed(K + d + 1)) * scale).to(DEV)
     with ops.precision("f16x3"):
-        assert ops.resblock_fusable(c1, c2, d)
+        assert C == 128 or ops.resblock_fusable(c1, c2, d)
         y = torch.full_like(x, float("nan"))
         ops.resblock_pair(x, y, c1, c2, d, 0.1)
         acc0 = (torch.randn(C, L, generator=torch.Generator().manual_seed(7)) * scale).to(DEV)
