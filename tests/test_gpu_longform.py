@@ -34,7 +34,7 @@ def test_unet_tiles_match_whole_image():
     img, Tp = rm.mel_image(mel)
     whole = rm.unet_seq(img, Tp)
     for a, b, r0, r1 in longform.tile_plan(Tp, 3):
-        tile = torch.zeros(1, r1 - r0 + 2, img.shape[-1], device=DEV)
+        tile = torch.zeros(1, r1 - r0 + 2, img.shape[-1], device=DEV, dtype=img.dtype)
         tile[0, 1:-1] = img[0, 1 + r0: 1 + r1]
         seq = rm.unet_seq(tile, r1 - r0)[:, a - r0: b - r0]
         err = (seq - whole[:, a:b]).abs().max().item()
