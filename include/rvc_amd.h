@@ -289,10 +289,10 @@ typedef struct rvc_conv64_args {
 int64_t rvc_conv64_workspace_bytes(const rvc_conv64_args* a);
 /* the planner's choice for a (diagnostics): out[0] tile (0..7: 16x512, 16x256, 32x256, 32x128, 64x128, 64x64,
  * 128x128, 128x64 with 16-deep k chunks; 8..12: 16x256, 32x128, 64x128, 64x64, 128x64 with 32-deep; 13, 14: 128x16
- * with 16- / 32-deep), out[1] split-K, out[2] compact form (wrap > 0: the H x W interior cells as the GEMM's
+ * with 16- / 32-deep; 15..17: 16x256, 32x128, 32x256 with 36-deep = 4 whole channels of a 3x3 conv), out[1] split-K, out[2] compact form (wrap > 0: the H x W interior cells as the GEMM's
  * columns instead of the bordered image), out[3] blocks of the conv launch */
 int rvc_conv64_plan(const rvc_conv64_args* a, int* out);
-/* force the planner (process-wide; sweeps and tests): tile -1..14, ksplit -1..32, compact -1..1 (-1 = planner's) */
+/* force the planner (process-wide; sweeps and tests): tile -1..17, ksplit -1..32, compact -1..1 (-1 = planner's) */
 int rvc_conv64_set_plan(int tile, int ksplit, int compact);
 int rvc_conv64(const rvc_conv64_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* Winograd F(4x4, 3x3) f64 conv for RMVPE's deep levels (3x3 pad 1 on bordered [C][H+2][W+2] images, as

@@ -64,8 +64,10 @@ RVC_DEV double act64(double v, int act, double slope) {
 
 // staged input doubles per thread (rows * span <= 256 * NB): 12 for the 512-column tile (3 channel rows of a
 // 3x3 conv's 774-wide span), 8 otherwise (a K = 1 chunk's 16 rows of 128)
-template <int BN>
-constexpr int nb64() { return BN >= 512 ? 12 : 8; }
+// (and 12 for the 256-column tiles of 32- / 36-deep chunks: 4 channel rows of a 3x3 conv's 518-wide span)
+constexpr int nb64h(int BN, int KC) { return (BN >= 512 || (KC >= 32 && BN >= 256)) ? 12 : 8; }
+template <int BN, int KC>
+constexpr int nb64() { return nb64h(BN, KC); }
 
 struct C64 {
     const double* x;
@@ -146,10 +148,11 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
     constexpr int KC = KC_;
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
-    constexpr int NB64 = nb64<BN>();
+    constexpr int NB64 = nb64<BN, KC>();
     constexpr int WS = BM + 4;            // weight tile row pitch (doubles)
-    constexpr int NA = KC * BM / 256;     // weight doubles staged per thread
-    static_assert(WM * WN == 4 && NA >= 1 && (KC * BM) % 256 == 0, "tile");
+    constexpr int NA = (KC * BM + 255) / 256;  // weight doubles staged per thread (the last slot partial at KC 36)
+    constexpr bool NA_PART = (KC * BM) % 256 != 0;
+    static_assert(WM * WN == 4 && NA >= 1 && KC % 4 == 0, "tile");
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int xs_n = p.rows_max * p.span_s + 1;  // + a dump cell
     double* Wsb = sm;                       // [2][KC][WS]
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
         for (int i = 0; i < NA; ++i) {
             const int idx = tid + 256 * i;
             const int kk = idx / BM, m = idx % BM;
-            const bool ok = k0 + kk < kmax && m0 + m < Co;
+            const bool ok = k0 + kk < kmax && m0 + m < Co && (!NA_PART || idx < KC * BM);
             ra[i] = wb[ok ? (int64_t)(k0 + kk) * Co + m0 + m : 0];
         }
         const int c_lo = k0 / K;
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256, 2) void conv64_kernel(C64 p) {
             const int idx = tid + 256 * i;
             const int kk = idx / BM, m = idx % BM;
             const bool ok = k0 + kk < kmax && m0 + m < Co;
-            Ws[kk * WS + m] = ok ? ra[i] : 0.0;
+            if (!NA_PART || idx < KC * BM) Ws[kk * WS + m] = ok ? ra[i] : 0.0;
         }
         const int c_lo = k0 / K;
         const int rows = min((k0 + KC - 1) / K, Ci - 1) - c_lo + 1;
@@ -374,7 +377,7 @@ struct Cfg64 {
 // the tiles the planner chooses from (BM x BN = 16 FM WM x 16 FN WN, k chunk KC): the 32-deep chunks halve the
 // barriers and staging rounds per k and pay where the tile's registers and LDS leave room (scripts/conv64_dbg.hip:
 // 32 x 128 tiles 15-20 % faster, 32 x 256 ones slower)
-constexpr int N_TILES64 = 15;
+constexpr int N_TILES64 = 18;
 constexpr Cfg64 kTiles64[N_TILES64] = {
     {1, 8, 1, 4, 16},  // 0: 16 x 512
     {1, 4, 1, 4, 16},  // 1: 16 x 256
@@ -391,6 +394,11 @@ constexpr Cfg64 kTiles64[N_TILES64] = {
     {4, 2, 2, 2, 32},  // 12: 128 x 64, KC 32
     {2, 1, 4, 1, 16},  // 13: 128 x 16 (the Winograd GEMMs of small images: a few dozen columns)
     {2, 1, 4, 1, 32},  // 14: 128 x 16, KC 32
+    // 3x3 convs only: 36-deep chunks = 4 whole input channels, so each channel row is staged once per block
+    // (16-deep chunks straddle channels and stage ~1.6 rows per channel)
+    {1, 4, 1, 4, 36},  // 15: 16 x 256, KC 36
+    {2, 2, 1, 4, 36},  // 16: 32 x 128, KC 36
+    {2, 4, 1, 4, 36},  // 17: 32 x 256, KC 36
 };
 
 // the compact form of the 128 x 128 tile spills (its per-lane column offsets on top of 255 VGPRs): not built;
@@ -530,8 +538,11 @@ int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds)
             const int BM = 16 * c.FM * c.WM, BN = 16 * c.FN * c.WN, KC = c.KC;
             const int rows_max = rows_of(KC);
             const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
+            // the channel-aligned chunks: 3x3 convs only (RVC_C64_KC36=0: never)
+            static const int kc36 = getenv("RVC_C64_KC36") ? atoi(getenv("RVC_C64_KC36")) : 1;
+            if (KC % 16 != 0 && (a->K != 9 || !kc36)) continue;
             const int span = span64(BN, maxoff, cmp ? W : 0);
-            if ((int64_t)rows_max * span > 256 * (BN >= 512 ? 12 : 8) || span >= 65536) continue;
+            if ((int64_t)rows_max * span > 256 * nb64h(BN, KC) || span >= 65536) continue;
             const size_t l = (size_t)(2 * KC * (BM + 4) + 2 * (rows_max * (span + 1) + 1)) * 8 + 2 * KC * 4;
             if (l > 160 * 1024) continue;
             const int occ = std::max(1, std::min(occ64(t, cmp), (int)(160 * 1024 / l)));

@@ -15,7 +15,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "rvc-maker_amd")]
 from rvc_amd import ops  # noqa: E402
 
 TILES = ["16x512", "16x256", "32x256", "32x128", "64x128", "64x64", "128x128", "128x64", "16x256/32", "32x128/32",
-         "64x128/32", "64x64/32", "128x64/32", "128x16", "128x16/32"]
+         "64x128/32", "64x64/32", "128x64/32", "128x16", "128x16/32", "16x256/36", "32x128/36", "32x256/36"]
 # (Ci, Co, H, W): one 3x3 conv per U-Net level (every level's convs are 1.77 GFLOP), the encoder's first conv
 SHAPES = [(16, 16, 3008, 128), (32, 32, 1504, 64), (64, 64, 752, 32), (128, 128, 376, 16), (256, 256, 188, 8),
           (512, 512, 94, 4), (256, 512, 94, 4), (1, 16, 3008, 128)]

@@ -278,7 +278,7 @@ def test_conv2d_bordered_image_writes_zero_border(ops, engine, Ci, Co, H, W, f64
 @pytest.mark.parametrize("Ci,Co,H,W,B,k", [(64, 128, 9, 4, 1, 3), (24, 40, 7, 5, 2, 3), (16, 16, 11, 3, 1, 3),
                                            (48, 72, 6, 4, 2, 1)])
 def test_conv64_every_plan(ops, Ci, Co, H, W, B, k):
-    """The f64 conv engine under every plan its planner can choose (rvc_conv64_set_plan: the 15 tiles, split-K
+    """The f64 conv engine under every plan its planner can choose (rvc_conv64_set_plan: the 18 tiles, split-K
     1..8, bordered and compact forms -- the compact one's GEMM columns are the H x W interior cells, and its
     epilogue writes the border cells beside the image's edge cells): interior = F.conv2d in f64 to 1e-13, border
     exactly 0, over a NaN-filled output, batched (batch strides) and not."""
@@ -296,7 +296,7 @@ def test_conv64_every_plan(ops, Ci, Co, H, W, B, k):
     border[1:-1, 1:-1] = False
     seen = set()
     try:
-        for tile in range(15):
+        for tile in range(18):
             for cmp in (0, 1):
                 for ks in (1, 2, 3, 8):
                     try:
