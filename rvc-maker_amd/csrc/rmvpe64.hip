@@ -1008,8 +1008,13 @@ RVC_DEV double rcp64(double d) {  // 1 / d for d >= 1: hardware estimate + 2 New
 template <int NWG>
 __global__ __launch_bounds__(4096 / NWG) void bigru64_kernel(const double* gi, const double* whh, const double* bhh,
                                                              double* y, unsigned long long* gran, int* err, int64_t T,
-                                                             unsigned spin_limit, int64_t gi_bs, int64_t y_bs) {
+                                                             unsigned spin_limit, int64_t gi_bs, int64_t y_bs,
+                                                             int prio) {
     constexpr int UPW = G_H / NWG;  // hidden units per workgroup
+    // the recurrence's waves first at their SIMDs' issue (s_setprio 3): they share CUs with the synthesizer's
+    // blocks in the clip stream, and every step waits on the slowest of 32 workgroups (RVC_BIGRU64_PRIO=1;
+    // measured neutral in the clip stream, 934 vs 932 xRT: off)
+    if (prio) __builtin_amdgcn_s_setprio(3);
     gi += (int64_t)blockIdx.y * gi_bs;
     y += (int64_t)blockIdx.y * y_bs;
     gran += (int64_t)blockIdx.y * 2 * 2 * G_H * 2;
@@ -1233,12 +1238,13 @@ extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double
         const int64_t nb = B - b0 < G_B_MAX ? B - b0 : G_B_MAX;
         RVC_HIP(hipMemsetAsync(gran_ws, 0, (size_t)nb * RVC_BIGRU64_GRAN_BYTES, s));
         static const int nwg = getenv("RVC_BIGRU64_WG") && atoi(getenv("RVC_BIGRU64_WG")) == 8 ? 8 : 16;
+        static const int prio = getenv("RVC_BIGRU64_PRIO") ? atoi(getenv("RVC_BIGRU64_PRIO")) : 0;
         if (nwg == 8)
             hipLaunchKernelGGL(bigru64_kernel<8>, dim3(2 * 8, (unsigned)nb), dim3(512), 0, s, gi + b0 * gi_bs, whh, bhh,
-                               y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
+                               y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs, prio);
         else
             hipLaunchKernelGGL(bigru64_kernel<16>, dim3(2 * 16, (unsigned)nb), dim3(256), 0, s, gi + b0 * gi_bs, whh,
-                               bhh, y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs);
+                               bhh, y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs, prio);
         RVC_HIP(hipGetLastError());
     }
     return RVC_OK;
