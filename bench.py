@@ -42,6 +42,7 @@ METRIC = "audio-seconds/sec/GPU (xRT) end-to-end VC, 48k v2; 1/2/4/8 GPU scaling
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
 PEAK_MFMA16_TFLOPS = 2500.0  # bf16 / fp16 dense MFMA peak (MI355X_MICROARCH.md)
 PEAK_F64_MFMA_TFLOPS = 78.6  # MI355X f64 matrix peak (AMD spec; the f64 RMVPE's conv engine, rmvpe64.hip)
+F64_MEASURED_TFLOPS = 39.0  # the MFMA-only f64 loop on every CU, real operands (scripts/conv64_dbg.hip, round 4)
 
 
 def pass_peak(passes):
@@ -80,6 +81,7 @@ class ConvProbe:
         self.orig = ops.conv1d
         self.orig_rb = ops.resblock_pair
         self.orig_64 = ops.conv64
+        self.orig_w64 = ops.wino64
         self.rec = []
 
     def __enter__(self):
@@ -126,15 +128,26 @@ class ConvProbe:
             valid = (Lout // wrap - 2) * (wrap - 2) if wrap else Lout
             self.rec.append((e0, e1, 2.0 * B * Co * Ci * K * valid, 2, 0.0, 64))
             return out
+        def wrapped_w64(x, v, Ci, Co, H, W, **k):
+            # the f64 RMVPE's Winograd convs (engine 2): the ALGORITHMIC FLOPs of the direct 3x3 conv they replace
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            out = self.orig_w64(x, v, Ci, Co, H, W, **k)
+            e1.record(s)
+            self.rec.append((e0, e1, 2.0 * k.get("B", 1) * Co * Ci * 9 * H * W, 2, 0.0, 64))
+            return out
         self.ops.conv1d = wrapped
         self.ops.resblock_pair = wrapped_rb
         self.ops.conv64 = wrapped_64
+        self.ops.wino64 = wrapped_w64
         return self
 
     def __exit__(self, *exc):
         self.ops.conv1d = self.orig
         self.ops.resblock_pair = self.orig_rb
         self.ops.conv64 = self.orig_64
+        self.ops.wino64 = self.orig_w64
 
     @staticmethod
     def _bytes(a, k, out):
@@ -592,7 +605,11 @@ def main():
                                "tflops": round(fl32 / max(ms32, 1e-9) / 1e9, 2), "peak": PEAK_F32_MFMA_TFLOPS},
                 "f64_engine": {"launches": n64, "kernel_ms": round(ms64, 3), "gflop": round(fl64 / 1e9, 1),
                                "tflops": round(fl64 / max(ms64, 1e-9) / 1e9, 2), "peak": PEAK_F64_MFMA_TFLOPS,
-                               "note": "the f64 RMVPE's convs (rmvpe64.hip conv64_kernel, split-K reduce included)"}}
+                               "measured_ceiling": F64_MEASURED_TFLOPS,
+                               "note": "the f64 RMVPE's convs (rmvpe64.hip: conv64_kernel with its split-K reduce, and "
+                                       "the Winograd F(4x4,3x3) convs at their direct-conv algorithmic FLOPs); peak = "
+                                       "the f64 matrix spec, measured_ceiling = what the chip sustains in f64 on real "
+                                       "operands (power-bound, DESIGN.md §4 conv64)"}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
