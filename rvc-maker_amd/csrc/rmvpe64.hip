@@ -540,7 +540,9 @@ int plan64(const rvc_conv64_args* a, C64& p, int& tile, dim3& grid, size_t& lds)
             const int nch = (int)((a->Ci * a->K + KC - 1) / KC);
             // the channel-aligned chunks: 3x3 convs only (RVC_C64_KC36=0: never)
             static const int kc36 = getenv("RVC_C64_KC36") ? atoi(getenv("RVC_C64_KC36")) : 1;
-            if (KC % 16 != 0 && (a->K != 9 || !kc36)) continue;
+            // (and not at 16 input channels: 4 chunks leave the pipeline no steady state -- the sweep's 16 -> 16
+            // level-0 conv ran 78.5 us with them against 74.7 with 16-deep chunks)
+            if (KC % 16 != 0 && (a->K != 9 || !kc36 || a->Ci < 32)) continue;
             const int span = span64(BN, maxoff, cmp ? W : 0);
             if ((int64_t)rows_max * span > 256 * nb64h(BN, KC) || span >= 65536) continue;
             const size_t l = (size_t)(2 * KC * (BM + 4) + 2 * (rows_max * (span + 1) + 1)) * 8 + 2 * KC * 4;
