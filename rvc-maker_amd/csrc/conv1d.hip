@@ -384,6 +384,15 @@ constexpr int X6_NI_MAX = 6;  // staged (position, 8-channel group) items per lo
 #define RVC_CONV_ABLATIONS 0
 #endif
 constexpr bool kAblations = RVC_CONV_ABLATIONS != 0;
+#ifndef X6_BPIN
+#define X6_BPIN 0
+#endif
+#ifndef X6_NOBAR
+#define X6_NOBAR 0  // profiling ablation only: no per-chunk barrier (races, wrong results)
+#endif
+#ifndef X6_PD8
+#define X6_PD8 0
+#endif
 
 // Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
@@ -653,7 +662,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         for (int i = 0; i < nck; ++i) {
             if (i + 1 < nck) xstore(pchunk(i + 1), xr[1], xs + ((i + 1) & 1) * bufsz);
             xload(pchunk(i + 2), xr[1]);
-            __syncthreads();
+            if constexpr (!X6_NOBAR) __syncthreads();
         }
       };
         // the loader body, once per form (a wave-uniform choice made once per block)
@@ -715,6 +724,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
             if (j + 1 < FN) bload(j + 1, bb[(j + 1) & 1]);
+            if constexpr (X6_BPIN) __builtin_amdgcn_sched_barrier(0);
             const uint4 (&bq)[NPL] = bb[j & 1];
             if (kAblations && (p.dbg & 2)) {
 #pragma unroll
@@ -757,7 +767,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     // (a 256-column tile, FN = 8, keeps its 64 accumulators by giving the ring 12 uint4)
     constexpr int PD_FIT = ((FN == 8 ? 12 : (NCW == 8 ? 18 : 24)) - (SA ? FM * FN : 0)) / (NPL * FM) - 1;
     constexpr int PD_MAX = x6_min_blocks<FM, FN, NCW, NP>() == 2 ? 1 : (NCW == 8 ? 2 : 4);
-    constexpr int PD = PD_FIT < 1 ? 1 : (PD_FIT > PD_MAX ? PD_MAX : PD_FIT);
+    constexpr int PD_SEL = PD_FIT < 1 ? 1 : (PD_FIT > PD_MAX ? PD_MAX : PD_FIT);
+    constexpr int PD = (FN == 8 && X6_PD8 > 0) ? X6_PD8 : PD_SEL;
     constexpr int NB = PD + 1;
     uint4 abuf[NB][NPL][FM];
     int li = 0, lt = 0;  // the next prefetch's logical (chunk index, tap index)
@@ -783,7 +794,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             if (s0 + u < nsteps) {
                 const int t = ct + rt < K ? ct + rt : ct + rt - K;
                 compute(t, xs + (ci & 1) * bufsz, abuf[u]);
-                if (ct == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
+                if (!X6_NOBAR && ct == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
             }
             if (++ct == K) { ct = 0; ++ci; }
         }
@@ -899,16 +910,29 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.xcd = xcd;
 }
 
+// compute units of the current device (read once per process: one device type per process)
+int num_cus() {
+    static const int n = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return cus;
+    }();
+    return n;
+}
+
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
 // per-thread override of the split-K target grid (rvc_conv1d_set_splitk_target; -1 = the process default)
 static thread_local int g_splitk_target = -1;
 
 void split_k(ConvParams& p, int64_t tiles, int nch, int per_cu = 2) {
-    // target grid (RVC_SPLITK_TILES, 0 = never split): 512 tiles = 2 per CU.  A kernel of which only one block fits
+    // target grid (RVC_SPLITK_TILES, 0 = never split): 256 tiles = 1 per CU (round 4, same box, alternated runs:
+    // per call 720-723 xRT at 512 -> 731-732 at 256, clip stream 906-908 -> 907-912).  A kernel of which only one block fits
     // a CU (the 8-compute-wave x6 tiles: 768 threads) targets 256: past one round of blocks a split only adds
     // rounds (ContentVec's K = 1 GEMMs, 30 s: 2304 x 768 x 1599 76 -> 49 us unsplit, 3072 x 768 95 -> 89;
     // RVC_X6_SPLIT_OCC=0 restores 512 for every tile)
-    static const int env_target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 512;
+    static const int env_target = getenv("RVC_SPLITK_TILES") ? atoi(getenv("RVC_SPLITK_TILES")) : 256;
     static const int occ_aware = getenv("RVC_X6_SPLIT_OCC") ? atoi(getenv("RVC_X6_SPLIT_OCC")) : 1;
     int target = g_splitk_target >= 0 ? g_splitk_target : env_target;
     if (occ_aware && per_cu == 1 && g_splitk_target < 0) target /= 2;
@@ -983,8 +1007,17 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         // 331 -> 307; end to end 820 -> 850 xRT.  The 6-pass form loses (its weight ring drops to 1 k-step
         // to fit 64 accumulators: C=128 K=11 883 -> 1113 us).
         static const int bn256 = getenv("RVC_X6_BN256") ? atoi(getenv("RVC_X6_BN256")) : 1;
+        // ... unless the 256-wide grid quantises worse onto the chip's one block per CU: C=256 at 30 s (2 x 150
+        // tiles, 1.17 rounds) runs 128-wide (2 x 300, 2.34 rounds): K=11 245-252 -> 226 us (conv_bench, round 4)
+        auto round_eff = [](int64_t t) {
+            const int64_t n = num_cus();
+            return (double)t / (double)(((t + n - 1) / n) * n);
+        };
+        const int64_t rows128 = (Cog + 127) / 128, nb = a->B * a->nphase;
+        const bool fills256 = round_eff(rows128 * ((ncols + 255) / 256) * nb) >=
+                              round_eff(rows128 * ((ncols + 127) / 128) * nb) - 0.05;
         if (Cog > 64 && w8 && bn256 && a->stride == 1 && 255 + max_tap_off(a) + 1 <= 64 * X6_NI_MAX - 2 &&
-            (bn256 == 2 || np == RVC_ARITH_F16X3))
+            (bn256 == 2 || np == RVC_ARITH_F16X3) && (fills256 || bn256 == 3))
             cfg = {2, 8, 4, 2, true};
         else if (Cog > 64 && w8) cfg = {2, 4, 4, 2, true};  // 128 x 128 on 8 compute waves
         else if (Cog > 64) cfg = {4, 4, 2, 2, true};   // 128 x 128 on 4 compute waves

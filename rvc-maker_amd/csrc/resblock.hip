@@ -38,6 +38,9 @@ struct RbParams {
 #ifndef RB_YREG
 #define RB_YREG 1  // accumulate operands loaded at S1 into registers (else in the epilogue)
 #endif
+#ifndef RB_BPIN
+#define RB_BPIN 1  // next fragment's B reads pinned ahead of this one's MFMAs (rb_bench: pairs -3.5 %)
+#endif
 #ifndef RB_FM_
 #define RB_FM_ 1
 #define RB_FN_ 4
@@ -243,6 +246,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
             if (j + 1 < FN && cg * FN + j + 1 < nfrag) bload(j + 1, bb[(j + 1) & 1]);
+            if constexpr (RB_BPIN) __builtin_amdgcn_sched_barrier(0);
             if (cg * FN + j < nfrag) {
                 const uint4 (&bq)[NPL] = bb[j & 1];
                 constexpr int PA[6] = {0, 0, 1, 0, 1, 2};

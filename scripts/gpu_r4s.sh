@@ -1,12 +1,9 @@
 #!/bin/bash
-# Winograd (unfused, per-thread input transform): tests, RMVPE time, bench.
+# A/B: split-K target grid (RVC_SPLITK_TILES: 512 default, 128, 0 = never split) on the clip stream.
 set -o pipefail
-export TMPDIR=/tmp
 O=gpurun_out/r4s; mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k "wino or conv64 or bordered" > $O/t_ops.log 2>&1 || { tail -30 $O/t_ops.log; exit 1; }
-tail -1 $O/t_ops.log
-timeout -k 10 200 python -u scripts/rmvpe_prof.py f64 5 > $O/rm.log 2>&1 || { tail $O/rm.log; exit 1; }
-tail -1 $O/rm.log
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_rmvpe.py tests/test_gpu_native.py tests/test_gpu_batch.py > $O/t_rm.log 2>&1 || { tail -30 $O/t_rm.log; exit 1; }
-tail -1 $O/t_rm.log
-TAG=r4s/ab R=2 VARIANTS="wino:RVC_X=1 off:RVC_RMVPE_WINO=0 fronts2q8:RVC_STREAM_FRONTS=2,GPU_MAX_HW_QUEUES=8 q8:GPU_MAX_HW_QUEUES=8" ./scripts/gpu_ab_env.sh
+run() { RVC_SPLITK_TILES=$2 timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/$1.log 2>&1; }
+run b1 512 && run z1 0 && run q1 128 && run b2 512 && run z2 0 && run q2 128
+rc=$?
+for f in b1 z1 q1 b2 z2 q2; do grep '"metric"' $O/$f.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$f', d['value'], d['per_call'])"; done
+exit $rc

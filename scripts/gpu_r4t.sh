@@ -1,7 +1,12 @@
 #!/bin/bash
-# K = 1 GEMMs on the f32 MFMA engine vs the split-bf16 engine: gemm_bench shapes and the clip stream.
+# A/B on one box: new defaults (split-K target 256, 128-wide split-fp16 tiles when the 256-wide grid
+# quantises worse) vs the previous ones (RVC_SPLITK_TILES=512 RVC_X6_BN256=3).
 set -o pipefail
-export TMPDIR=/tmp
 O=gpurun_out/r4t; mkdir -p $O
-for k1 in 1 0; do RVC_X6_K1=$k1 timeout -k 10 200 python -u scripts/gemm_bench.py > $O/gemm_k1_$k1.log 2>&1 || { tail $O/gemm_k1_$k1.log; exit 1; }; echo "k1=$k1"; tail -8 $O/gemm_k1_$k1.log; done
-TAG=r4t/ab R=2 VARIANTS="x6:RVC_X=1 f32k1:RVC_X6_K1=0" ./scripts/gpu_ab_env.sh
+old() { RVC_SPLITK_TILES=512 RVC_X6_BN256=3 timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/$1.log 2>&1; }
+new() { timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/$1.log 2>&1; }
+timeout -k 10 300 python -u scripts/conv_bench.py --reps 10 --check > $O/conv.log 2>&1 && \
+old o1 && new n1 && old o2 && new n2 && old o3 && new n3
+rc=$?; grep "C=\|total" $O/conv.log
+for f in o1 n1 o2 n2 o3 n3; do grep '"metric"' $O/$f.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$f', d['value'], d['per_call'])"; done
+exit $rc
