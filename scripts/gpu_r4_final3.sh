@@ -3,7 +3,7 @@
 # stamped with the kernel-source hash, then the default bench line with the traffic filled in.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/final5; mkdir -p $O
+O=gpurun_out/${TAG:-final6}; mkdir -p $O
 timeout -k 10 2400 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread > $O/gpu_suite.log 2>&1 || { tail -40 $O/gpu_suite.log; exit 1; }
 tail -2 $O/gpu_suite.log
 timeout -k 10 600 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
