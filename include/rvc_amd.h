@@ -111,8 +111,8 @@ int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_
  * kernel alone (bench.py's roofline probe).  NULL (the default) turns it off. */
 void rvc_conv1d_set_probe_event(void* hip_event);
 /* Split-K policy (this host thread): the library splits a conv's k range over blocks while its tile grid is
- * below `target` tiles (default 512 = 2 per CU, or RVC_SPLITK_TILES); 0 = never split, -1 = back to the
- * default.  Returns the previous setting.  Results depend on it at f32 rounding level (the split changes the
+ * below `target` tiles (default 256 = 1 per CU, halved for tiles of which one block fills a CU; or
+ * RVC_SPLITK_TILES); 0 = never split, -1 = back to the default.  Returns the previous setting.  Results depend on it at f32 rounding level (the split changes the
  * summation order). */
 int rvc_conv1d_set_splitk_target(int target);
 /* A stream restricted to the CUs set in mask (nwords 32-bit words, bit i = CU i), and its release. */

@@ -2,7 +2,7 @@
 # PMC traffic passes (stamped with the kernel-source hash), then the default bench line with the traffic filled in.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/final4b; mkdir -p $O
+O=gpurun_out/${TAG:-final7}; mkdir -p $O
 bash scripts/pmc_traffic.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
 cp gpurun_out/pmc_traffic/summary.json $O/pmc_traffic.json
 cp gpurun_out/pmc_traffic/summary.json profiles/r4_pmc_traffic.json
