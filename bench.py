@@ -7,12 +7,14 @@ output waveforms gathered to rank 0 over RCCL).
 
 Default: a clip stream (VC.pipeline_device_stream) -- K steps are K clips per GPU, clip k+1's front end
 (filtfilt, RMVPE, ContentVec) running on its own streams under clip k's synthesizer; the line also carries
-"per_call", the same K clips as one finished pipeline_device call each.
+"per_call", the same K clips as one finished pipeline_device call each.  Each clip's output waveform is copied
+to pinned host memory inside the timed region (host-visible output; --hbm-output leaves it in HBM).
 
 --utterances U (BASELINE configs[3], SURVEY §8(d) cfg 4): a fixed job of U utterances of --seconds each (1 h =
 120 x 30 s), sharded longest-first over the ranks (rvc_amd.shard.shard_utterances), each rank's share issued as
 one clip stream, the output waveforms gathered to rank 0 by grouped send / recv (RCCL over xGMI); a step is the
-whole job, "scaling": "strong".
+whole job, "scaling": "strong".  Utterance i draws its noise with seed 17 + i (shard.convert_utterances), so the
+gathered waveforms are the same bits at every world size (tests/test_gpu_shard.py).
 
 --gpus N without WORLD_SIZE in the environment starts N ranks itself (torch.distributed.run as a
 child process, one rank per GPU); under an external launcher WORLD_SIZE must equal N.
@@ -280,24 +282,30 @@ def pmc_traffic(kernel_family="x6"):
     return None, "no PMC summary committed"
 
 
-def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
-    """SURVEY §8(d) cfg 3 index shape: IVF2564,Flat over 100k 768-d vectors, nprobe 1.  Vectors are drawn
-    around 2564 seeded centres (a trained IVF index has balanced lists; uniform Gaussians in 768-d would
-    pile most vectors onto a few "hub" centroids); the centres are the IVF centroids."""
+def synthetic_ivf(dev, n=100_000, nlist=2564, seed=77):
+    """SURVEY §8(d) cfg 3 index shape as a host IVFFlatIndex: IVF2564,Flat over 100k 768-d vectors, nprobe 1.
+    Vectors are drawn around 2564 seeded centres (a trained IVF index has balanced lists; uniform Gaussians in
+    768-d would pile most vectors onto a few "hub" centroids); the centres are the IVF centroids.  The list
+    assignment (nearest centre) runs on ``dev`` (host-side index build, never timed)."""
     from rvc_amd.faiss_index import IVFFlatIndex
-    from rvc_amd.retrieval import IVFFlatDevice
     rng = np.random.default_rng(seed)
     cent = rng.standard_normal((nlist, 768)).astype(np.float32)
     xb = (cent[rng.integers(0, nlist, n)] + 0.35 * rng.standard_normal((n, 768))).astype(np.float32)
     x = torch.from_numpy(xb).to(dev)
     c = torch.from_numpy(cent).to(dev)
-    assign = torch.cdist(x, c).argmin(1).cpu().numpy()  # host-side index build (not timed)
+    assign = torch.cdist(x, c).argmin(1).cpu().numpy()
     order = np.argsort(assign, kind="stable")
     sizes = np.bincount(assign, minlength=nlist)
     off = np.concatenate([[0], np.cumsum(sizes)])
     codes = [xb[order[off[i]:off[i + 1]]] for i in range(nlist)]
     ids = [order[off[i]:off[i + 1]].astype(np.int64) for i in range(nlist)]
-    return IVFFlatDevice(IVFFlatIndex(768, cent, codes, ids, nprobe=1, ntotal=n), dev)
+    return IVFFlatIndex(768, cent, codes, ids, nprobe=1, ntotal=n)
+
+
+def synthetic_index(dev, n=100_000, nlist=2564, seed=77):
+    """synthetic_ivf uploaded to the device (retrieval.IVFFlatDevice)."""
+    from rvc_amd.retrieval import IVFFlatDevice
+    return IVFFlatDevice(synthetic_ivf(dev, n, nlist, seed), dev)
 
 
 def cpu_calibration():
@@ -389,6 +397,9 @@ def main():
     ap.add_argument("--utterances", type=int, default=0,
                     help="> 0: BASELINE configs[3] -- a fixed job of U utterances sharded over the ranks (strong "
                          "scaling; a step = the whole job)")
+    ap.add_argument("--hbm-output", action="store_true",
+                    help="leave each output waveform in HBM (no per-clip D2H copy to pinned host memory in the timed "
+                         "region; the default copies each clip's waveform to the host as VC.pipeline's .cpu() does)")
     ap.add_argument("--index-rate", type=float, default=0.0,
                     help="> 0: FAISS IVF-Flat retrieval over a synthetic index (SURVEY §8d cfg 3 shape)")
     args = ap.parse_args()
@@ -430,19 +441,31 @@ def main():
         cap = args.f0.split("-", 1)[1]
         vc.crepe[cap] = CrepeAMD(synthetic.crepe_state_dict(1240, cap), cap, dev)
     # inputs resident in HBM before the timed region: one distinct clip per chunk
-    mine = None
-    if args.utterances > 0:  # cfg 4: this rank's share of the whole job (seed = 1000 + utterance index, §8(d))
+    mine = shards = None
+    if args.utterances > 0:  # cfg 4: this rank's share of the whole job (input seed = 1000 + utterance index, §8(d))
         from rvc_amd.shard import shard_utterances
         if args.graph or args.batch > 1 or args.chunks > 1:
             raise SystemExit("bench.py: --utterances runs the clip stream (no --graph / --batch / --chunks)")
-        mine = shard_utterances([int(args.seconds * 16000)] * args.utterances, world)[rank]
+        shards = shard_utterances([int(args.seconds * 16000)] * args.utterances, world)
+        mine = shards[rank]
         clips = [torch.from_numpy(synthetic.synthetic_audio(args.seconds, seed=1000 + i)).to(dev) for i in mine]
         args.stream = True
     else:
         clips = [torch.from_numpy(synthetic.synthetic_audio(args.seconds, seed=1000 + 97 * rank + c)).to(dev)
                  for c in range(max(1, args.chunks))]
-    audio_dev = clips[0]
-    vc.seed = 17 + rank
+    audio_dev = clips[0] if clips else None
+    # noise seeds: clip k of a rank's stream draws seed vc.seed + k; ranks start far apart so no two clips of the
+    # job share noise (cfg 4 keys each utterance's seed to its global index instead: shard.convert_utterances)
+    vc.seed = 17 + 1_000_003 * rank
+    host_visible = not args.hbm_output and mine is None
+    out_cap = int(args.seconds * args.sr) + args.sr  # >= one clip's output samples
+    host_bufs = []
+
+    def host_buffers(n):
+        """n pinned host buffers for the clips' waveforms (the reference signature's .cpu(), convert.py:455)."""
+        while len(host_bufs) < n:
+            host_bufs.append(torch.empty(out_cap, dtype=torch.float32, pin_memory=True))
+        return host_bufs[:n]
 
     clip_graph = None
     if args.graph:
@@ -468,9 +491,12 @@ def main():
                 outs.append(clip_graph(clip).clone() if len(clips) > 1 else clip_graph(clip))
             else:
                 outs.append(vc.pipeline_device(hub, net_g, 0, clip, 0, "v2", 0.33, index, args.index_rate, args.f0))
+        if host_visible:  # each waveform to pinned host memory, as VC.pipeline hands it back
+            for o, hb in zip(outs, host_buffers(len(outs))):
+                hb[: o.numel()].copy_(o, non_blocking=True)
         if dist is not None:
             # the path's only collective: output waveforms gathered to rank 0 (RCCL over xGMI)
-            got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0)
+            got = gather_waveforms(outs, dist, dst=0)
             if got is not None:
                 gathered[0] += sum(len(g) for g in got)
         return outs[-1]
@@ -479,22 +505,20 @@ def main():
         # one stream over nsteps x chunks clips: every clip's whole pass is issued inside the call, and the
         # call returns after the last clip's output is ordered on this stream
         if mine is not None:  # cfg 4: a step is the whole job -- this rank's utterances, then the gather
+            from rvc_amd.shard import convert_utterances
             last = None
             for _ in range(nsteps):
-                outs = vc.pipeline_device_stream(hub, net_g, 0, clips, 0, "v2", 0.33, index, args.index_rate,
-                                                 args.f0) if clips else []
-                if dist is not None:
-                    got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0,
-                                           stats=p2p)
-                    if got is not None:
-                        gathered[0] += sum(len(g) for g in got)
-                last = outs[-1] if outs else last
+                got = convert_utterances(vc, hub, net_g, 0, clips, shards, dist, 0, "v2", 0.33, index, args.index_rate,
+                                         args.f0, seed=17, stats=p2p)
+                if dist is not None and got is not None:
+                    gathered[0] += len(got)
+                last = got[-1] if got else last
             return last
         order = [clips[i % len(clips)] for i in range(nsteps * len(clips))]
         outs = vc.pipeline_device_stream(hub, net_g, 0, order, 0, "v2", 0.33, index, args.index_rate, args.f0,
-                                         batch=args.batch)
+                                         batch=args.batch, host_out=host_buffers(len(order)) if host_visible else None)
         if dist is not None:
-            got = gather_waveforms(outs if backend == "nccl" else [o.cpu() for o in outs], dist, dst=0)
+            got = gather_waveforms(outs, dist, dst=0)
             if got is not None:
                 gathered[0] += sum(len(g) for g in got)
         return outs[-1]
@@ -502,6 +526,8 @@ def main():
     p2p = {}
 
     gathered = [0]
+    if host_visible:  # pinned buffers allocated before the timed region
+        host_buffers(max(args.steps, args.warmup, 1) * len(clips))
 
     if args.stream:
         if args.warmup:
@@ -619,6 +645,10 @@ def main():
                 "collective": ("none" if world == 1 else
                                "RCCL gather over xGMI" if backend == "nccl" else "gloo (ranks share a GPU)"),
                 "waveforms_gathered_per_step": gathered_per_step,
+                "output": ("host-visible: each clip's waveform copied to pinned host memory inside the timed region "
+                           "(the reference signature's .cpu(), SURVEY §8(d))" if host_visible else
+                           "HBM-resident (gathered to rank 0's device)" if mine is not None else
+                           "HBM-resident (--hbm-output)"),
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "strong" if mine is not None else "weak", "vs_baseline": None,
                 "dtype": DTYPES[args.precision],

@@ -84,17 +84,24 @@ static void parse_tensor(const char* obj, const char* data, size_t data_size, rv
     const char* s = strstr(obj, "\"shape\"");
     const char* o = strstr(obj, "\"data_offsets\"");
     if (!d || !s || !o) DIE("bad tensor entry");
+    const char* colon = strchr(d + 7, ':');
+    if (!colon || *skip_ws(colon + 1) != '"') DIE("bad dtype");
     char dt[16];
-    read_str(skip_ws(strchr(d + 7, ':') + 1), dt, sizeof(dt));
+    read_str(skip_ws(colon + 1), dt, sizeof(dt));
     if (!strcmp(dt, "F16")) prm->dtype = RVC_DT_F16;
     else if (!strcmp(dt, "F32")) prm->dtype = RVC_DT_F32;
     else if (!strcmp(dt, "F64")) prm->dtype = RVC_DT_F64;
     else DIE("unsupported dtype %s", dt);
-    const char* p = strchr(s, '[') + 1;
+    const char* p = strchr(s, '[');
+    if (!p) DIE("bad shape");
+    ++p;
     prm->ndim = 0;
     while (*(p = skip_ws(p)) != ']') {
         if (prm->ndim == 4) DIE("more than 4 dims");
-        prm->shape[prm->ndim++] = strtoll(p, (char**)&p, 10);
+        char* q;
+        prm->shape[prm->ndim++] = strtoll(p, &q, 10);
+        if (q == p) DIE("bad shape");
+        p = q;
         p = skip_ws(p);
         if (*p == ',') ++p;
     }
@@ -143,9 +150,11 @@ static Model load_safetensors(const char* path, const char* meta_key, char** kee
         p = skip_ws(p);
         if (*p == '}' || !*p) break;
         char key[256];
+        if (*p != '"') DIE("bad safetensors header");
         p = read_str(p, key, sizeof(key));
         p = skip_ws(p);
-        ++p; /* ':' */
+        if (*p != ':') DIE("bad safetensors header");
+        ++p;
         p = skip_ws(p);
         const char* end = skip_value(p);
         size_t len = (size_t)(end - p);
@@ -156,12 +165,17 @@ static Model load_safetensors(const char* path, const char* meta_key, char** kee
             char pat[128];
             snprintf(pat, sizeof(pat), "\"%s\"", meta_key ? meta_key : "");
             const char* c = meta_key ? strstr(obj, pat) : NULL;
+            const char* colon = c ? strchr(c + strlen(pat), ':') : NULL;
+            if (c && (!colon || *skip_ws(colon + 1) != '"')) DIE("bad metadata %s", meta_key);
             if (c) {
                 char val[1024];
-                read_str(skip_ws(strchr(c + strlen(pat), ':') + 1), val, sizeof(val));
+                read_str(skip_ws(colon + 1), val, sizeof(val));
                 char* q = val;
                 while (*q && m.ncfg < 64) {
-                    m.cfg[m.ncfg++] = (int)strtol(q, &q, 10);
+                    char* e;
+                    m.cfg[m.ncfg++] = (int)strtol(q, &e, 10);
+                    if (e == q) DIE("bad metadata %s: not a list of ints", meta_key);
+                    q = e;
                     while (*q == ' ') ++q;
                 }
             }

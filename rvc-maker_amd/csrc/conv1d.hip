@@ -390,6 +390,9 @@ constexpr bool kAblations = RVC_CONV_ABLATIONS != 0;
 #ifndef X6_NOBAR
 #define X6_NOBAR 0  // profiling ablation only: no per-chunk barrier (races, wrong results)
 #endif
+#if X6_NOBAR && !RVC_CONV_ABLATIONS
+#error "X6_NOBAR races (wrong results): only in a -DRVC_CONV_ABLATIONS=1 profiling build"
+#endif
 #ifndef X6_PD8
 #define X6_PD8 0
 #endif

@@ -2,6 +2,7 @@
 // RMVPE (rvc_amd/rmvpe.py) loaded from their checkpoints' named host arrays and run natively with the same
 // launches, pass sets and order as the Python models -- bit-identical to them on the same weights and
 // constants.  Scratch per model is sized by a dry run of the forward (Scratch / RUN in model_common.h).
+#include "host_f0file.h"
 #include "model_common.h"
 
 using namespace rvcm;
@@ -1308,50 +1309,11 @@ int vc_segments(const VcPlan& p, const std::vector<int64_t>& opt_ts, std::vector
     return RVC_OK;
 }
 
-// convert.py:316-318 on the host: the f0 file (rows "time,f0", f32 as read_f0_file gives them) resampled to 100
-// frames/s by numpy's np.interp (f64, its branch structure), n = np.round((max t - min t) * 100 + 1) in f32
+// convert.py:316-318 on the host (host_f0file.h, plain C++: also built with -fsanitize on the CPU by
+// tests/test_c_host_cpu.py)
 int f0_file_rep(const float* rows, int64_t nrows, std::vector<double>& rep) {
-#pragma clang fp contract(off)
     MCHECK(rows && nrows >= 1, "rvc_vc_convert: empty f0 file");
-    float tmin = rows[0], tmax = rows[0];
-    for (int64_t i = 1; i < nrows; ++i) {
-        tmin = rows[2 * i] < tmin ? rows[2 * i] : tmin;
-        tmax = rows[2 * i] > tmax ? rows[2 * i] : tmax;
-    }
-    const float span = tmax - tmin;
-    const float v = span * 100.f + 1.f;
-    const int64_t n = (int16_t)rintf(v);  // np.round (half to even), astype(np.int16)
-    rep.assign(n > 0 ? n : 0, 0.0);
-    std::vector<double> xp(nrows), fp(nrows);
-    for (int64_t i = 0; i < nrows; ++i) {
-        xp[i] = (double)(rows[2 * i] * 100.f);  // inp_f0[:, 0] * 100 is f32, np.interp takes it as f64
-        fp[i] = (double)rows[2 * i + 1];
-    }
-    for (int64_t k = 0; k < (int64_t)rep.size(); ++k) {
-        const double x = (double)k;
-        if (x < xp[0]) {
-            rep[k] = fp[0];
-            continue;
-        }
-        if (x > xp[nrows - 1]) {
-            rep[k] = fp[nrows - 1];
-            continue;
-        }
-        int64_t j = 0;  // xp[j] <= x < xp[j + 1] (binary search over a sorted xp)
-        int64_t lo = 0, hi = nrows - 1;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi + 1) / 2;
-            if (xp[mid] <= x) lo = mid;
-            else hi = mid - 1;
-        }
-        j = lo;
-        if (j == nrows - 1 || xp[j] == x) {
-            rep[k] = fp[j];
-            continue;
-        }
-        const double slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]);
-        rep[k] = slope * (x - xp[j]) + fp[j];
-    }
+    MCHECK(rvc_host::f0_file_interp(rows, nrows, rep) == 0, "rvc_vc_convert: f0 file times not finite or too long");
     return RVC_OK;
 }
 

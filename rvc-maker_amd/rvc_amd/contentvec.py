@@ -155,21 +155,31 @@ class ContentVecAMD:
     @classmethod
     def from_transformers(cls, path: str, device: str = "cuda") -> "ContentVecAMD":
         """``HubertModelWithFinalProj.from_pretrained(path)`` (main/library/utils.py:157-165) without transformers:
-        ``path`` is the model directory (config.json + model.safetensors, or *.safetensors shards) or a
-        .safetensors file with config.json beside it."""
-        import glob
+        ``path`` is the model directory (config.json + model.safetensors, or the shards that
+        model.safetensors.index.json lists, as from_pretrained reads them) or a .safetensors file with config.json
+        beside it.  A tensor named by two files raises."""
         import json
         import os
         from safetensors.torch import load_file
         d = path if os.path.isdir(path) else os.path.dirname(path)
-        files = [path] if not os.path.isdir(path) else sorted(glob.glob(os.path.join(d, "*.safetensors")))
-        if not files:
-            raise FileNotFoundError(f"no .safetensors weights under {path}")
+        if not os.path.isdir(path):
+            files = [path]
+        elif os.path.exists(os.path.join(d, "model.safetensors")):
+            files = [os.path.join(d, "model.safetensors")]
+        elif os.path.exists(os.path.join(d, "model.safetensors.index.json")):
+            with open(os.path.join(d, "model.safetensors.index.json")) as f:
+                files = [os.path.join(d, fn) for fn in sorted(set(json.load(f)["weight_map"].values()))]
+        else:
+            raise FileNotFoundError(f"no model.safetensors or model.safetensors.index.json under {path}")
         with open(os.path.join(d, "config.json")) as f:
             cfg = json.load(f)
         sd = {}
         for fn in files:
-            sd.update(load_file(fn))
+            part = load_file(fn)
+            dup = sd.keys() & part.keys()
+            if dup:
+                raise ValueError(f"{fn}: tensors {sorted(dup)[:4]} already loaded from another file")
+            sd.update(part)
         m = cls({"cfg": {"model": hf_config_to_fairseq(cfg)}, "model": hf_to_fairseq(sd)}, device)
         m.embed_suffix = ".safetensors"
         return m

@@ -38,7 +38,10 @@ class VoiceConverterAMD:
         self.sid = sid
         self.use_f0 = use_f0
         self.sample_rate = 16000
-        self.suffix, self.embed_suffix = ".pth", ".pt"
+        self.suffix = ".pth"
+        # the loaded embedder's suffix (load_embedders_model returns it, utils.py:131-165); convert_audio checks it
+        # against its embedders_mode argument
+        self.embed_suffix = getattr(hubert_model, "embed_suffix", ".pt")
 
     def convert_audio(self, audio_input_path, audio_output_path, index_path="", embedder_model="contentvec_base",
                       pitch=0, f0_method="rmvpe", index_rate=0.5, volume_envelope=1, protect=0.5, hop_length=64,
@@ -53,6 +56,10 @@ class VoiceConverterAMD:
                 raise NotImplementedError("formant shifting is not on the MI355X path")
             if export_format != "wav":
                 raise NotImplementedError("only WAV export (no soundfile / ffmpeg in this build)")
+            embed_suffix = embed_suffix_of(embedders_mode)
+            if embed_suffix != self.embed_suffix:
+                raise ValueError(f"embedders_mode {embedders_mode!r} reads a {embed_suffix} embedder, but the loaded "
+                                 f"model is a {self.embed_suffix} one")
             audio = audio_io.load_audio(audio_input_path, self.sample_rate)
             audio_max = np.abs(audio).max() / 0.95
             if audio_max > 1:
@@ -70,7 +77,7 @@ class VoiceConverterAMD:
                     f0_method=f0_method, file_index=index, index_rate=index_rate, pitch_guidance=self.use_f0,
                     filter_radius=filter_radius, volume_envelope=volume_envelope, version=self.version,
                     protect=protect, hop_length=hop_length, f0_autotune=f0_autotune,
-                    f0_autotune_strength=f0_autotune_strength, suffix=self.suffix, embed_suffix=self.embed_suffix,
+                    f0_autotune_strength=f0_autotune_strength, suffix=self.suffix, embed_suffix=embed_suffix,
                     f0_file=f0_file, f0_onnx=f0_onnx, pbar=pbar)))
             out = edges.restore(converted, total_len=len(audio), dtype=converted[0][2].dtype) if split_audio \
                 else converted[0][2]
@@ -84,6 +91,16 @@ class VoiceConverterAMD:
         except Exception as e:  # noqa: BLE001 -- the reference logs and returns (convert.py:520-523)
             log.error(f"convert_audio: {e}")
             return None
+
+
+def embed_suffix_of(embedders_mode):
+    """main/library/utils.py:131-165: the suffix load_embedders_model returns for a mode ("fairseq" -> ".pt",
+    "transformers" / "spin" -> ".safetensors"); ONNX embedders are not on the MI355X path."""
+    if embedders_mode == "fairseq":
+        return ".pt"
+    if embedders_mode in ("transformers", "spin"):
+        return ".safetensors"
+    raise NotImplementedError(f"embedders_mode {embedders_mode!r}: fairseq and transformers are on the MI355X path")
 
 
 def batch_files(input_path, export_format="wav"):

@@ -60,10 +60,22 @@ class _CuMaskedStream:
             ops.check(ops._lib.load().rvc_stream_destroy(h), "stream_destroy")
 
 
-def _close_streams(owned):
-    """VC's finalizer (weakref.finalize: on close(), when the VC is collected, or at interpreter exit)."""
+def _close_streams(owned, strict=False):
+    """VC's finalizer (weakref.finalize: when the VC is collected or at interpreter exit) and ``VC.close``.  Only an
+    explicit ``close()`` raises; the finalizer and ``__exit__`` under an exception log a failed release (e.g. after
+    a sticky GPU error) and carry on, so they never bury the original failure."""
+    first = None
     while owned:
-        owned.pop().close()
+        try:
+            owned.pop().close()
+        except Exception as e:  # noqa: BLE001
+            if strict and first is None:
+                first = e
+            else:
+                import logging
+                logging.getLogger(__name__).warning(f"VC stream release failed: {e}")
+    if first is not None:
+        raise first
 
 
 class Config:
@@ -98,7 +110,7 @@ class VC:
         # library-created streams (CU-masked) this VC owns: destroyed by close() / at exit, after their work
         self._owned = []
         self._finalizer = weakref.finalize(self, _close_streams, self._owned)
-        self.embed_suffix = None  # pipeline()'s embed_suffix (convert.py:390); None = the model's own
+        self.embed_suffix = None  # pipeline()'s embed_suffix during that call (convert.py:390); None = the model's own
         self.crepe = dict(crepe or {})  # capacity -> CrepeAMD (loaded on first use otherwise)
         self.noise_fn = None  # parity hook: noise_fn(seg, "z"|"sine", shape) -> device tensor
         self.seed = 0
@@ -317,7 +329,7 @@ class VC:
         return outs
 
     def pipeline_device_stream(self, model, net_g, sid, audios, pitch, version, protect, index=None, index_rate=0.0,
-                               f0_method="rmvpe", batch=1, events=None):
+                               f0_method="rmvpe", batch=1, events=None, seeds=None, host_out=None):
         """``pipeline_device`` over a sequence of clips (the file / chunk loops of convert.py:129-135 and
         :506-507) with clip k+1's front end -- filtfilt, f0 on the side stream, ContentVec features -- issued
         on a front stream while clip k's synthesizer runs on a back stream.  The two are independent, so the
@@ -327,13 +339,18 @@ class VC:
         equal-length clips at once (``pipeline_device_batch``'s batched RMVPE and ContentVec), group g+1's
         under group g's synthesizer, which runs as B-clip launches (``voice_conversion_batch_device``).
 
-        Clip k draws its noise with seed ``self.seed + k`` (as ``pipeline_device_batch``): at batch 1 its
+        Clip k draws its noise with seed ``seeds[k]`` when ``seeds`` is given (a sharded job keys it to the global
+        utterance index, so the output does not depend on the rank or world size), else ``self.seed + k`` (as
+        ``pipeline_device_batch``): at batch 1 its
         waveform is bit-identical to ``pipeline_device`` of that clip at ``seed = self.seed + k`` -- every
         launch is the same launch on the same data, only its stream differs (batched groups: up to the
         batched launches' split-K / split-KV order, as ``pipeline_device_batch``).  Clips must fit one segment (N + window
         <= t_max, 41 s; longer inputs go through ``pipeline_device``'s host quiet-point search).  Returns the
         list of device waveforms, ordered on the caller's current stream.  ``events`` (a list) collects
-        timing events (role, group, torch.cuda.Event) at each group's front / back start and end."""
+        timing events (role, group, torch.cuda.Event) at each group's front / back start and end.  ``host_out``
+        (a list of pinned host f32 tensors, one per clip, each at least the clip's output length) receives each
+        waveform as it is finished: a non-blocking copy on the caller's stream after that clip's synthesizer,
+        overlapping the next clips' work (the reference's ``.cpu()`` of each output, convert.py:455)."""
 
         def mark(role, g, stream):
             if events is not None:
@@ -359,6 +376,20 @@ class VC:
         if self._ws is None:
             self._ws = torch.zeros(4, dtype=torch.int32, device=dev)
         seed0, tp = self.seed, self.t_pad_tgt
+        if seeds is not None and len(seeds) != len(audios):
+            raise ValueError("pipeline_device_stream: one seed per clip")
+        if host_out is not None and len(host_out) != len(audios):
+            raise ValueError("pipeline_device_stream: one host buffer per clip")
+        seed_of = (lambda k: int(seeds[k])) if seeds is not None else (lambda k: seed0 + k)
+
+        def emit(out):
+            outs.append(out)
+            if host_out is not None:  # D2H of this clip on the caller's stream, behind its synthesizer only
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                caller.wait_event(ev)
+                with torch.cuda.stream(caller):
+                    host_out[len(outs) - 1][: out.numel()].copy_(out, non_blocking=True)
 
         def issue_front(group, g):
             """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event).
@@ -418,23 +449,23 @@ class VC:
                         for t in it:
                             t.record_stream(back)
                     if len(items) > 1 and self.SYNTH_BATCH:
-                        seeds = [seed0 + len(outs) + b for b in range(len(items))]
+                        gseeds = [seed_of(len(outs) + b) for b in range(len(items))]
                         ob = self.voice_conversion_batch_device(model, net_g, sid, items, version, protect, index,
-                                                                index_rate, seeds)
+                                                                index_rate, gseeds)
                         for b in range(len(items)):
                             out = ob[b, tp: ob.shape[1] - tp]
                             ops.peak_normalize(out, self._ws)
-                            outs.append(out)
+                            emit(out)
                         items = []
                     for xp, coarse, pitchf, feats in items:
                         p_len = xp.numel() // self.window
-                        self.seed = seed0 + len(outs)
+                        self.seed = seed_of(len(outs))
                         o = self.voice_conversion_device(model, net_g, sid, xp, coarse[:p_len], pitchf[:p_len],
                                                          version, protect, 0, feats=feats, index=index,
                                                          index_rate=index_rate)
                         out = o[tp: o.numel() - tp]
                         ops.peak_normalize(out, self._ws)
-                        outs.append(out)
+                        emit(out)
                     mark("back_end", g, back)
         finally:
             self.seed = seed0
@@ -481,19 +512,22 @@ class VC:
                 self._streams[key] = torch.cuda.Stream(device=device, priority=prio)
         return self._streams[key]
 
-    def close(self):
+    def close(self, strict=True):
         """Wait for and destroy the streams the library created for this VC (also done when the VC is collected
-        and at interpreter exit); the VC creates new ones if used again."""
-        self._finalizer()
+        and at interpreter exit); the VC creates new ones if used again.  ``strict`` False logs a failed release
+        instead of raising."""
+        self._finalizer.detach()
+        owned = self._owned
         self._streams = {}
         self._owned = []
         self._finalizer = weakref.finalize(self, _close_streams, self._owned)
+        _close_streams(owned, strict=strict)
 
     def __enter__(self):
         return self
 
-    def __exit__(self, *exc):
-        self.close()
+    def __exit__(self, exc_type, *exc):
+        self.close(strict=exc_type is None)  # under an exception, never replace it with a release failure
 
     # The synthesizer (back) stream is created through hipExtStreamCreateWithCUMask (RVC_BACK_CU_MASK:
     # "mod:m:r", "top:n" or "none").  What a mask does was probed in round 4 (scripts/cu_mask_probe.hip,
@@ -616,15 +650,20 @@ class VC:
             raise NotImplementedError("no-f0 models: the reference's no-f0 Generator is not buildable (SURVEY §0)")
         if suffix != ".pth" or embed_suffix not in (".pt", ".safetensors"):
             raise NotImplementedError("ONNX models are not on the MI355X path")
-        self.embed_suffix = embed_suffix  # convert.py:390
         if pbar is not None:
             pbar.update(1)
         inp_f0 = read_f0_file(f0_file)
         if pbar is not None:
             pbar.update(1)
-        out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
-                                   protect, index, index_rate, f0_method, bool(f0_autotune), f0_autotune_strength,
-                                   inp_f0, volume_envelope)
+        # convert.py:390 keeps the suffix on the VC; here it holds for this call only, so a later pipeline_device /
+        # clip-stream call reads the model's own suffix again
+        prev, self.embed_suffix = self.embed_suffix, embed_suffix
+        try:
+            out = self.pipeline_device(model, net_g, int(sid), np.asarray(audio, dtype=np.float32), pitch, version,
+                                       protect, index, index_rate, f0_method, bool(f0_autotune), f0_autotune_strength,
+                                       inp_f0, volume_envelope)
+        finally:
+            self.embed_suffix = prev
         if pbar is not None:
             pbar.update(2)
         out = out.cpu().numpy()

@@ -81,3 +81,33 @@ def test_pipeline_safetensors_matches_reference_golden(golden, name, tmp_path):
                              volume_envelope=1.0, version=version, protect=float(g["protect"]), hop_length=64,
                              f0_autotune=False, f0_autotune_strength=1.0, suffix=".pth", embed_suffix=".pt")
         assert rms(out_pt, g["out"]) > 1e-3
+
+
+def test_convert_audio_transformers_mode_v1(golden, tmp_path, monkeypatch):
+    """VoiceConverterAMD.convert_audio(embedders_mode="transformers") on a transformers-loaded v1 model: the
+    pipeline runs with the ".safetensors" suffix load_embedders_model returns (utils.py:155-165), i.e. the last
+    layer + final_proj (convert.py:342-345), and matches the reference's golden; a mode that disagrees with the
+    loaded model is refused (logged, None), not run with the wrong layer."""
+    from rvc_amd import audio_io
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.convert import VoiceConverterAMD
+    from rvc_amd.pipeline import VC, Config
+    from rvc_amd.rmvpe import RMVPEAMD
+    from rvc_amd.synth import SynthesizerAMD
+    g = golden("pipeline_32k_v1_st")
+    sr, version, seed = int(g["sr"]), str(g["version"]), int(g["seed"])
+    assert np.abs(g["audio"]).max() <= 0.95  # convert_audio's peak limit leaves it as the golden pipeline saw it
+    net_g = SynthesizerAMD(synthetic.make_synth_ckpt(sr, version, seed=seed), DEV)
+    hub = ContentVecAMD.from_transformers(write_dir(tmp_path, seed + 1), DEV)
+    vc = VC(sr, Config(DEV), rmvpe=RMVPEAMD(synthetic.rmvpe_state_dict(seed + 2), DEV))
+    vc.noise_fn = lambda seg, kind, shape: torch.from_numpy(
+        g[f"{'z' if kind == 'z' else 'sine'}_noise_{seg}"]).to(DEV)
+    monkeypatch.setattr(audio_io, "load_audio", lambda *a, **k: g["audio"].copy())
+    cvt = VoiceConverterAMD(vc, net_g, hub, sr, version=version)
+    kw = dict(pitch=float(g["pitch"]), f0_method="rmvpe", index_rate=0.0, volume_envelope=1.0,
+              protect=float(g["protect"]))
+    out = cvt.convert_audio("in.wav", str(tmp_path / "out.wav"), embedders_mode="transformers", **kw)
+    assert out is not None, "convert_audio logged an error"
+    assert rms(out, g["out"]) < 1e-4
+    assert vc.embed_suffix is None  # the call's suffix does not stay on the VC
+    assert cvt.convert_audio("in.wav", str(tmp_path / "out2.wav"), embedders_mode="fairseq", **kw) is None

@@ -96,3 +96,35 @@ def test_pipeline_with_index_vs_oracle(tmp_path):
     # f0 decisions vs the exact model (tests/f0check.py), then the waveform within 1e-4 RMS of the oracle
     f0check.assert_pipeline(vc, out, synthetic.rmvpe_state_dict(seed + 2), audio, lambda f0: opl.pipeline(
         Wc, Ws, Wr, mb, ck["config"], 0, audio, 0.0, version, 0.33, noise, index=idx, index_rate=0.75, f0_track=f0))
+
+
+@pytest.mark.timeout(400)
+def test_search_cfg3_index_shape_matches_oracle():
+    """BASELINE configs[2]'s benchmarked index (bench.synthetic_ivf: IVF2564,Flat over 100k x 768, nprobe 1) searched
+    with 1,599 queries -- one 32 s padded chunk's ContentVec frames, the largest query count the bench issues -- at
+    the real [nq][nlist] coarse workspace and list sizes: identical neighbour ids and bit-identical distances to
+    oracle/ivf.py.  Half the queries are drawn like the indexed data (close competition between nearby lists and
+    neighbours), half are ContentVec features of a synthetic clip (the bench's own queries).
+    Reference: create_index.py:63-83 (IVF{n},Flat, nprobe 1), convert.py:349-359 (search k=8)."""
+    import importlib.util
+    import os
+    from rvc_amd import synthetic
+    from rvc_amd.contentvec import ContentVecAMD
+    from rvc_amd.retrieval import IVFFlatDevice
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    idx = bench.synthetic_ivf(DEV)
+    assert idx.nlist == 2564 and idx.ntotal == 100_000
+    rng = np.random.default_rng(5)
+    near = (idx.centroids[rng.integers(0, idx.nlist, 800)] + 0.35 * rng.standard_normal((800, 768))).astype(np.float32)
+    hub = ContentVecAMD(synthetic.make_contentvec_ckpt(1235), DEV)
+    cv = hub.features_cf(torch.from_numpy(synthetic.synthetic_audio(32.0, seed=1000)).to(DEV)).t().cpu().numpy()
+    q = np.ascontiguousarray(np.concatenate([near, cv[: 1599 - 800]]), dtype=np.float32)
+    assert q.shape == (1599, 768)
+    dev = IVFFlatDevice(idx, DEV)
+    Dg, Ig = dev.search_cf(torch.from_numpy(np.ascontiguousarray(q.T)).to(DEV), k=8)
+    Do, Io = oivf.search(idx, q, k=8)
+    np.testing.assert_array_equal(Ig.cpu().numpy(), Io)
+    np.testing.assert_array_equal(Dg.cpu().numpy(), Do)
