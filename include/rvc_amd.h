@@ -110,6 +110,9 @@ int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_
  * right after the conv kernel, before any split-K reduce, so that a caller's events can bracket the conv
  * kernel alone (bench.py's roofline probe).  NULL (the default) turns it off. */
 void rvc_conv1d_set_probe_event(void* hip_event);
+/* Diagnostic build only (-DRVC_CONV_STAMPS=1, scripts/conv_stamps.py): the split-operand conv engine's per-block
+ * phase stamps (s_memtime) go to buf ([bytes / 2048][256] u64); returns -1 in a production build. */
+int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
 /* Split-K policy (this host thread): the library splits a conv's k range over blocks while its tile grid is
  * below `target` tiles (default 256 = 1 per CU, halved for tiles of which one block fills a CU; or
  * RVC_SPLITK_TILES); 0 = never split, -1 = back to the default.  Returns the previous setting.  Results depend on it at f32 rounding level (the split changes the

@@ -48,6 +48,10 @@ struct ConvParams {
     int rot;  // x6: rotate each block's (chunk, tap) order so that the CUs of an XCD spread over the weight image
     int xcd;  // x6: XCD-aware tile order (each XCD takes a contiguous run of tiles: row tiles share weights in its L2)
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
+#if RVC_CONV_STAMPS
+    unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
+    int64_t stamp_blocks;
+#endif
 };
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
@@ -396,6 +400,30 @@ constexpr bool kAblations = RVC_CONV_ABLATIONS != 0;
 #ifndef X6_PD8
 #define X6_PD8 0
 #endif
+// In-kernel stamps (diagnostic build -DRVC_CONV_STAMPS=1 only; scripts/conv_stamps.py): compute wave 0 and the first
+// loader wave record s_memtime at the phase boundaries of each block into a buffer of their own (never an output),
+// one lane, vector stores.  Layout per block (X6_STAMP_W words): 0 compute start, 1 memrealtime at start, 2 HW_ID,
+// 3 compute: prefetch issued, 4 compute: F16 scale barrier passed, 5 compute: chunk 0 barrier passed,
+// 6 compute: k-loop done, 7 compute: epilogue done, 8 loader start, 9 loader: F16 |max| published,
+// 10 loader: chunk 0 staged, 11 loader: loop done, 12 number of chunks; then per chunk c (< X6_STAMP_NC):
+// 16 + 4c: compute arrives at chunk c's barrier, +1 released, +2 loader arrives, +3 released.
+#ifndef RVC_CONV_STAMPS
+#define RVC_CONV_STAMPS 0
+#endif
+constexpr int X6_STAMP_W = 256, X6_STAMP_NC = 60;
+#if RVC_CONV_STAMPS
+#define X6_STAMP(slot, val)                                                                                      \
+    do {                                                                                                          \
+        const int64_t sb_ = (int64_t)blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z); \
+        if (p.stamps && lane == 0 && sb_ < p.stamp_blocks && (slot) < X6_STAMP_W)                                 \
+            p.stamps[sb_ * X6_STAMP_W + (slot)] = (val);                                                         \
+    } while (0)
+#else
+#define X6_STAMP(slot, val) \
+    do {                    \
+    } while (0)
+#endif
+#define X6_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
 
 // Block = 8 waves: waves 0-3 compute (WM x WN), waves 4-7 stage the input.  Each role keeps only its
 // own loads in its vmcnt queue, so the compute waves' weight prefetch and the loaders' two-chunk-deep
@@ -474,9 +502,18 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         return ch_beg + (c >= nck ? c - nck : c);
     };
 
+    if (wave == 0) {
+        X6_STAMP(0, X6_NOW());
+        X6_STAMP(1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        X6_STAMP(2, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
+        X6_STAMP(12, (unsigned long long)(min(nch, ch_beg + p.chunks_per_split) - ch_beg));
+        X6_STAMP(13, (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)));  // XCC_ID
+    }
     if (wave >= NCW) {
         // ---------------- loader waves: chunk c+1 split into LDS while chunk c computes
         const int ltid = tid - 64 * NCW;
+        const bool lw0 = wave == NCW;
+        if (lw0) X6_STAMP(8, X6_NOW());
         const int lin = (int)p.Lin;
         const float* xb = p.x + b * p.x_bstride;
         const int base = (int)(n0 * p.stride - p.pad);
@@ -647,6 +684,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             xload(pchunk(1), xr[1]);
             am = wave_max(fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])))) * fabsf(p.in_scale);
             if (lane == 0) tmax[wave - NCW] = am;
+            if (lw0) X6_STAMP(9, X6_NOW());
             __syncthreads();  // tile max published
             sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
             xstore(pchunk(0), xr[0], xs);
@@ -655,6 +693,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             xstore(pchunk(0), xr[0], xs);
             xload(pchunk(1), xr[1]);
         }
+        if (lw0) X6_STAMP(10, X6_NOW());
         __syncthreads();
         // iteration i (chunk ch_beg + i computing): stage chunk i + 1 from ring slot 1 into the other LDS buffer
         // (released by chunk i - 1 at the last barrier), then load chunk i + 2 into the same slot -- one chunk of
@@ -665,8 +704,11 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         for (int i = 0; i < nck; ++i) {
             if (i + 1 < nck) xstore(pchunk(i + 1), xr[1], xs + ((i + 1) & 1) * bufsz);
             xload(pchunk(i + 2), xr[1]);
+            if (lw0 && i < X6_STAMP_NC) X6_STAMP(16 + 4 * i + 2, X6_NOW());
             if constexpr (!X6_NOBAR) __syncthreads();
+            if (lw0 && i < X6_STAMP_NC) X6_STAMP(16 + 4 * i + 3, X6_NOW());
         }
+        if (lw0) X6_STAMP(11, X6_NOW());
       };
         // the loader body, once per form (a wave-uniform choice made once per block)
         if constexpr (!F16) {
@@ -781,11 +823,14 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         if (++lt == K) { lt = 0; ++li; }
     }
     float tile_rs = 1.f;
+    if (wave == 0) X6_STAMP(3, X6_NOW());
     if constexpr (F16) {
         __syncthreads();  // tile max published by the loaders
         tile_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+        if (wave == 0) X6_STAMP(4, X6_NOW());
     }
     __syncthreads();  // chunk 0 staged
+    if (wave == 0) X6_STAMP(5, X6_NOW());
     const int nsteps = s_end - s_beg;
     int ci = 0, ct = 0;  // the computing k-step's logical (chunk index, tap index)
     for (int s0 = 0; s0 < nsteps; s0 += NB) {
@@ -797,11 +842,14 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             if (s0 + u < nsteps) {
                 const int t = ct + rt < K ? ct + rt : ct + rt - K;
                 compute(t, xs + (ci & 1) * bufsz, abuf[u]);
+                if (RVC_CONV_STAMPS && wave == 0 && ct == K - 1 && ci < X6_STAMP_NC) X6_STAMP(16 + 4 * ci, X6_NOW());
                 if (!X6_NOBAR && ct == K - 1) __syncthreads();  // chunk done: hand the buffer back, take the next one
+                if (RVC_CONV_STAMPS && wave == 0 && ct == K - 1 && ci < X6_STAMP_NC) X6_STAMP(16 + 4 * ci + 1, X6_NOW());
             }
             if (++ct == K) { ct = 0; ++ci; }
         }
     }
+    if (wave == 0) X6_STAMP(6, X6_NOW());
     if constexpr (SA) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -828,6 +876,12 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             }
     }
     conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
+#if RVC_CONV_STAMPS
+    if (wave == 0) {
+        __builtin_amdgcn_s_waitcnt(0);  // the epilogue's stores issued and retired
+        X6_STAMP(7, X6_NOW());
+    }
+#endif
 }
 
 // The split-K reduce: sums the ksplit partials in split order, then the epilogue.  (A last-arriving-block
@@ -885,6 +939,11 @@ hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) 
     return hipGetLastError();
 }
 
+#if RVC_CONV_STAMPS
+unsigned long long* g_stamps = nullptr;
+int64_t g_stamp_blocks = 0;
+#endif
+
 void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.x = a->x; p.w = a->w; p.bias = a->bias; p.bias2 = a->bias2; p.res = a->res; p.y = a->y; p.ws = nullptr;
     p.B = a->B; p.Ci = a->Ci; p.Co = a->Co; p.Lin = a->Lin; p.Lout = a->Lout;
@@ -904,6 +963,10 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.wx_passes = a->wx_passes == 0 ? 6 : a->wx_passes;
     static const int dbg = getenv("RVC_CONV_DEBUG") ? atoi(getenv("RVC_CONV_DEBUG")) : 0;
     p.dbg = dbg;
+#if RVC_CONV_STAMPS
+    p.stamps = g_stamps;
+    p.stamp_blocks = g_stamp_blocks;
+#endif
     // k-step rotation (RVC_X6_ROT=1): +3 % on the conv suite, but it changes every output's
     // summation order, which moved one RMVPE voicing decision in the 45 s pipeline test past the 1e-4
     // waveform bar -- off, so the engine keeps the summation order the parity suite validated
@@ -1245,6 +1308,20 @@ extern "C" int rvc_conv1d_set_splitk_target(int target) {
 static thread_local hipEvent_t g_probe_event = nullptr;
 
 extern "C" void rvc_conv1d_set_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
+
+// Diagnostic build only (-DRVC_CONV_STAMPS=1): the x6 engine's per-block phase stamps go to buf
+// ([blocks][256] u64, blocks = bytes / 2048); returns -1 in a production build (no stamps compiled).
+extern "C" int rvc_conv1d_set_stamps(void* buf, int64_t bytes) {
+#if RVC_CONV_STAMPS
+    g_stamps = (unsigned long long*)buf;
+    g_stamp_blocks = buf ? bytes / (8 * X6_STAMP_W) : 0;
+    return 0;
+#else
+    (void)buf;
+    (void)bytes;
+    return -1;
+#endif
+}
 
 extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
     ConvParams p;
