@@ -113,6 +113,10 @@ void rvc_conv1d_set_probe_event(void* hip_event);
 /* Diagnostic build only (-DRVC_CONV_STAMPS=1, scripts/conv_stamps.py): the split-operand conv engine's per-block
  * phase stamps (s_memtime) go to buf ([bytes / 2048][256] u64); returns -1 in a production build. */
 int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
+/* The split-operand engine's epilogue form for this thread's launches: 1 = the tile epilogue through LDS (the
+ * default), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI.  Both give the same bits (tests/test_gpu_ops.py);
+ * an A/B switch for measurements in one process. */
+int rvc_conv1d_set_tile_epi(int on);
 /* Split-K policy (this host thread): the library splits a conv's k range over blocks while its tile grid is
  * below `target` tiles (default 256 = 1 per CU, halved for tiles of which one block fills a CU; or
  * RVC_SPLITK_TILES); 0 = never split, -1 = back to the default.  Returns the previous setting.  Results depend on it at f32 rounding level (the split changes the

@@ -48,6 +48,7 @@ struct ConvParams {
     int rot;  // x6: rotate each block's (chunk, tap) order so that the CUs of an XCD spread over the weight image
     int xcd;  // x6: XCD-aware tile order (each XCD takes a contiguous run of tiles: row tiles share weights in its L2)
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
+    int tile_epi;  // x6: the tile epilogue through LDS (x6_tile_epilogue), set by plan() for plain stride-1 stores
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
@@ -449,6 +450,91 @@ constexpr int x6_min_blocks() { return (FM * FN <= 4 && NCW == 4 && NP >= 3) ? 2
 // The loaders keep one chunk in flight in registers (chunk c + 2's loads are issued while chunk c computes, after
 // chunk c + 1 was staged).  A 4-deep ring (with an L2 prefetch of the K = 1 weight panels by the loaders) measured
 // no faster on ContentVec's K = 1 GEMMs and slower end to end: not kept.
+// The x6 engine's tile epilogue (round 5).  The in-register epilogue (conv_epilogue) made each compute wave issue
+// one dword load per residual / accumulate element and one dword store per output (64 stores per wave on the
+// 128 x 256 tile), in FM passes, with the 4 loader waves idle: in-kernel stamps put it at 29k of a 154k-cycle block
+// on the hottest conv (scripts/conv_stamps.py), the MFMA pipe idle throughout.  Here the compute waves finish
+// bias / activation / scale in registers and write their fragments into the block's LDS (the X buffers are dead
+// after the last chunk), then ALL waves of the block stream the tile row-major: every residual / accumulate load
+// issued first (16 B per lane), then the adds and 16-B stores.  Same operations in the same order per element as
+// conv_epilogue, so the outputs are the same bits.  Split-K blocks store their raw partial tile to the workspace
+// the same way.  Only plain stores (one phase, output column = GEMM column): plan() sets p.tile_epi.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const float* ot, int tid, int split, int b,
+                                                 int m0g, int64_t n0) {
+    constexpr int TS = BN + 4, C4 = BN / 4, NV = BM * C4, IT = (NV + NT - 1) / NT;
+    const int Cog = (int)p.Co;
+    const bool part = p.ksplit > 1;
+    // destination rows and the columns valid in this tile
+    float* dst;
+    const float* rb = nullptr;
+    const float* yb_in = nullptr;
+    int64_t ld;
+    int lim;
+    if (part) {
+        dst = p.ws + (((int64_t)split * p.B + b) * p.Co) * p.ncols;
+        ld = p.ncols;
+        lim = (int)min((int64_t)BN, p.ncols - n0);
+    } else {
+        dst = p.y + b * p.y_bstride;
+        ld = p.Lout;
+        lim = (int)min((int64_t)BN, min(p.ncols, p.Lout) - n0);
+        if (p.res) rb = p.res + b * p.res_bstride;
+        if (p.accumulate) yb_in = dst;
+    }
+    const bool vec = lim == BN && (ld & 3) == 0 && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)rb & 15) == 0;
+    if (vec) {
+        float4 rv[IT], av[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {  // every load first, from clamped addresses
+            const int idx = tid + it * NT;
+            const int row = idx / C4, c = (idx - row * C4) * 4;
+            const int m = m0g + row;
+            const int64_t o = (int64_t)(idx < NV && m < Cog ? m : 0) * ld + n0 + c;
+            if (rb) rv[it] = *reinterpret_cast<const float4*>(rb + o);
+            if (yb_in) av[it] = *reinterpret_cast<const float4*>(yb_in + o);
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int idx = tid + it * NT;
+            const int row = idx / C4, c = (idx - row * C4) * 4;
+            const int m = m0g + row;
+            if (idx < NV && m < Cog) {
+                float4 v = *reinterpret_cast<const float4*>(ot + row * TS + c);
+                if (rb) {
+                    v.x += rv[it].x;
+                    v.y += rv[it].y;
+                    v.z += rv[it].z;
+                    v.w += rv[it].w;
+                }
+                if (yb_in) {
+                    v.x += av[it].x;
+                    v.y += av[it].y;
+                    v.z += av[it].z;
+                    v.w += av[it].w;
+                }
+                *reinterpret_cast<float4*>(dst + (int64_t)m * ld + n0 + c) = v;
+            }
+        }
+        return;
+    }
+    // edge tile (the last column tile) or unaligned rows: element by element, lanes along the row
+    constexpr int NS = BM * BN, ITS = (NS + NT - 1) / NT;
+#pragma unroll 4
+    for (int it = 0; it < ITS; ++it) {
+        const int idx = tid + it * NT;
+        const int row = idx / BN, c = idx - row * BN;
+        const int m = m0g + row;
+        if (idx < NS && m < Cog && c < lim) {
+            const int64_t o = (int64_t)m * ld + n0 + c;
+            float v = ot[row * TS + c];
+            if (rb) v += rb[o];
+            if (yb_in) v += yb_in[o];
+            dst[o] = v;
+        }
+    }
+}
+
 template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
@@ -715,10 +801,16 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             if ((Cig & 31) == 0 && p.in_scale == 1.f && (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
                 if (p.in_act == RVC_ACT_LRELU) loader(std::true_type{}, std::true_type{});
                 else loader(std::true_type{}, std::false_type{});
-                return;
+            } else {
+                loader(std::false_type{}, std::false_type{});
             }
+        } else {
+            loader(std::false_type{}, std::false_type{});
         }
-        loader(std::false_type{}, std::false_type{});
+        if (p.tile_epi) {  // the compute waves' tile is in LDS after this barrier
+            __syncthreads();
+            x6_tile_epilogue<BM, BN, 64 * (NCW + 4)>(p, reinterpret_cast<const float*>(xs), tid, split, b, m0g, n0);
+        }
         return;
     }
 
@@ -875,7 +967,47 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 for (int j = 0; j < FN; ++j) acc[i][j][r] *= f;
             }
     }
-    conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
+    if (p.tile_epi) {
+        // bias, 2nd bias, activation and scale in registers (conv_epilogue's order), then the fragments into LDS: row
+        // (wm * 16 FM + 16 i + 4 lg + r), column (wn * 16 FN + 16 j + ln); a row stride of BN + 4 floats puts the two
+        // 16-lane halves of each ds_write_b32 on different banks
+        float* ot = reinterpret_cast<float*>(xs);
+        constexpr int TS = BN + 4;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            floatx4 (&av)[1][FN] = *reinterpret_cast<floatx4 (*)[1][FN]>(&acc[i][0]);
+            if (p.ksplit == 1) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int mg = m0g + wm * 16 * FM + i * 16 + lg * 4 + r;
+                    const int mr = mg < Cog ? mg : 0;
+                    float bs = 0.f;
+                    if (p.bias) bs = p.bias[mr];
+                    if (p.bias2) bs += p.bias2[mr];
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) av[0][j][r] += bs;
+                }
+                switch (p.out_act) {
+                    case RVC_ACT_LRELU: apply_act<RVC_ACT_LRELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+                    case RVC_ACT_RELU: apply_act<RVC_ACT_RELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+                    case RVC_ACT_TANH: apply_act<RVC_ACT_TANH, 1, FN>(av, p.out_slope, p.out_scale); break;
+                    case RVC_ACT_GELU: apply_act<RVC_ACT_GELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+                    case RVC_ACT_SIGMOID: apply_act<RVC_ACT_SIGMOID, 1, FN>(av, p.out_slope, p.out_scale); break;
+                    case RVC_ACT_LOGCLAMP: apply_act<RVC_ACT_LOGCLAMP, 1, FN>(av, p.out_slope, p.out_scale); break;
+                    default: apply_act<RVC_ACT_NONE, 1, FN>(av, p.out_slope, p.out_scale); break;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    ot[(wm * 16 * FM + i * 16 + lg * 4 + r) * TS + wn * 16 * FN + j * 16 + ln] = av[0][j][r];
+        }
+        __syncthreads();
+        x6_tile_epilogue<BM, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g, n0);
+    } else {
+        conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
+    }
 #if RVC_CONV_STAMPS
     if (wave == 0) {
         __builtin_amdgcn_s_waitcnt(0);  // the epilogue's stores issued and retired
@@ -963,6 +1095,7 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.wx_passes = a->wx_passes == 0 ? 6 : a->wx_passes;
     static const int dbg = getenv("RVC_CONV_DEBUG") ? atoi(getenv("RVC_CONV_DEBUG")) : 0;
     p.dbg = dbg;
+    p.tile_epi = 0;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -991,6 +1124,8 @@ int num_cus() {
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
 // per-thread override of the split-K target grid (rvc_conv1d_set_splitk_target; -1 = the process default)
 static thread_local int g_splitk_target = -1;
+// per-thread override of the x6 tile epilogue (rvc_conv1d_set_tile_epi; -1 = RVC_X6_TILE_EPI, default on)
+static thread_local int g_tile_epi = -1;
 
 void split_k(ConvParams& p, int64_t tiles, int nch, int per_cu = 2) {
     // target grid (RVC_SPLITK_TILES, 0 = never split): 256 tiles = 1 per CU (round 4, same box, alternated runs:
@@ -1108,6 +1243,14 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         split_k(p, tiles, p.wx_nch, cfg.WM * cfg.WN == 8 ? 1 : 2);
         lds = (size_t)2 * (p.wx_passes == 6 || p.wx_passes == RVC_ARITH_FP32_SA ? 3 : (p.wx_passes == 1 ? 1 : 2)) *
               p.span * 64 + 16;  // + the split-fp16 tile |max|
+        // the tile epilogue (x6_tile_epilogue) for plain stores: one phase, output column = GEMM column, no 2-D border;
+        // its [BM][BN + 4] f32 tile reuses the X buffers' LDS (RVC_X6_TILE_EPI=0: the in-register epilogue, A/B switch)
+        static const int tepi_env = getenv("RVC_X6_TILE_EPI") ? atoi(getenv("RVC_X6_TILE_EPI")) : 1;
+        const int tepi = g_tile_epi >= 0 ? g_tile_epi : tepi_env;
+        const size_t tile_bytes = (size_t)BM * (BN + 4) * 4;
+        p.tile_epi = tepi && a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&
+                     tile_bytes <= 160 * 1024;
+        if (p.tile_epi && tile_bytes > lds) lds = tile_bytes;
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         return RVC_OK;
@@ -1308,6 +1451,11 @@ extern "C" int rvc_conv1d_set_splitk_target(int target) {
 static thread_local hipEvent_t g_probe_event = nullptr;
 
 extern "C" void rvc_conv1d_set_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
+
+extern "C" int rvc_conv1d_set_tile_epi(int on) {
+    g_tile_epi = on < 0 ? -1 : (on ? 1 : 0);
+    return RVC_OK;
+}
 
 // Diagnostic build only (-DRVC_CONV_STAMPS=1): the x6 engine's per-block phase stamps go to buf
 // ([blocks][256] u64, blocks = bytes / 2048); returns -1 in a production build (no stamps compiled).

@@ -387,3 +387,47 @@ def test_conv1d_f16x3(ops, case, spread):
     rel, rel32 = rms(y - ref), rms(f32 - ref)
     assert float(rel.max()) < 2.0 ** -18, float(rel.max())
     assert bool((rel <= 8 * rel32 + 1e-6).all()), (float(rel.max()), float(rel32.max()))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp32x6", "bf16x3"])
+@pytest.mark.parametrize("Ci,Co,K,d,L,B,epi", [
+    (128, 128, 11, 5, 5000, 1, "rb"),     # the 128 x 256 split-fp16 tile, ragged last tile
+    (128, 128, 3, 1, 4096, 1, "rb"),      # full tiles, Lout % 4 == 0: the 16-B path everywhere
+    (64, 64, 5, 1, 3001, 2, "full"),      # bias2 / tanh / scale / residual / accumulate, batched, Lout % 4 != 0
+    (768, 768, 1, 1, 1599, 1, "plain"),   # split-K partial tiles through the workspace
+    (40, 72, 3, 1, 777, 1, "full"),       # ragged rows and channels
+    (256, 256, 7, 1, 300, 1, "rb"),
+])
+def test_x6_tile_epilogue_bit_identical(ops, prec, Ci, Co, K, d, L, B, epi):
+    """The x6 engine's LDS tile epilogue (round 5) gives the same bits as the in-register epilogue it replaced, for
+    every epilogue feature and tile shape (rvc_conv1d_set_tile_epi toggles it within the process)."""
+    g = gen(11)
+    x = torch.randn(B, Ci, L, generator=g).to(DEV)
+    w = torch.randn(Co, Ci, K, generator=g) / math.sqrt(Ci * K)
+    b = torch.randn(Co, generator=g)
+    b2 = torch.randn(Co, generator=g).to(DEV)
+    res = torch.randn(B, Co, L, generator=g).to(DEV)
+    acc0 = torch.randn(B, Co, L, generator=g).to(DEV)
+    c = ops.Conv(w, b)
+    p = d * (K - 1) // 2
+    outs = []
+    lib = ops._lib.load()
+    for on in (0, 1):
+        lib.rvc_conv1d_set_tile_epi(on)
+        try:
+            y = acc0.clone() if epi == "full" else torch.empty(B, Co, L, device=DEV)
+            kw = dict(pad=p, dil=d, out=y)
+            if epi == "rb":
+                kw.update(res=res, in_act=ops.ACT_LRELU, in_slope=0.1)
+            elif epi == "full":
+                kw.update(bias2=b2, res=res, accumulate=True, in_act=ops.ACT_LRELU, in_slope=0.1, in_scale=0.5,
+                          out_act=ops.ACT_TANH, out_scale=-1.0)
+            with ops.precision(prec):
+                c(x if B > 1 else x[0], **{k: (v[0] if B == 1 and torch.is_tensor(v) and v.dim() == 3 else v)
+                                           for k, v in kw.items()})
+            assert ops.LAST_CONV_ENGINE == 1
+            torch.cuda.synchronize()
+            outs.append(y.cpu())
+        finally:
+            lib.rvc_conv1d_set_tile_epi(-1)
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
