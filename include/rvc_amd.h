@@ -97,6 +97,12 @@ typedef struct rvc_conv1d_args {
        on the fp16 MFMA: ~2^-20 relative per product, f32 accumulation. */
     const void* wx;
     int wx_nmf, wx_passes;
+    /* Tensor |max| side channel (round 5): amax_out (or NULL) receives max |y| over every value the launch stores
+       (an atomic max on the f32 bits; the caller zeroes the word before the producing launch), and amax_in (or
+       NULL) is such a word for x: a split-fp16 launch (RVC_ARITH_F16X3) then takes its activation scale from it
+       (times |in_scale|: an upper bound of |pre(x)|) instead of a per-tile |max| pre-pass over its input. */
+    const unsigned* amax_in;
+    unsigned* amax_out;
 } rvc_conv1d_args;
 
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned

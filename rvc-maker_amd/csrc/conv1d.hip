@@ -49,6 +49,8 @@ struct ConvParams {
     int xcd;  // x6: XCD-aware tile order (each XCD takes a contiguous run of tiles: row tiles share weights in its L2)
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
     int tile_epi;  // x6: the tile epilogue through LDS (x6_tile_epilogue), set by plan() for plain stride-1 stores
+    const unsigned* amax_in;  // |max| of x (f32 bits) or null: split-fp16 loaders take their scale from it
+    unsigned* amax_out;       // or null: max |y| over the stored values (atomic max of the f32 bits)
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
@@ -56,6 +58,13 @@ struct ConvParams {
 };
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
+
+// amax_out: the wave's largest |stored value| folded into the tensor's word (atomic max of the f32 bits: for values
+// >= 0 the bit patterns order as the floats do).  Called by every lane of a wave (the shuffles need them all).
+__device__ __forceinline__ void amax_publish(unsigned* amax_out, float m) {
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) atomicMax(amax_out, __float_as_uint(m));
+}
 
 // Output column n -> store position t; -1 when the column is not stored (beyond ncols / Lout);
 // -(t + 2) for a border cell of a 2-D image, which is stored as 0 (the bordered [C][H+2][W+2]
@@ -73,7 +82,8 @@ __device__ __forceinline__ int out_pos(const ConvParams& p, int64_t n, int phase
 
 // Branch-free epilogue for one element: every load is issued unconditionally from a clamped
 // address (a per-element guarded load makes hipcc branch and wait vmcnt(0) per element).
-__device__ __forceinline__ void epilogue_store(const ConvParams& p, float acc, int b, int64_t m, int t) {
+// returns the value stored (0 when nothing is stored: a border cell stores 0, a column past the end nothing)
+__device__ __forceinline__ float epilogue_store(const ConvParams& p, float acc, int b, int64_t m, int t) {
     const bool ok = t >= 0;
     const int64_t o = m * p.Lout + (ok ? t : 0);
     float v = acc;
@@ -85,6 +95,7 @@ __device__ __forceinline__ void epilogue_store(const ConvParams& p, float acc, i
     if (p.accumulate) v += yb[o];
     if (ok) yb[o] = v;
     else if (t <= -2) yb[m * p.Lout + (-t - 2)] = 0.f;  // 2-D border cell
+    return ok ? v : 0.f;
 }
 
 template <int ACT, int FM, int FN>
@@ -133,6 +144,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
     float* yb = p.y + b * p.y_bstride;
     const float* rb2 = p.res ? p.res + b * p.res_bstride : nullptr;
     const int Lo = (int)p.Lout;
+    float amx = 0.f;  // amax_out: largest |stored value| of this lane
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
         floatx4 (&av)[1][FN] = *reinterpret_cast<floatx4 (*)[1][FN]>(&acc[i][0]);
@@ -174,10 +186,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
-                if (mok[r] && tcol[j] >= 0) yb[mrow[r] * Lo + tcol[j]] = av[0][j][r];
-                else if (mok[r] && tcol[j] <= -2) yb[mrow[r] * Lo + (-tcol[j] - 2)] = 0.f;  // 2-D border cell
+                if (mok[r] && tcol[j] >= 0) {
+                    yb[mrow[r] * Lo + tcol[j]] = av[0][j][r];
+                    amx = fmaxf(amx, fabsf(av[0][j][r]));
+                } else if (mok[r] && tcol[j] <= -2) {
+                    yb[mrow[r] * Lo + (-tcol[j] - 2)] = 0.f;  // 2-D border cell
+                }
             }
     }
+    if (p.amax_out) amax_publish(p.amax_out, amx);
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -483,6 +500,7 @@ __device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const floa
         if (p.accumulate) yb_in = dst;
     }
     const bool vec = lim == BN && (ld & 3) == 0 && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)rb & 15) == 0;
+    float amx = 0.f;  // amax_out: largest |stored value| of this thread (final values only, not split-K partials)
     if (vec) {
         float4 rv[IT], av[IT];
 #pragma unroll
@@ -514,8 +532,10 @@ __device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const floa
                     v.w += av[it].w;
                 }
                 *reinterpret_cast<float4*>(dst + (int64_t)m * ld + n0 + c) = v;
+                amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
             }
         }
+        if (p.amax_out && !part) amax_publish(p.amax_out, amx);
         return;
     }
     // edge tile (the last column tile) or unaligned rows: element by element, lanes along the row
@@ -531,8 +551,10 @@ __device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const floa
             if (rb) v += rb[o];
             if (yb_in) v += yb_in[o];
             dst[o] = v;
+            amx = fmaxf(amx, fabsf(v));
         }
     }
+    if (p.amax_out && !part) amax_publish(p.amax_out, amx);
 }
 
 template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
@@ -761,14 +783,21 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 return m;
             };
             float am = 0.f;
-            for (int i = 2; i < nck; i += 2) {
-                xload(pchunk(i), xr[0]);
-                xload(pchunk(i + 1 < nck ? i + 1 : i), xr[1]);
-                am = fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])));
+            if (p.amax_in) {
+                // the producer published |max| of the whole input tensor (amax side channel): no pre-pass
+                xload(pchunk(0), xr[0]);
+                xload(pchunk(1), xr[1]);
+                am = __uint_as_float(*p.amax_in) * fabsf(p.in_scale);
+            } else {
+                for (int i = 2; i < nck; i += 2) {
+                    xload(pchunk(i), xr[0]);
+                    xload(pchunk(i + 1 < nck ? i + 1 : i), xr[1]);
+                    am = fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])));
+                }
+                xload(pchunk(0), xr[0]);
+                xload(pchunk(1), xr[1]);
+                am = wave_max(fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])))) * fabsf(p.in_scale);
             }
-            xload(pchunk(0), xr[0]);
-            xload(pchunk(1), xr[1]);
-            am = wave_max(fmaxf(am, fmaxf(rmax(xr[0]), rmax(xr[1])))) * fabsf(p.in_scale);
             if (lane == 0) tmax[wave - NCW] = am;
             if (lw0) X6_STAMP(9, X6_NOW());
             __syncthreads();  // tile max published
@@ -807,9 +836,19 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         } else {
             loader(std::false_type{}, std::false_type{});
         }
-        if (p.tile_epi) {  // the compute waves' tile is in LDS after this barrier
+        if (p.tile_epi == 1) {  // the compute waves' tile is in LDS after this barrier
             __syncthreads();
             x6_tile_epilogue<BM, BN, 64 * (NCW + 4)>(p, reinterpret_cast<const float*>(xs), tid, split, b, m0g, n0);
+        } else if (p.tile_epi == 2) {  // in two row halves (the tile is twice the X buffers' LDS)
+            if constexpr (WM % 2 == 0) {
+                __syncthreads();
+                x6_tile_epilogue<BM / 2, BN, 64 * (NCW + 4)>(p, reinterpret_cast<const float*>(xs), tid, split, b, m0g,
+                                                             n0);
+                __syncthreads();
+                __syncthreads();
+                x6_tile_epilogue<BM / 2, BN, 64 * (NCW + 4)>(p, reinterpret_cast<const float*>(xs), tid, split, b,
+                                                             m0g + BM / 2, n0);
+            }
         }
         return;
     }
@@ -997,14 +1036,30 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                     default: apply_act<RVC_ACT_NONE, 1, FN>(av, p.out_slope, p.out_scale); break;
                 }
             }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    ot[(wm * 16 * FM + i * 16 + lg * 4 + r) * TS + wn * 16 * FN + j * 16 + ln] = av[0][j][r];
         }
-        __syncthreads();
-        x6_tile_epilogue<BM, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g, n0);
+        // the fragments into LDS: the whole tile, or (tile_epi 2) the row half h of waves wm in [h WM / 2, (h + 1) WM / 2)
+        auto put = [&](int row0) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        ot[(wm * 16 * FM - row0 + i * 16 + lg * 4 + r) * TS + wn * 16 * FN + j * 16 + ln] = acc[i][j][r];
+        };
+        if (p.tile_epi == 1) {
+            put(0);
+            __syncthreads();
+            x6_tile_epilogue<BM, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g, n0);
+        } else if constexpr (WM % 2 == 0) {
+            if (wm < WM / 2) put(0);
+            __syncthreads();
+            x6_tile_epilogue<BM / 2, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g, n0);
+            __syncthreads();  // half 0 read out: its LDS is free
+            if (wm >= WM / 2) put(BM / 2);
+            __syncthreads();
+            x6_tile_epilogue<BM / 2, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g + BM / 2, n0);
+        }
     } else {
         conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
     }
@@ -1024,12 +1079,13 @@ __global__ void conv_splitk_reduce(ConvParams p) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = blockIdx.y;
     const int bp = blockIdx.z;
-    if (n >= p.ncols) return;
+    if (n >= p.ncols && !p.amax_out) return;  // (amax: every lane of the wave joins the shuffle)
     const int64_t sstride = p.B * p.nphase * p.Co * p.ncols;
-    const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + n;
+    const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + (n < p.ncols ? n : 0);
     float s = 0.f;
     for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
-    epilogue_store(p, s, bp / p.nphase, m, out_pos(p, n, bp % p.nphase));
+    const float v = epilogue_store(p, s, bp / p.nphase, m, out_pos(p, n, bp % p.nphase));
+    if (p.amax_out) amax_publish(p.amax_out, fabsf(v));
 }
 
 struct Cfg {
@@ -1096,6 +1152,8 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     static const int dbg = getenv("RVC_CONV_DEBUG") ? atoi(getenv("RVC_CONV_DEBUG")) : 0;
     p.dbg = dbg;
     p.tile_epi = 0;
+    p.amax_in = a->amax_in;
+    p.amax_out = a->amax_out;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -1245,12 +1303,16 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
               p.span * 64 + 16;  // + the split-fp16 tile |max|
         // the tile epilogue (x6_tile_epilogue) for plain stores: one phase, output column = GEMM column, no 2-D border;
         // its [BM][BN + 4] f32 tile reuses the X buffers' LDS (RVC_X6_TILE_EPI=0: the in-register epilogue, A/B switch)
+        // Only where it needs no more LDS than the X buffers (whole, or in two row halves): a launch with a larger
+        // LDS footprint leaves no room on its CUs for the concurrent front-end streams' blocks (round 5, the 128 x 256
+        // tile with a 133 KB tile: its epilogue no faster -- every CU's blocks reach it at once and it is HBM-bound --
+        // and the clip stream 928 -> 889 xRT); and not on the 256-wide tile, whose epilogue measured 29k -> 33k cycles.
         static const int tepi_env = getenv("RVC_X6_TILE_EPI") ? atoi(getenv("RVC_X6_TILE_EPI")) : 1;
         const int tepi = g_tile_epi >= 0 ? g_tile_epi : tepi_env;
         const size_t tile_bytes = (size_t)BM * (BN + 4) * 4;
-        p.tile_epi = tepi && a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&
-                     tile_bytes <= 160 * 1024;
-        if (p.tile_epi && tile_bytes > lds) lds = tile_bytes;
+        const bool plain = a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&
+                           BN <= 128;
+        p.tile_epi = !(tepi && plain) ? 0 : tile_bytes <= lds ? 1 : (cfg.WM % 2 == 0 && tile_bytes / 2 <= lds) ? 2 : 0;
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         return RVC_OK;

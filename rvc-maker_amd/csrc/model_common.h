@@ -48,6 +48,7 @@ struct rvc_ctx {
     int prec = RVC_PREC_FP32;
     int rm_prec = RVC_PREC_FP64;  // RMVPE's arithmetic (rvc_ctx_set_rmvpe_precision), read by rvc_load_rmvpe
     bool x6 = true, f16mix = true, fused_rb = true;  // RVC_AMD_X6 / RVC_AMD_F16MIX / RVC_AMD_FUSED_RB as ops.py
+    bool amax = true;  // RVC_AMD_AMAX as synth.py: the generator's |max| side channel
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;
@@ -287,9 +288,10 @@ inline int make_convT(rvc_ctx* c, ModelBase& m, const HostT& w, const HostT& b, 
 // ------------------------------------------------------------------ pass sets (ops.conv_passes / rb_passes)
 inline int base_passes(const rvc_ctx* c) { return c->prec == RVC_PREC_FP32 ? 6 : c->prec; }
 
-inline int conv_passes(const rvc_ctx* c, int K, int64_t Cig, int stride, bool two_d) {
+// amax: the input's |max| comes from its producer (the amax side channel): split-fp16 for every stride-1 1-D conv
+inline int conv_passes(const rvc_ctx* c, int K, int64_t Cig, int stride, bool two_d, bool amax = false) {
     if (c->prec == RVC_PREC_FP32 && c->f16mix && stride == 1 && !two_d &&
-        ((K >= 7 && Cig <= 256) || (K >= 3 && Cig >= 64 && Cig <= 128)))
+        (amax || (K >= 7 && Cig <= 256) || (K >= 3 && Cig >= 64 && Cig <= 128)))
         return RVC_ARITH_F16X3;
     return base_passes(c);
 }
@@ -332,6 +334,8 @@ struct CallOpts {
     int64_t B = 1, x_bstride = 0, y_bstride = 0, res_bstride = 0;
     int ntoff = 0, wrap = 0;  // 2-D mode (RMVPE): tap offsets and border masking
     int toff[16] = {0};
+    const unsigned* amax_in = nullptr;  // the |max| side channel (rvc_conv1d_args.amax_in / amax_out)
+    unsigned* amax_out = nullptr;
 };
 
 inline int conv(rvc_ctx* c, ModelBase& m, const ConvW& cw, const float* x, int64_t Lin, float* y, const CallOpts& o,
@@ -363,6 +367,8 @@ inline int conv(rvc_ctx* c, ModelBase& m, const ConvW& cw, const float* x, int64
     a.ntoff = o.ntoff;
     a.wrap = o.wrap;
     for (int i = 0; i < o.ntoff; ++i) a.toff[i] = o.toff[i];
+    a.amax_in = o.amax_in;
+    a.amax_out = o.amax_out;
     int stride = o.stride;
     if (cw.nphase > 1) {  // ConvT as u phase convs (ops.ConvT.__call__)
         const int64_t Lout = (Lin - 1) * cw.u - 2 * cw.tpad + cw.Kfull;
@@ -384,7 +390,7 @@ inline int conv(rvc_ctx* c, ModelBase& m, const ConvW& cw, const float* x, int64
         a.ostride = 1;
     }
     if (cw.wx_bf) {
-        const int passes = conv_passes(c, cw.K, cw.Ci / cw.groups, stride, o.ntoff > 0);
+        const int passes = conv_passes(c, cw.K, cw.Ci / cw.groups, stride, o.ntoff > 0, o.amax_in != nullptr);
         a.wx = passes == RVC_ARITH_F16X3 ? cw.wx_hf : cw.wx_bf;
         a.wx_nmf = cw.nmf;
         a.wx_passes = passes;

@@ -80,9 +80,12 @@ bool resblock_fusable(const rvc_ctx* c, const ConvW& c1, const ConvW& c2, int d)
 
 
 
+// |max| side-channel cells per generator stage (synth.py AMAX_PER_STAGE): y, then t1 / nxt of each unfused pair
+constexpr int kAmaxPerStage = 16;
+
 struct Bufs {
     int64_t phone_cf, lin, x, tmp, o, ml, qkv, rk, ffh, stats, znoise, zp, fb0, fb1, h, acts, outacc, xin, gc, har, work,
-        snoise, xpre, reg[2];
+        snoise, xpre, amax, reg[2];
     std::vector<int64_t> Li;
     int64_t stage_floats = 0, total = 0;
 };
@@ -115,6 +118,7 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
     b.work = p.take(T);
     b.snoise = p.take(L);
     b.xpre = p.take((int64_t)g.upsample_initial_channel * T);
+    b.amax = p.take(kAmaxPerStage * 8);  // the |max| cells of the unfused ResBlock stages (synth.py generator)
     int64_t Lc = T;
     for (size_t i = 0; i < S.ups.size(); ++i) {
         Lc = convT_out_len(S.ups[i], Lc);
@@ -261,6 +265,9 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     }
     MTRY(rvc_sine_source(nsff0, sine_noise, har, work, 1, T, S.upp, (float)g.sr, S.lin_w, S.lin_b, s));
     float* xcur = A + bf.xpre;
+    unsigned* amax = reinterpret_cast<unsigned*>(A + bf.amax);
+    const bool use_amax = c->amax && (int64_t)S.ups.size() <= 8;
+    if (use_amax) MHIP(hipMemsetAsync(amax, 0, sizeof(unsigned) * kAmaxPerStage * S.ups.size(), s));
     {
         CallOpts o;
         o.pad = 3;
@@ -285,11 +292,17 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         on.stride = S.noise_stride[i];
         on.pad = S.noise_pad[i];
         on.accumulate = 1;
+        // the |max| side channel (synth.py generator): y, each unfused c1 output and each non-last c2 output publish
+        // their |max|; the convs that read them take their split-fp16 scale from it
+        unsigned* cell = use_amax ? amax + kAmaxPerStage * i : nullptr;
+        int ncell = 1;
+        if (cell) on.amax_out = cell;
         MTRY(conv(c, S, S.noise[i], har, L, y, on, s));
         for (int j = 0; j < nk; ++j) {
             const int kk = g.resblock_kernel_sizes[j];
             const std::vector<Pair>& pairs = S.res[i][j];
             float* cur = y;
+            const unsigned* cur_cell = cell;
             for (size_t m = 0; m < pairs.size(); ++m) {
                 const Pair& P = pairs[m];
                 const bool last = m + 1 == pairs.size();
@@ -315,28 +328,37 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
                     ra.slope = kLreluSlope;
                     MTRY(rvc_resblock_pair(&ra, s));
                     cur = nxt;
+                    cur_cell = nullptr;
                     continue;
                 }
+                unsigned* t1_cell = cell && ncell < kAmaxPerStage ? cell + ncell++ : nullptr;
                 CallOpts o1;
                 o1.pad = (kk * P.d - P.d) / 2;
                 o1.dil = P.d;
                 o1.in_act = RVC_ACT_LRELU;
                 o1.in_slope = kLreluSlope;
+                o1.amax_in = cur_cell;
+                o1.amax_out = t1_cell;
                 MTRY(conv(c, S, P.c1, cur, Li, t1, o1, s));
                 CallOpts o2;
                 o2.pad = (kk - 1) / 2;
                 o2.res = cur;
                 o2.in_act = RVC_ACT_LRELU;
                 o2.in_slope = kLreluSlope;
+                o2.amax_in = t1_cell;
                 float* nxt;
+                unsigned* nxt_cell = nullptr;
                 if (last) {
                     nxt = xs;
                     o2.accumulate = j > 0;
                 } else {
                     nxt = cur != xa ? xa : xb;
+                    nxt_cell = cell && ncell < kAmaxPerStage ? cell + ncell++ : nullptr;
+                    o2.amax_out = nxt_cell;
                 }
                 MTRY(conv(c, S, P.c2, t1, Li, nxt, o2, s));
                 cur = nxt;
+                cur_cell = nxt_cell;
             }
         }
         xcur = xs;
@@ -367,6 +389,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->x6 = env_on("RVC_AMD_X6");
     c->f16mix = env_on("RVC_AMD_F16MIX");
     c->fused_rb = env_on("RVC_AMD_FUSED_RB");
+    c->amax = env_on("RVC_AMD_AMAX");
     *out = c;
     return RVC_OK;
 }

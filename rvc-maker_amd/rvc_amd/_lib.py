@@ -27,7 +27,8 @@ class Conv1dArgs(ctypes.Structure):
                 ("in_act", c_int), ("out_act", c_int), ("accumulate", c_int), ("_pad0", c_int),
                 ("in_scale", c_float), ("in_slope", c_float), ("out_slope", c_float), ("out_scale", c_float),
                 ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16),
-                ("wx", c_void_p), ("wx_nmf", c_int), ("wx_passes", c_int)]
+                ("wx", c_void_p), ("wx_nmf", c_int), ("wx_passes", c_int),
+                ("amax_in", c_void_p), ("amax_out", c_void_p)]
 
 
 class Conv64Args(ctypes.Structure):

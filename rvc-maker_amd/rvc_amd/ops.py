@@ -68,12 +68,14 @@ PASSES = {"fp32": 6, "fp32x6": 6, "fp32sa": 7, "f16x3": F16X3, "bf16x3": 3, "bf1
 F16_MIX = os.environ.get("RVC_AMD_F16MIX", "1") != "0"
 
 
-def conv_passes(K, Ci, stride=1, two_d=False):
+def conv_passes(K, Ci, stride=1, two_d=False, amax=False):
     """The pass set a conv launch runs at under the current precision (see PASSES): in "fp32", split-fp16
     where it measured faster than 6-pass split-bf16 (scripts/conv_bench.py, same box: k >= 7 up to 256
-    input channels, and k = 3 at 64-128 channels; 6-pass at k = 3 over 256 or 32 channels)."""
+    input channels, and k = 3 at 64-128 channels; 6-pass at k = 3 over 256 or 32 channels) -- and every stride-1
+    1-D conv whose input's |max| comes from its producer (``amax``: no per-tile pre-pass, which is what made the
+    short-tap and wide convs slower in split-fp16)."""
     if _PRECISION == "fp32" and F16_MIX and stride == 1 and not two_d and \
-            ((K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128)):
+            (amax or (K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128)):
         return F16X3
     return PASSES[_PRECISION]
 _PRECISION = os.environ.get("RVC_AMD_PRECISION", "fp32")
@@ -203,6 +205,17 @@ class ConvT:
                       flops=2.0 * B * Ci * self.Co * self.K * Lin, wx=self.wx, wx_nmf=self.wx_nmf, **kw)
 
 
+class AmaxSlots:
+    """n one-word |max| cells (the conv engine's amax side channel) for one pass, zeroed by one launch: ``s[k]`` is
+    cell k, handed to a producer as ``amax_out`` and to its consumers as ``amax_in``."""
+
+    def __init__(self, n, device):
+        self.words = torch.zeros(n, dtype=torch.int32, device=device)
+
+    def __getitem__(self, k):
+        return self.words[k:k + 1]
+
+
 LAST_CONV_FLOPS = 0.0
 LAST_CONV_ENGINE = 0  # 0 = f32 MFMA engine, 1 = split-bf16 (x6) engine
 LAST_CONV_PASSES = 0  # the split-operand launch's pass set (PASSES values; F16X3 = split-fp16), 0 = f32 engine
@@ -259,8 +272,13 @@ def _shape3(x):
 def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, groups=1, Lout=None, ncols=0,
            nphase=1, ostride=1, ooffset=0, out=None, res=None, in_act=ACT_NONE, in_slope=0.0, in_scale=1.0,
            out_act=ACT_NONE, out_slope=0.0, out_scale=1.0, accumulate=False, B=None, Lin=None, x_bstride=0,
-           w_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, flops=None, wx=None, wx_nmf=0):
+           w_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, flops=None, wx=None, wx_nmf=0,
+           amax_in=None, amax_out=None):
     """y = conv(pre(x)) with fused epilogue.  x: [B][Ci][Lin] device f32 (t contiguous).
+
+    ``amax_out`` / ``amax_in``: one-word device tensors (``AmaxSlots``) of the |max| side channel -- the launch
+    folds max |y| into ``amax_out`` (zeroed beforehand), and a split-fp16 launch takes its activation scale from
+    ``amax_in`` (the producer's word for x) instead of a per-tile pre-pass (include/rvc_amd.h).
 
     ``flops`` is the launch's ALGORITHMIC FLOP count for roofline accounting (recorded in
     LAST_CONV_FLOPS); the default is 2*B*Co*(Ci/g)*K*(valid outputs)."""
@@ -307,8 +325,9 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
         for i, v in enumerate(toff):
             a.toff[i] = int(v)
     a.wrap = wrap
+    a.amax_in, a.amax_out = _p(amax_in), _p(amax_out)
     if wx is not None:
-        passes = conv_passes(K, Ci // groups, stride, toff is not None)
+        passes = conv_passes(K, Ci // groups, stride, toff is not None, amax_in is not None)
         a.wx, a.wx_nmf, a.wx_passes = ctypes.c_void_p(wx.data_ptr(passes)), wx_nmf, passes
     if flops is None:
         valid = (Lout // wrap - 2) * (wrap - 2) if wrap else (ncols or Lout) * nphase

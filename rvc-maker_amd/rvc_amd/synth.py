@@ -25,7 +25,13 @@ import torch
 from . import ops
 from .ops import ACT_LRELU, ACT_RELU, ACT_TANH, Conv, ConvT
 
+import os
+
 LRELU_SLOPE = 0.1
+# the generator's |max| side channel (RVC_AMD_AMAX=0: per-tile pre-passes, the round-4 form; rvc_model.cpp reads the
+# same switch): cells per upsample stage -- y, then each unfused pair's c1 output and non-last c2 output
+AMAX = os.environ.get("RVC_AMD_AMAX", "1") != "0"
+AMAX_PER_STAGE = 16
 
 
 def fold_weight_norm(weight: dict) -> dict:
@@ -191,12 +197,20 @@ class SynthesizerAMD:
         x = self.conv_pre(z.reshape(B, self.inter, T), pad=3, bias2=gdec)
         scale = 1.0
         nk = len(self.rks)
+        # the |max| side channel (ops.AmaxSlots, include/rvc_amd.h): in each stage y (written last by the noise conv),
+        # every unfused c1 output t1 and every non-last c2 output publish their |max|, and the convs reading them take
+        # their split-fp16 activation scale from it -- no per-tile pre-pass, so split-fp16 pays at k = 3 and 256
+        # channels too (rvc_model.cpp mirrors this cell by cell)
+        cells = ops.AmaxSlots(AMAX_PER_STAGE * len(self.ur), dev) if AMAX else None
         for i in range(len(self.ur)):
             up = self.ups[i]
             y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale)
             Li = y.shape[-1]
             nc, s, pad = self.noise[i]
-            nc(har.view(B, 1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True)
+            base = AMAX_PER_STAGE * i
+            ncell = 1
+            nc(har.view(B, 1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True,
+               amax_out=cells[base] if cells else None)
             C = self.chans[i]
             t1 = None  # c1 output of the unfused pairs
             xa = torch.empty(B, C, Li, device=dev)
@@ -205,23 +219,34 @@ class SynthesizerAMD:
             y = y.view(B, C, Li)
             for j, (kk, pairs) in enumerate(self.res[i]):
                 cur = y
+                cur_cell = cells[base] if cells else None
                 for m, (d, c1, c2) in enumerate(pairs):
                     last = m == len(pairs) - 1
                     if ops.resblock_fusable(c1, c2, d):  # one launch, c1's output stays in LDS
                         nxt = xs if last else (xa if cur is not xa else xb)
                         ops.resblock_pair(cur, nxt, c1, c2, d, LRELU_SLOPE, accumulate=last and j > 0)
                         cur = nxt
+                        cur_cell = None
                         continue
                     if t1 is None:
                         t1 = torch.empty(B, C, Li, device=dev)
-                    c1(cur, pad=(kk * d - d) // 2, dil=d, out=t1, in_act=ACT_LRELU, in_slope=LRELU_SLOPE)
+                    t1_cell = None
+                    if cells and ncell < AMAX_PER_STAGE:
+                        t1_cell, ncell = cells[base + ncell], ncell + 1
+                    c1(cur, pad=(kk * d - d) // 2, dil=d, out=t1, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
+                       amax_in=cur_cell, amax_out=t1_cell)
                     if m == len(pairs) - 1:
                         c2(t1, pad=(kk - 1) // 2, out=xs, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
-                           accumulate=(j > 0))
+                           accumulate=(j > 0), amax_in=t1_cell)
+                        cur_cell = None
                     else:
                         nxt = xa if cur is not xa else xb
-                        c2(t1, pad=(kk - 1) // 2, out=nxt, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE)
-                        cur = nxt
+                        nxt_cell = None
+                        if cells and ncell < AMAX_PER_STAGE:
+                            nxt_cell, ncell = cells[base + ncell], ncell + 1
+                        c2(t1, pad=(kk - 1) // 2, out=nxt, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
+                           amax_in=t1_cell, amax_out=nxt_cell)
+                        cur, cur_cell = nxt, nxt_cell
             del t1, xa, xb, y
             x = xs
             scale = 1.0 / nk
