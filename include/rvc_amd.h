@@ -62,6 +62,7 @@ int rvc_version(void);
  *   pre(v) = in_act(v * in_scale)
  */
 #define RVC_ARITH_F16X3 16 /* rvc_conv1d_args.wx_passes / rvc_resblock_args.passes: split-fp16, 3 passes */
+#define RVC_AMAX_SHARDS 64 /* u32 words per |max| cell (rvc_conv1d_args.amax_in / amax_out) */
 #define RVC_ARITH_FP32_SA 7 /* rvc_conv1d_args.wx_passes: 6-pass split-bf16 with the correction passes in their
                                own f32 accumulators (fewer roundings of the large sum; RMVPE) */
 
@@ -97,10 +98,11 @@ typedef struct rvc_conv1d_args {
        on the fp16 MFMA: ~2^-20 relative per product, f32 accumulation. */
     const void* wx;
     int wx_nmf, wx_passes;
-    /* Tensor |max| side channel (round 5): amax_out (or NULL) receives max |y| over every value the launch stores
-       (an atomic max on the f32 bits; the caller zeroes the word before the producing launch), and amax_in (or
-       NULL) is such a word for x: a split-fp16 launch (RVC_ARITH_F16X3) then takes its activation scale from it
-       (times |in_scale|: an upper bound of |pre(x)|) instead of a per-tile |max| pre-pass over its input. */
+    /* Tensor |max| side channel (round 5): amax_out (or NULL) is a cell of RVC_AMAX_SHARDS u32 words that receives
+       max |y| over every value the launch stores (atomic maxes of the f32 bits, spread over the words; the caller
+       zeroes the cell before the producing launch), and amax_in (or NULL) is such a cell for x: a split-fp16
+       launch (RVC_ARITH_F16X3) then takes its activation scale from the largest word (times |in_scale|: an upper
+       bound of |pre(x)|) instead of a per-tile |max| pre-pass over its input. */
     const unsigned* amax_in;
     unsigned* amax_out;
 } rvc_conv1d_args;
@@ -119,8 +121,8 @@ void rvc_conv1d_set_probe_event(void* hip_event);
 /* Diagnostic build only (-DRVC_CONV_STAMPS=1, scripts/conv_stamps.py): the split-operand conv engine's per-block
  * phase stamps (s_memtime) go to buf ([bytes / 2048][256] u64); returns -1 in a production build. */
 int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
-/* The split-operand engine's epilogue form for this thread's launches: 1 = the tile epilogue through LDS (the
- * default), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI.  Both give the same bits (tests/test_gpu_ops.py);
+/* The split-operand engine's epilogue form for this thread's launches: 1 = the tile epilogue through LDS (on the
+ * 128-wide tiles where it needs no extra LDS), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI (default 0).  Both give the same bits (tests/test_gpu_ops.py);
  * an A/B switch for measurements in one process. */
 int rvc_conv1d_set_tile_epi(int on);
 /* Split-K policy (this host thread): the library splits a conv's k range over blocks while its tile grid is

@@ -59,11 +59,20 @@ struct ConvParams {
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
 
-// amax_out: the wave's largest |stored value| folded into the tensor's word (atomic max of the f32 bits: for values
-// >= 0 the bit patterns order as the floats do).  Called by every lane of a wave (the shuffles need them all).
+// amax_out: the wave's largest |stored value| folded into the tensor's cell (atomic max of the f32 bits: for values
+// >= 0 the bit patterns order as the floats do).  A cell is RVC_AMAX_SHARDS words and each wave adds to one of them
+// (by block and wave): thousands of waves on ONE address serialise at the memory side (round 5: the generator ran
+// 904 -> 882 xRT with one word per tensor).  Called by every lane of a wave (the shuffles need them all).
 __device__ __forceinline__ void amax_publish(unsigned* amax_out, float m) {
     m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) atomicMax(amax_out, __float_as_uint(m));
+    const unsigned shard = (blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z + (threadIdx.x >> 6)) % RVC_AMAX_SHARDS;
+    if ((threadIdx.x & 63) == 0) atomicMax(amax_out + shard, __float_as_uint(m));
+}
+
+// the |max| of a cell: the largest of its shards (a wave-wide read: every lane of the calling wave must call it)
+__device__ __forceinline__ float amax_read(const unsigned* cell) {
+    const int l = threadIdx.x & 63;
+    return wave_max(__uint_as_float(cell[l < RVC_AMAX_SHARDS ? l : 0]));
 }
 
 // Output column n -> store position t; -1 when the column is not stored (beyond ncols / Lout);
@@ -717,7 +726,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             for (int it = 0; it < X6_NI; ++it) {
                 if (ltid + 256 * it < 4 * span) {
                     uint32_t hw[4], mw[4], lw[4];
-                    {  // the fast form (FASTL, never split-fp16)
+                    {  // the fast form (FASTL; split-fp16 only with the producer's |max|, amax_in)
                         const bool ok = (iok >> it) & 1u;
 #pragma unroll
                         for (int e2 = 0; e2 < 4; ++e2) {
@@ -726,7 +735,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                                 v0 = v0 >= 0.f ? v0 : v0 * p.in_slope;
                                 v1 = v1 >= 0.f ? v1 : v1 * p.in_slope;
                             }
-                            split3_pk(ok ? v0 : 0.f, ok ? v1 : 0.f, hw[e2], mw[e2], lw[e2]);
+                            if constexpr (F16) split2h_pk(ok ? v0 * sc : 0.f, ok ? v1 * sc : 0.f, hw[e2], mw[e2]);
+                            else split3_pk(ok ? v0 : 0.f, ok ? v1 : 0.f, hw[e2], mw[e2], lw[e2]);
                         }
                     }
                     const int pos = ipos[it];
@@ -783,12 +793,13 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 return m;
             };
             float am = 0.f;
-            if (p.amax_in) {
-                // the producer published |max| of the whole input tensor (amax side channel): no pre-pass
+            if (FASTL || p.amax_in) {
+                // the producer published |max| of the whole input tensor (amax side channel): no pre-pass (the fast
+                // form is only dispatched with amax_in, so its body never instantiates the pre-pass)
                 xload(pchunk(0), xr[0]);
                 xload(pchunk(1), xr[1]);
-                am = __uint_as_float(*p.amax_in) * fabsf(p.in_scale);
-            } else {
+                am = amax_read(p.amax_in) * fabsf(p.in_scale);
+            } else if constexpr (!FASTL) {
                 for (int i = 2; i < nck; i += 2) {
                     xload(pchunk(i), xr[0]);
                     xload(pchunk(i + 1 < nck ? i + 1 : i), xr[1]);
@@ -825,9 +836,13 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         }
         if (lw0) X6_STAMP(11, X6_NOW());
       };
-        // the loader body, once per form (a wave-uniform choice made once per block)
-        if constexpr (!F16) {
-            if ((Cig & 31) == 0 && p.in_scale == 1.f && (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
+        // the loader body, once per form (a wave-uniform choice made once per block); split-fp16 takes the fast form
+        // only with the producer's |max| (amax_in): with the per-tile pre-pass instantiated in both forms the 128 x 256
+        // kernel spilled 181 VGPRs (round 3)
+        // (the 8-compute-wave tiles only: on the 4-wave small tiles the fast form took them from 3 to 2 waves per SIMD)
+        if constexpr (!F16 || NCW == 8) {
+            if ((!F16 || p.amax_in) && (Cig & 31) == 0 && p.in_scale == 1.f &&
+                (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
                 if (p.in_act == RVC_ACT_LRELU) loader(std::true_type{}, std::true_type{});
                 else loader(std::true_type{}, std::false_type{});
             } else {
@@ -1307,7 +1322,9 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         // LDS footprint leaves no room on its CUs for the concurrent front-end streams' blocks (round 5, the 128 x 256
         // tile with a 133 KB tile: its epilogue no faster -- every CU's blocks reach it at once and it is HBM-bound --
         // and the clip stream 928 -> 889 xRT); and not on the 256-wide tile, whose epilogue measured 29k -> 33k cycles.
-        static const int tepi_env = getenv("RVC_X6_TILE_EPI") ? atoi(getenv("RVC_X6_TILE_EPI")) : 1;
+        // Off by default: even LDS-neutral it measured slower end to end (893-899 vs 899-905 xRT, interleaved on one
+        // box, r5c) -- kept as the RVC_X6_TILE_EPI=1 / rvc_conv1d_set_tile_epi(1) option, tested bit-identical.
+        static const int tepi_env = getenv("RVC_X6_TILE_EPI") ? atoi(getenv("RVC_X6_TILE_EPI")) : 0;
         const int tepi = g_tile_epi >= 0 ? g_tile_epi : tepi_env;
         const size_t tile_bytes = (size_t)BM * (BN + 4) * 4;
         const bool plain = a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&

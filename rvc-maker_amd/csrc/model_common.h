@@ -49,6 +49,7 @@ struct rvc_ctx {
     int rm_prec = RVC_PREC_FP64;  // RMVPE's arithmetic (rvc_ctx_set_rmvpe_precision), read by rvc_load_rmvpe
     bool x6 = true, f16mix = true, fused_rb = true;  // RVC_AMD_X6 / RVC_AMD_F16MIX / RVC_AMD_FUSED_RB as ops.py
     bool amax = true;  // RVC_AMD_AMAX as synth.py: the generator's |max| side channel
+    bool amax_f16all = true;  // RVC_AMD_AMAX_F16ALL as ops.py
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;
@@ -291,7 +292,7 @@ inline int base_passes(const rvc_ctx* c) { return c->prec == RVC_PREC_FP32 ? 6 :
 // amax: the input's |max| comes from its producer (the amax side channel): split-fp16 for every stride-1 1-D conv
 inline int conv_passes(const rvc_ctx* c, int K, int64_t Cig, int stride, bool two_d, bool amax = false) {
     if (c->prec == RVC_PREC_FP32 && c->f16mix && stride == 1 && !two_d &&
-        (amax || (K >= 7 && Cig <= 256) || (K >= 3 && Cig >= 64 && Cig <= 128)))
+        ((amax && c->amax_f16all) || (K >= 7 && Cig <= 256) || (K >= 3 && Cig >= 64 && Cig <= 128)))
         return RVC_ARITH_F16X3;
     return base_passes(c);
 }

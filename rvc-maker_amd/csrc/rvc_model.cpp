@@ -118,7 +118,7 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
     b.work = p.take(T);
     b.snoise = p.take(L);
     b.xpre = p.take((int64_t)g.upsample_initial_channel * T);
-    b.amax = p.take(kAmaxPerStage * 8);  // the |max| cells of the unfused ResBlock stages (synth.py generator)
+    b.amax = p.take(kAmaxPerStage * 8 * RVC_AMAX_SHARDS);  // the |max| cells of the ResBlock stages (synth.py generator)
     int64_t Lc = T;
     for (size_t i = 0; i < S.ups.size(); ++i) {
         Lc = convT_out_len(S.ups[i], Lc);
@@ -267,7 +267,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     float* xcur = A + bf.xpre;
     unsigned* amax = reinterpret_cast<unsigned*>(A + bf.amax);
     const bool use_amax = c->amax && (int64_t)S.ups.size() <= 8;
-    if (use_amax) MHIP(hipMemsetAsync(amax, 0, sizeof(unsigned) * kAmaxPerStage * S.ups.size(), s));
+    if (use_amax) MHIP(hipMemsetAsync(amax, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * kAmaxPerStage * S.ups.size(), s));
     {
         CallOpts o;
         o.pad = 3;
@@ -294,7 +294,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         on.accumulate = 1;
         // the |max| side channel (synth.py generator): y, each unfused c1 output and each non-last c2 output publish
         // their |max|; the convs that read them take their split-fp16 scale from it
-        unsigned* cell = use_amax ? amax + kAmaxPerStage * i : nullptr;
+        unsigned* cell = use_amax ? amax + RVC_AMAX_SHARDS * kAmaxPerStage * i : nullptr;
         int ncell = 1;
         if (cell) on.amax_out = cell;
         MTRY(conv(c, S, S.noise[i], har, L, y, on, s));
@@ -331,7 +331,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
                     cur_cell = nullptr;
                     continue;
                 }
-                unsigned* t1_cell = cell && ncell < kAmaxPerStage ? cell + ncell++ : nullptr;
+                unsigned* t1_cell = cell && ncell < kAmaxPerStage ? cell + RVC_AMAX_SHARDS * ncell++ : nullptr;
                 CallOpts o1;
                 o1.pad = (kk * P.d - P.d) / 2;
                 o1.dil = P.d;
@@ -353,7 +353,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
                     o2.accumulate = j > 0;
                 } else {
                     nxt = cur != xa ? xa : xb;
-                    nxt_cell = cell && ncell < kAmaxPerStage ? cell + ncell++ : nullptr;
+                    nxt_cell = cell && ncell < kAmaxPerStage ? cell + RVC_AMAX_SHARDS * ncell++ : nullptr;
                     o2.amax_out = nxt_cell;
                 }
                 MTRY(conv(c, S, P.c2, t1, Li, nxt, o2, s));
@@ -390,6 +390,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->f16mix = env_on("RVC_AMD_F16MIX");
     c->fused_rb = env_on("RVC_AMD_FUSED_RB");
     c->amax = env_on("RVC_AMD_AMAX");
+    c->amax_f16all = env_on("RVC_AMD_AMAX_F16ALL");
     *out = c;
     return RVC_OK;
 }

@@ -66,6 +66,10 @@ X6 = os.environ.get("RVC_AMD_X6", "1") != "0"
 F16X3 = 16  # RVC_ARITH_F16X3
 PASSES = {"fp32": 6, "fp32x6": 6, "fp32sa": 7, "f16x3": F16X3, "bf16x3": 3, "bf16": 1}
 F16_MIX = os.environ.get("RVC_AMD_F16MIX", "1") != "0"
+# with the producer's |max| (amax side channel), split-fp16 for every stride-1 1-D conv (RVC_AMD_AMAX_F16ALL=0: only
+# where conv_passes picks it anyway; the cell then just replaces the per-tile pre-pass)
+AMAX_F16ALL = os.environ.get("RVC_AMD_AMAX_F16ALL", "1") != "0"
+AMAX_SHARDS = 64  # RVC_AMAX_SHARDS: u32 words per |max| cell
 
 
 def conv_passes(K, Ci, stride=1, two_d=False, amax=False):
@@ -75,7 +79,7 @@ def conv_passes(K, Ci, stride=1, two_d=False, amax=False):
     1-D conv whose input's |max| comes from its producer (``amax``: no per-tile pre-pass, which is what made the
     short-tap and wide convs slower in split-fp16)."""
     if _PRECISION == "fp32" and F16_MIX and stride == 1 and not two_d and \
-            (amax or (K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128)):
+            ((amax and AMAX_F16ALL) or (K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128)):
         return F16X3
     return PASSES[_PRECISION]
 _PRECISION = os.environ.get("RVC_AMD_PRECISION", "fp32")
@@ -206,14 +210,14 @@ class ConvT:
 
 
 class AmaxSlots:
-    """n one-word |max| cells (the conv engine's amax side channel) for one pass, zeroed by one launch: ``s[k]`` is
-    cell k, handed to a producer as ``amax_out`` and to its consumers as ``amax_in``."""
+    """n |max| cells (the conv engine's amax side channel, AMAX_SHARDS words each) for one pass, zeroed by one
+    launch: ``s[k]`` is cell k, handed to a producer as ``amax_out`` and to its consumers as ``amax_in``."""
 
     def __init__(self, n, device):
-        self.words = torch.zeros(n, dtype=torch.int32, device=device)
+        self.words = torch.zeros(n * AMAX_SHARDS, dtype=torch.int32, device=device)
 
     def __getitem__(self, k):
-        return self.words[k:k + 1]
+        return self.words[k * AMAX_SHARDS:(k + 1) * AMAX_SHARDS]
 
 
 LAST_CONV_FLOPS = 0.0
