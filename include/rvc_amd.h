@@ -213,6 +213,14 @@ int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const
 /* GroupNorm(C, C) over time + affine (+ exact GELU)      fairseq.py:1149-1155,1183-1185 */
 int rvc_chnorm_gelu(const float* x, const float* gamma, const float* beta, float* out, int64_t B, int64_t C, int64_t L,
                     float eps, int gelu, rvc_stream_t stream);
+/* ContentVec's first layer fused (fairseq.py:1165-1195, layer 0): conv(1 -> C, k K, stride) of the 16 kHz signal x
+ * [B][N] (w_km: the K-major packed weight [K][C], no bias) + GroupNorm(C, C) over time + affine (+ exact GELU) ->
+ * out [B][C][T], T = (N - K) / stride + 1; statistics in f64.  ws: rvc_fe0_ws_bytes(B, C, T) device bytes.
+ * Replaces rvc_conv1d + rvc_chnorm_gelu for that layer (no HBM round trip of the conv output). */
+int64_t rvc_fe0_ws_bytes(int64_t B, int64_t C, int64_t T);
+int rvc_fe0_gn_gelu(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km, int64_t C, int K,
+                    int stride, const float* gamma, const float* beta, float* out, float eps, int gelu, void* ws,
+                    int64_t ws_bytes, rvc_stream_t stream);
 /* z_p = m + exp(logs) * noise * nscale, stats = [m; logs]  synthesizers.py:449 */
 int rvc_prior_sample(const float* stats, const float* noise, float* zp, int64_t B, int64_t C, int64_t T, float nscale,
                      rvc_stream_t stream);

@@ -219,3 +219,121 @@ extern "C" int rvc_chnorm_gelu(const float* x, const float* gamma, const float* 
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }
+
+// ---------------------------------------------------------------- ContentVec's first layer, fused (round 5)
+// conv(1 -> C, k K, stride S) + GroupNorm(C, C) over time + affine + exact GELU (fairseq.py:1165-1195 layer 0) without
+// the [C][T] conv output's HBM round trip: the conv (K FMAs per output) is cheap enough to compute twice.
+//   fe0_stats:  per (time tile, channel) f64 sum / sum of squares of the conv outputs  -> ws partials
+//   fe0_final:  per channel, the partials in tile order -> mean, 1 / sqrt(var + eps)
+//   fe0_apply:  the conv again (the same fmaf chain, so the same bits), normalise, GELU, one coalesced write
+// The separate conv + chnorm_gelu wrote the 210 MB output of a 32 s input at 0.4 TB/s and read it twice.
+// w is the conv's K-major packed weight ([K][C], ops.Conv / ConvW); x the 16 kHz signal [B][N] (batch stride xbs).
+constexpr int FE0_TT = 256;   // frames per tile
+constexpr int FE0_KMAX = 16;  // taps (ContentVec: 10)
+
+__device__ __forceinline__ float fe0_conv(const float* w, const float* xw, int c, int C, int K) {
+    float y = 0.f;
+    for (int k = 0; k < K; ++k) y = fmaf(w[k * C + c], xw[k], y);
+    return y;
+}
+
+__global__ __launch_bounds__(512) void fe0_stats_kernel(const float* x, int64_t xbs, int64_t T, const float* w, int C,
+                                                        int K, int S, double* part) {
+    __shared__ float xs[FE0_TT * 8 + FE0_KMAX];
+    const int b = blockIdx.y, tile = blockIdx.x;
+    const int64_t t0 = (int64_t)tile * FE0_TT;
+    const int nt = (int)min((int64_t)FE0_TT, T - t0);
+    const float* xb = x + b * xbs + t0 * S;
+    const int nx = (nt - 1) * S + K;
+    for (int i = threadIdx.x; i < nx; i += blockDim.x) xs[i] = xb[i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float wr[FE0_KMAX];
+        for (int k = 0; k < K; ++k) wr[k] = w[k * C + c];
+        double s = 0.0, q = 0.0;
+        for (int t = 0; t < nt; ++t) {
+            float y = 0.f;
+            for (int k = 0; k < K; ++k) y = fmaf(wr[k], xs[t * S + k], y);
+            s += y;
+            q += (double)y * y;
+        }
+        double* pp = part + (((int64_t)b * gridDim.x + tile) * C + c) * 2;
+        pp[0] = s;
+        pp[1] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void fe0_final_kernel(const double* part, int ntile, int C, int64_t T, float eps,
+                                                        float* stat) {
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < ntile; ++i) {
+        const double* pp = part + (((int64_t)b * ntile + i) * C + c) * 2;
+        s += pp[0];
+        q += pp[1];
+    }
+    const double mean = s / (double)T;
+    const double var = fmax(q / (double)T - mean * mean, 0.0);
+    stat[((int64_t)b * C + c) * 2] = (float)mean;
+    stat[((int64_t)b * C + c) * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+__global__ __launch_bounds__(256) void fe0_apply_kernel(const float* x, int64_t xbs, int64_t T, const float* w, int C,
+                                                        int K, int S, const float* stat, const float* gamma,
+                                                        const float* beta, float* out, int gelu) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // w [K][C], then (mean, rstd, gamma, beta) [C][4]
+    float* ws = sm;
+    float* cs = sm + K * C;
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < K * C; i += blockDim.x) ws[i] = w[i];
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        cs[4 * c] = stat[((int64_t)b * C + c) * 2];
+        cs[4 * c + 1] = stat[((int64_t)b * C + c) * 2 + 1];
+        cs[4 * c + 2] = gamma[c];
+        cs[4 * c + 3] = beta[c];
+    }
+    __syncthreads();
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    float xw[FE0_KMAX];
+    const float* xb = x + b * xbs + t * S;
+    for (int k = 0; k < K; ++k) xw[k] = xb[k];
+    float* ob = out + (int64_t)b * C * T + t;
+    for (int c = 0; c < C; ++c) {
+        const float y = fe0_conv(ws, xw, c, C, K);
+        const float v = (y - cs[4 * c]) * cs[4 * c + 1] * cs[4 * c + 2] + cs[4 * c + 3];
+        ob[(int64_t)c * T] = gelu ? act_apply(v, RVC_ACT_GELU, 0.f) : v;
+    }
+}
+
+extern "C" int64_t rvc_fe0_ws_bytes(int64_t B, int64_t C, int64_t T) {
+    if (B <= 0 || C <= 0 || T <= 0) return -1;
+    const int64_t ntile = (T + FE0_TT - 1) / FE0_TT;
+    return B * ntile * C * 2 * 8 + B * C * 2 * 4 + 256;
+}
+
+extern "C" int rvc_fe0_gn_gelu(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km, int64_t C,
+                               int K, int stride, const float* gamma, const float* beta, float* out, float eps,
+                               int gelu, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
+    RVC_CHECK_ARG(x && w_km && gamma && beta && out && ws && B > 0 && C > 0 && C <= 4096 && K > 0 &&
+                      K <= FE0_KMAX && stride > 0 && stride <= 8 && N >= K,
+                  "fe0_gn_gelu: bad args");
+    const int64_t T = (N - K) / stride + 1;
+    RVC_CHECK_ARG(ws_bytes >= rvc_fe0_ws_bytes(B, C, T), "fe0_gn_gelu: workspace too small");
+    const int64_t xbs = x_bstride ? x_bstride : N;
+    const int ntile = (int)((T + FE0_TT - 1) / FE0_TT);
+    double* part = (double*)ws;
+    float* stat = (float*)((char*)ws + B * ntile * C * 2 * 8);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(fe0_stats_kernel, dim3(ntile, (unsigned)B), dim3(512), 0, s, x, xbs, T, w_km, (int)C, K, stride,
+                       part);
+    hipLaunchKernelGGL(fe0_final_kernel, dim3((unsigned)((C + 255) / 256), (unsigned)B), dim3(256), 0, s, part, ntile,
+                       (int)C, T, eps, stat);
+    const size_t lds = (size_t)(K * C + 4 * C) * 4;
+    hipLaunchKernelGGL(fe0_apply_kernel, dim3((unsigned)((T + 255) / 256), (unsigned)B), dim3(256), lds, s, x, xbs, T,
+                       w_km, (int)C, K, stride, stat, gamma, beta, out, gelu);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
+}

@@ -98,15 +98,20 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
     const int64_t L0 = (N - kFeLayers[0][1]) / kFeLayers[0][2] + 1;
     bufs[0] = sc.take(512 * L0);
     bufs[1] = sc.take(512 * L0);
+    float* fe0ws = sc.take((rvc_fe0_ws_bytes(1, 512, L0) + 3) / 4);
     for (int i = 0; i < 7; ++i) {
         const int k = kFeLayers[i][1], st = kFeLayers[i][2];
         const int64_t Lo = (L - k) / st + 1;
         float* y = bufs[i & 1];
-        CallOpts o;
-        o.stride = st;
-        if (i > 0) o.out_act = RVC_ACT_GELU;
-        RUN(conv(c, M, M.fe[i], x, L, y, o, s));
-        if (i == 0) RUN(rvc_chnorm_gelu(y, M.gn_w, M.gn_b, y, 1, 512, Lo, 1e-5f, 1, s));
+        if (i == 0) {  // conv + GroupNorm + GELU fused (rvc_fe0_gn_gelu, as contentvec.py)
+            RUN(rvc_fe0_gn_gelu(x, 1, L, 0, M.fe[0].w, 512, k, st, M.gn_w, M.gn_b, y, 1e-5f, 1, fe0ws,
+                                rvc_fe0_ws_bytes(1, 512, Lo), s));
+        } else {
+            CallOpts o;
+            o.stride = st;
+            o.out_act = RVC_ACT_GELU;
+            RUN(conv(c, M, M.fe[i], x, L, y, o, s));
+        }
         x = y;
         L = Lo;
     }

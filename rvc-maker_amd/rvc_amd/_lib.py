@@ -148,6 +148,9 @@ SIGNATURES = {
     "rvc_layernorm_cf": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
                          c_void_p],
     "rvc_chnorm_gelu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_int, c_void_p],
+    "rvc_fe0_ws_bytes": [c_int64, c_int64, c_int64],
+    "rvc_fe0_gn_gelu": [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                        c_float, c_int, c_void_p, c_int64, c_void_p],
     "rvc_prior_sample": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_gate": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_flip_channels": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
@@ -254,7 +257,8 @@ _RESTYPES = {"rvc_last_error": ctypes.c_char_p, "rvc_conv1d_workspace_bytes": c_
              "rvc_ctx_destroy": None, "rvc_conv1d_set_probe_event": None, "rvc_synth_out_len": c_int64,
              "rvc_contentvec_frames": c_int64, "rvc_rmvpe_frames": c_int64, "rvc_rmvpe_salience_ld": c_int64,
              "rvc_vc_out_len": c_int64, "rvc_device_bytes_in_use": c_int64,
-             "rvc_quiet_points_count": c_int64, "rvc_f0_file_resample": c_int64, "rvc_quiet_points_ws_bytes": c_int64}
+             "rvc_quiet_points_count": c_int64, "rvc_f0_file_resample": c_int64, "rvc_quiet_points_ws_bytes": c_int64,
+             "rvc_fe0_ws_bytes": c_int64}
 
 _lib = None
 

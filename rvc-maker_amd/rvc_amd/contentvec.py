@@ -8,7 +8,7 @@ main/library/utils.py:157-165: config.json + model.safetensors); pos_conv weight
 host at load.  The two layouts are the same network; the embed suffix only changes which layer feeds
 final_proj (``embed_cf``, convert.py:337-345).  Activations stay channels-first [C][T] on the device:
 
-  conv FE   conv1d(1->512, k10 s5) + chnorm_gelu (GroupNorm(512,512) + GELU), 6 x conv1d(k3/k2, s2) + GELU
+  conv FE   fe0_gn_gelu (conv1d(1->512, k10 s5) + GroupNorm(512,512) + GELU fused), 6 x conv1d(k3/k2, s2) + GELU
   proj      layernorm_cf(512) + conv1d(K=1, 512->768)
   encoder   pos_conv (grouped conv k128, SamePad, GELU, +x fused) + LN, then post-LN layers:
             fused QKV conv, flash attention (12 x 64), out_proj, LN(x+y), fc1+GELU, fc2, LN(x+y)
@@ -213,9 +213,8 @@ class ContentVecAMD:
         B, N = (wav.shape[0], wav.shape[1]) if batched else (1, wav.numel())
         x = wav.reshape(B, 1, N) if batched else wav.view(1, N)
         for i, (c, k, s) in enumerate(FE_LAYERS):
-            if i == 0:
-                x = self.fe[0](x, stride=s)
-                ops.chnorm_gelu(x, self.gn[0], self.gn[1], x, B, c, x.shape[-1])
+            if i == 0:  # conv + GroupNorm + GELU in one pass over the signal (rvc_fe0_gn_gelu)
+                x = ops.fe0_gn_gelu(wav.contiguous(), self.fe[0].w, self.gn[0], self.gn[1], B, N, c, k, s)
             else:
                 x = self.fe[i](x, stride=s, out_act=ACT_GELU)
         T = x.shape[-1]

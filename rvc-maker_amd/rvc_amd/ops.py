@@ -433,6 +433,19 @@ def chnorm_gelu(x, gamma, beta, out, B, C, L, eps=1e-5, gelu=True):
     return out
 
 
+def fe0_gn_gelu(wav, w_km, gamma, beta, B, N, C, K, stride, eps=1e-5, gelu=True, x_bstride=0):
+    """ContentVec's first layer fused: conv(1 -> C, k K, stride) of wav [B][N] + GroupNorm(C, C) + affine + GELU
+    -> [B][C][T] (rvc_fe0_gn_gelu; w_km: the K-major packed conv weight [K][C], ops.Conv.w)."""
+    lib = _lib.load()
+    T = (N - K) // stride + 1
+    out = torch.empty(B, C, T, device=wav.device) if B > 1 else torch.empty(C, T, device=wav.device)
+    need = lib.rvc_fe0_ws_bytes(B, C, T)
+    ws = _workspace(wav.device, need, kind="fe0")
+    check(lib.rvc_fe0_gn_gelu(_p(wav), B, N, x_bstride, _p(w_km), C, K, stride, _p(gamma), _p(beta), _p(out), eps,
+                              int(gelu), _p(ws), need, _stream()), "fe0_gn_gelu")
+    return out
+
+
 def prior_sample(stats, noise, zp, B, C, T, nscale=0.66666):
     check(_lib.load().rvc_prior_sample(_p(stats), _p(noise), _p(zp), B, C, T, nscale, _stream()), "prior_sample")
     return zp

@@ -73,10 +73,10 @@ def analyse(st, nblk, K, kname):
     res["mfma_busy_block"] = float(mf * nc / max(res["block_cycles_med"], 1))
     # CU timeline: HW_ID (CU / SE fields) + XCC, blocks per CU, gap between a CU's consecutive blocks (realtime, 10 ns)
     hw = st[:, 2].astype(np.int64)
-    cu_key = (st[:, 13].astype(np.int64) << 32) | (hw & 0xFFFF0F00)  # XCC, SE/SH/CU fields (wave slot bits dropped)
+    cu_key = (st[:, 13].astype(np.int64) << 32) | ((hw >> 8) & 0xFF)  # XCC, then HW_ID's CU / SH / SE fields
     rt = st[:, 1].astype(np.float64)
     dur_rt = (d(0, 7) / max(res["block_cycles_med"], 1)) * 0  # placeholder (memtime and realtime differ in rate)
-    gaps, per_cu = [], []
+    gaps, per_cu, ends = [], [], []
     clk = None
     for k in np.unique(cu_key):
         idx = np.where(cu_key == k)[0]
@@ -84,11 +84,16 @@ def analyse(st, nblk, K, kname):
         per_cu.append(len(order))
         for a, b in zip(order[:-1], order[1:]):
             gaps.append(rt[b] - rt[a])
+            # the next block's start against this block's end, in the CU's own shader clock
+            ends.append(float(st[b, 0]) - float(st[a, 7]) if st[b, 0] > st[a, 7] else np.nan)
     res["cus_seen"] = int(len(per_cu))
     res["blocks_per_cu_med"] = float(np.median(per_cu))
     if gaps:
         res["cu_block_period_us_med"] = float(np.median(gaps)) / 100.0  # 100 MHz realtime
     res["launch_span_us"] = float((rt.max() - rt.min()) / 100.0)
+    if ends:
+        e = np.array(ends, dtype=np.float64)
+        res["next_block_start_after_end_cyc_med"] = float(np.nanmedian(e)) if np.isfinite(e).any() else None
     return res
 
 
@@ -97,6 +102,8 @@ def main():
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default="")
+    ap.add_argument("--amax", action="store_true", help="hand each conv its input's |max| (the amax side channel, "
+                                                        "as the generator does): no split-fp16 pre-pass")
     args = ap.parse_args()
     from rvc_amd import _lib, ops
     lib = _lib.load()
@@ -118,6 +125,10 @@ def main():
         y = torch.empty(Co, L, device="cuda")
         p = d * (K - 1) // 2
         kw = dict(pad=p, dil=d, out=y, res=res)
+        if args.amax:
+            cell = ops.AmaxSlots(1, "cuda")
+            cell.words[0] = int(np.float32(x.abs().max().item()).view(np.int32))
+            kw["amax_in"] = cell[0]
         if rb:
             kw.update(in_act=ops.ACT_LRELU, in_slope=0.1)
         for _ in range(3):
@@ -146,6 +157,8 @@ def main():
               + (f" (f16 scale wait {r['f16_scale_wait_med']:.0f}, loader pre-pass {r['loader_prepass_med']:.0f})"
                  if 'f16_scale_wait_med' in r else "")
               + f" + loop {r['loop_med']:.0f} + epilogue {r['epilogue_med']:.0f};  loader chunk0 {r['loader_chunk0_med']:.0f}")
+        print(f"   CU period {r.get('cu_block_period_us_med', 0):.1f} us; next block starts "
+              f"{r.get('next_block_start_after_end_cyc_med')} cyc after wave 0's epilogue stamp")
         print(f"   per chunk: compute {pc['compute_med']:.0f} + barrier wait {pc['barrier_wait_med']:.0f} (MFMA-bound "
               f"{pc['mfma_bound']:.0f}); loader busy {pc['loader_busy_med']:.0f} wait {pc['loader_wait_med']:.0f};  "
               f"MFMA busy in loop {r['mfma_busy_in_loop']:.2f}, over the block {r['mfma_busy_block']:.2f}")

@@ -431,3 +431,19 @@ def test_x6_tile_epilogue_bit_identical(ops, prec, Ci, Co, K, d, L, B, epi):
         finally:
             lib.rvc_conv1d_set_tile_epi(-1)
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+
+
+@pytest.mark.parametrize("B,N", [(1, 16000 * 3 + 123), (2, 8000), (1, 400)])
+def test_fe0_gn_gelu(ops, B, N):
+    """ContentVec's first layer fused (rvc_fe0_gn_gelu: conv 1 -> 512, k10 s5, GroupNorm(512, 512), GELU) against
+    torch's f64 evaluation of the reference's layers (fairseq.py:1165-1195)."""
+    g = gen(21)
+    wav = torch.randn(B, N, generator=g) * 0.3
+    w = torch.randn(512, 1, 10, generator=g) * 0.3
+    gamma, beta = torch.rand(512, generator=g) + 0.5, torch.randn(512, generator=g) * 0.1
+    y = F.conv1d(wav.double().unsqueeze(1), w.double(), None, 5)
+    ref = F.gelu(F.group_norm(y, 512, gamma.double(), beta.double(), 1e-5))
+    c = ops.Conv(w, None)
+    out = ops.fe0_gn_gelu(wav.to(DEV).contiguous(), c.w, gamma.to(DEV), beta.to(DEV), B, N, 512, 10, 5)
+    got = out.cpu().double().reshape(ref.shape)
+    assert (got - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
