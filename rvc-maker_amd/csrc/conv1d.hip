@@ -50,6 +50,7 @@ struct ConvParams {
     int dbg;  // RVC_CONV_DEBUG (profiling only): 1 = no epilogue, 2 = no MFMA, 4 = loaders skip global loads
     int tile_epi;  // x6: the tile epilogue through LDS (x6_tile_epilogue), set by plan() for plain stride-1 stores
     const unsigned* amax_in;  // |max| of x (f32 bits) or null: split-fp16 loaders take their scale from it
+    int f16_fast;             // split-fp16 with amax_in: the fast loader form (RVC_X6_F16FAST, A/B switch)
     unsigned* amax_out;       // or null: max |y| over the stored values (atomic max of the f32 bits)
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
@@ -841,7 +842,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         // kernel spilled 181 VGPRs (round 3)
         // (the 8-compute-wave tiles only: on the 4-wave small tiles the fast form took them from 3 to 2 waves per SIMD)
         if constexpr (!F16 || NCW == 8) {
-            if ((!F16 || p.amax_in) && (Cig & 31) == 0 && p.in_scale == 1.f &&
+            if ((!F16 || (p.amax_in && p.f16_fast)) && (Cig & 31) == 0 && p.in_scale == 1.f &&
                 (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
                 if (p.in_act == RVC_ACT_LRELU) loader(std::true_type{}, std::true_type{});
                 else loader(std::true_type{}, std::false_type{});
@@ -1169,6 +1170,8 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.tile_epi = 0;
     p.amax_in = a->amax_in;
     p.amax_out = a->amax_out;
+    static const int f16fast = getenv("RVC_X6_F16FAST") ? atoi(getenv("RVC_X6_F16FAST")) : 1;
+    p.f16_fast = f16fast;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;

@@ -349,8 +349,8 @@ class VC:
         list of device waveforms, ordered on the caller's current stream.  ``events`` (a list) collects
         timing events (role, group, torch.cuda.Event) at each group's front / back start and end.  ``host_out``
         (a list of pinned host f32 tensors, one per clip, each at least the clip's output length) receives each
-        waveform as it is finished: a non-blocking copy on the caller's stream after that clip's synthesizer,
-        overlapping the next clips' work (the reference's ``.cpu()`` of each output, convert.py:455)."""
+        waveform as it is finished: a non-blocking copy on the synthesizer's stream right after that clip,
+        overlapping the next clips' front end (the reference's ``.cpu()`` of each output, convert.py:455)."""
 
         def mark(role, g, stream):
             if events is not None:
@@ -384,12 +384,11 @@ class VC:
 
         def emit(out):
             outs.append(out)
-            if host_out is not None:  # D2H of this clip on the caller's stream, behind its synthesizer only
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(dev))
-                caller.wait_event(ev)
-                with torch.cuda.stream(caller):
-                    host_out[len(outs) - 1][: out.numel()].copy_(out, non_blocking=True)
+            if host_out is not None:
+                # D2H of this clip on the back stream, right behind its synthesizer.  (On the caller's stream it made
+                # the caller wait for each clip, and the front streams wait for the caller before every group: the
+                # front end then never ran more than one clip ahead -- round 5 timeline, the back stream idle 35 %.)
+                host_out[len(outs) - 1][: out.numel()].copy_(out, non_blocking=True)
 
         def issue_front(group, g):
             """front end of one group on the front / fside streams -> ([(xp, coarse, pitchf, feats)], event).
