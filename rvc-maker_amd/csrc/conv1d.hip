@@ -428,6 +428,9 @@ constexpr bool kAblations = RVC_CONV_ABLATIONS != 0;
 #ifndef X6_PD8
 #define X6_PD8 0
 #endif
+#ifndef X6_F16FAST
+#define X6_F16FAST 0
+#endif
 // In-kernel stamps (diagnostic build -DRVC_CONV_STAMPS=1 only; scripts/conv_stamps.py): compute wave 0 and the first
 // loader wave record s_memtime at the phase boundaries of each block into a buffer of their own (never an output),
 // one lane, vector stores.  Layout per block (X6_STAMP_W words): 0 compute start, 1 memrealtime at start, 2 HW_ID,
@@ -796,10 +799,12 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             float am = 0.f;
             if (FASTL || p.amax_in) {
                 // the producer published |max| of the whole input tensor (amax side channel): no pre-pass (the fast
-                // form is only dispatched with amax_in, so its body never instantiates the pre-pass)
+                // form is only dispatched with amax_in, so its body never instantiates the pre-pass).  The cell is
+                // read before the chunk loads are issued: behind them (vmcnt counts in order) its wait would include
+                // two chunks' HBM latency
+                am = amax_read(p.amax_in) * fabsf(p.in_scale);
                 xload(pchunk(0), xr[0]);
                 xload(pchunk(1), xr[1]);
-                am = amax_read(p.amax_in) * fabsf(p.in_scale);
             } else if constexpr (!FASTL) {
                 for (int i = 2; i < nck; i += 2) {
                     xload(pchunk(i), xr[0]);
@@ -841,7 +846,10 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         // only with the producer's |max| (amax_in): with the per-tile pre-pass instantiated in both forms the 128 x 256
         // kernel spilled 181 VGPRs (round 3)
         // (the 8-compute-wave tiles only: on the 4-wave small tiles the fast form took them from 3 to 2 waves per SIMD)
-        if constexpr (!F16 || NCW == 8) {
+        // (X6_F16FAST=1 builds the split-fp16 fast form too: its loader registers pushed the 128 x 256 kernel's spills
+        // from 34 to 93 VGPRs and its prologue, under the amax read, from 19k to 61k cycles -- end to end neutral,
+        // r5f; off)
+        if constexpr (!F16 || (NCW == 8 && X6_F16FAST)) {
             if ((!F16 || (p.amax_in && p.f16_fast)) && (Cig & 31) == 0 && p.in_scale == 1.f &&
                 (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
                 if (p.in_act == RVC_ACT_LRELU) loader(std::true_type{}, std::true_type{});
@@ -852,7 +860,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         } else {
             loader(std::false_type{}, std::false_type{});
         }
-        if (p.tile_epi == 1) {  // the compute waves' tile is in LDS after this barrier
+        if (BN > 128) {  // (plan() never sets tile_epi on the 256-wide tile: not compiled there)
+        } else if (p.tile_epi == 1) {  // the compute waves' tile is in LDS after this barrier
             __syncthreads();
             x6_tile_epilogue<BM, BN, 64 * (NCW + 4)>(p, reinterpret_cast<const float*>(xs), tid, split, b, m0g, n0);
         } else if (p.tile_epi == 2) {  // in two row halves (the tile is twice the X buffers' LDS)
@@ -1022,7 +1031,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 for (int j = 0; j < FN; ++j) acc[i][j][r] *= f;
             }
     }
-    if (p.tile_epi) {
+    if (BN <= 128 && p.tile_epi) {
         // bias, 2nd bias, activation and scale in registers (conv_epilogue's order), then the fragments into LDS: row
         // (wm * 16 FM + 16 i + 4 lg + r), column (wn * 16 FN + 16 j + ln); a row stride of BN + 4 floats puts the two
         // 16-lane halves of each ds_write_b32 on different banks
