@@ -70,10 +70,15 @@ __device__ __forceinline__ void amax_publish(unsigned* amax_out, float m) {
     if ((threadIdx.x & 63) == 0) atomicMax(amax_out + shard, __float_as_uint(m));
 }
 
-// the |max| of a cell: the largest of its shards (a wave-wide read: every lane of the calling wave must call it)
+// the |max| of a cell: the largest of its shards, read through the scalar cache (wave-uniform address, s_load: it does
+// not queue behind the wave's vector loads in vmcnt order, and no shuffle)
+typedef const __attribute__((address_space(4))) unsigned* amax_const_ptr;  // constant space: s_load
 __device__ __forceinline__ float amax_read(const unsigned* cell) {
-    const int l = threadIdx.x & 63;
-    return wave_max(__uint_as_float(cell[l < RVC_AMAX_SHARDS ? l : 0]));
+    const amax_const_ptr c = (amax_const_ptr)cell;  // read-only for the whole launch
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < RVC_AMAX_SHARDS; ++i) m = max(m, c[i]);
+    return __uint_as_float(m);
 }
 
 // Output column n -> store position t; -1 when the column is not stored (beyond ncols / Lout);

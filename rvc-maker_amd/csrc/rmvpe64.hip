@@ -591,6 +591,32 @@ __global__ void mel_image64_kernel(const double* mel, double* img, int M, int64_
     if (t >= Tp || m >= M) return;
     const int64_t s = t < F ? t : 2 * (F - 1) - t;
     img[(t + 1) * (M + 2) + m + 1] = mel[(int64_t)m * F + s] * scale + shift;
+    // the zero border too (the image needs no zero-fill launch before it)
+    if (m == 0) {
+        img[(t + 1) * (M + 2)] = 0.0;
+        img[(t + 1) * (M + 2) + M + 1] = 0.0;
+    }
+    if (t == 0 || t == Tp - 1) {
+        double* row = img + (t == 0 ? 0 : (Tp + 1) * (M + 2));
+        row[m + 1] = 0.0;
+        if (m == 0) {
+            row[0] = 0.0;
+            row[M + 1] = 0.0;
+        }
+    }
+}
+
+// the zero border cells beside interior cell (y, x) of a [H + 2][W + 2] plane (corners by the corner cells)
+RVC_DEV void border_zero64(double* plane, int y, int x, int H, int W) {
+    const int R = W + 2;
+    if (x == 0) plane[(int64_t)(y + 1) * R] = 0.0;
+    if (x == W - 1) plane[(int64_t)(y + 1) * R + W + 1] = 0.0;
+    if (y == 0 || y == H - 1) {
+        double* row = plane + (y == 0 ? 0 : (int64_t)(H + 1) * R);
+        row[x + 1] = 0.0;
+        if (x == 0) row[0] = 0.0;
+        if (x == W - 1) row[W + 1] = 0.0;
+    }
 }
 
 // AvgPool2d(2): ((a + b) + c) + d, / 4
@@ -610,6 +636,7 @@ __global__ void avgpool2_64_kernel(const double* in, double* out, int C, int H, 
     s += ib[a0 + W + 2];
     s += ib[a0 + W + 3];
     out[(int64_t)c * (Ho + 2) * (Wo + 2) + (int64_t)(y + 1) * (Wo + 2) + x + 1] = s / 4.0;
+    border_zero64(out + (int64_t)c * (Ho + 2) * (Wo + 2), y, x, Ho, Wo);
 }
 
 __global__ void interleave4_64_kernel(const double* ph, double* out, int C, int H, int W, int64_t ph_bs,
@@ -626,6 +653,7 @@ __global__ void interleave4_64_kernel(const double* ph, double* out, int C, int 
     const int64_t plane = (int64_t)(H + 2) * (W + 2);
     out[(int64_t)c * (Ho + 2) * (Wo + 2) + (int64_t)(yo + 1) * (Wo + 2) + xo + 1] =
         ph[((int64_t)(py * 2 + px) * C + c) * plane + (int64_t)(y + 1) * (W + 2) + x + 1];
+    border_zero64(out + (int64_t)c * (Ho + 2) * (Wo + 2), yo, xo, Ho, Wo);
 }
 
 __global__ void img_to_seq64_kernel(const double* img, double* x, int C, int64_t H, int W, int64_t img_bs,

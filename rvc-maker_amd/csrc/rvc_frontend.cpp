@@ -573,7 +573,6 @@ int rm_one64(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, flo
     }
     int64_t H = Tp, W = kMels;
     double* x = take64(sc, (H + 2) * (W + 2));
-    RUN(hipMemsetAsync(x, 0, (H + 2) * (W + 2) * 8, s) == hipSuccess ? RVC_OK : RVC_EHIP);
     RUN(rvc_mel_image64(mel, x, 1, kMels, F, Tp, M.in_scale64, M.in_shift64, 0, 0, s));
     struct Cat {
         double* buf;
@@ -585,7 +584,6 @@ int rm_one64(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, flo
     for (size_t l = 0; l < M.enc.size(); ++l) {
         const int64_t img = (H + 2) * (W + 2);
         double* cat = take64(sc, 2 * C * img);
-        RUN(hipMemsetAsync(cat, 0, 2 * C * img * 8, s) == hipSuccess ? RVC_OK : RVC_EHIP);
         for (int b = 0; b < nb; ++b) {
             double* out = b == nb - 1 ? cat + C * img : take64(sc, C * img);
             MTRY(cbr_run64(M, sc, M.enc[l][b], x, H, W, out, s));
@@ -593,7 +591,6 @@ int rm_one64(rvc_ctx* c, Rmvpe& M, Scratch& sc, const float* wav, int64_t N, flo
         }
         cats.push_back({cat, C, H, W});
         double* pooled = take64(sc, C * (H / 2 + 2) * (W / 2 + 2));
-        RUN(hipMemsetAsync(pooled, 0, C * (H / 2 + 2) * (W / 2 + 2) * 8, s) == hipSuccess ? RVC_OK : RVC_EHIP);
         RUN(rvc_avgpool2_64(x, pooled, 1, C, H, W, 0, 0, s));
         x = pooled;
         H /= 2;

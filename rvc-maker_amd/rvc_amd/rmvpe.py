@@ -253,7 +253,8 @@ class RMVPEAMD:
         F = mel.shape[-1]
         Tp = 32 * ((F - 1) // 32 + 1)
         mel = mel.to(self.dt).contiguous()  # a caller's f32 mel (the reference's mel2hidden input) in the f64 form
-        x = torch.zeros(1, Tp + 2, N_MELS + 2, device=mel.device, dtype=self.dt)
+        # (the f64 kernels write the zero border themselves: no zero-fill launch on the f0 chain)
+        x = (torch.empty if self.f64 else torch.zeros)(1, Tp + 2, N_MELS + 2, device=mel.device, dtype=self.dt)
         (ops.mel_image64 if self.f64 else ops.mel_image)(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
         return x, Tp
 
@@ -282,13 +283,16 @@ class RMVPEAMD:
         cats = []
         C = 16
         for l in range(5):
-            cat = torch.zeros(*bshape, 2 * C, H + 2, W + 2, device=dev, dtype=self.dt)
+            # cat[C:] is written whole by the encoder's last conv (border included), cat[:C] by the decoder's
+            # interleave (which writes its border in the f64 form); pooled by the f64 pooling, border included
+            alloc = torch.empty if self.f64 else torch.zeros
+            cat = alloc(*bshape, 2 * C, H + 2, W + 2, device=dev, dtype=self.dt)
             for b, blk in enumerate(self.enc[l]):
                 out = cat[..., C:, :, :] if b == self.nb - 1 else \
                     torch.empty(*bshape, C, H + 2, W + 2, device=dev, dtype=self.dt)
                 x = self._cbr(blk, x, H, W, out)
             cats.append((cat, C, H, W))
-            pooled = torch.zeros(*bshape, C, H // 2 + 2, W // 2 + 2, device=dev, dtype=self.dt)
+            pooled = alloc(*bshape, C, H // 2 + 2, W // 2 + 2, device=dev, dtype=self.dt)
             self._pool(x, pooled, C, H, W)
             x, H, W = pooled, H // 2, W // 2
             C *= 2
@@ -373,7 +377,7 @@ class RMVPEAMD:
         B, _, F = mel.shape
         Tp = 32 * ((F - 1) // 32 + 1)
         mel = mel.to(self.dt).contiguous()
-        x = torch.zeros(B, 1, Tp + 2, N_MELS + 2, device=dev, dtype=self.dt)
+        x = (torch.empty if self.f64 else torch.zeros)(B, 1, Tp + 2, N_MELS + 2, device=dev, dtype=self.dt)
         if self.f64:
             ops.mel_image64(mel, x, N_MELS, F, Tp, self.in_scale, self.in_shift)
         else:
