@@ -125,6 +125,9 @@ int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
  * 128-wide tiles where it needs no extra LDS), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI (default 0).  Both give the same bits (tests/test_gpu_ops.py);
  * an A/B switch for measurements in one process. */
 int rvc_conv1d_set_tile_epi(int on);
+/* Per-thread override of the split-fp16 loaders' fast form (used with amax_in on the 8-compute-wave tiles; same
+ * bits as the general form): 1 on, 0 off, -1 back to RVC_X6_F16FAST (default on).  Diagnostic / test knob. */
+int rvc_conv1d_set_f16_fast(int on);
 /* Split-K policy (this host thread): the library splits a conv's k range over blocks while its tile grid is
  * below `target` tiles (default 256 = 1 per CU, halved for tiles of which one block fills a CU; or
  * RVC_SPLITK_TILES); 0 = never split, -1 = back to the default.  Returns the previous setting.  Results depend on it at f32 rounding level (the split changes the

@@ -52,11 +52,16 @@ struct ConvParams {
     const unsigned* amax_in;  // |max| of x (f32 bits) or null: split-fp16 loaders take their scale from it
     int f16_fast;             // split-fp16 with amax_in: the fast loader form (RVC_X6_F16FAST, A/B switch)
     unsigned* amax_out;       // or null: max |y| over the stored values (atomic max of the f32 bits)
+    int stagger;              // x6: the first round of blocks starts spread over this many shader cycles (0 = off)
+    int stagger_blocks;       // ... the blocks of that round (one per CU)
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
 #endif
 };
+
+// per-thread override of the split-fp16 fast loader form (rvc_conv1d_set_f16_fast; -1 = RVC_X6_F16FAST, default on)
+static thread_local int g_f16_fast = -1;
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
 
@@ -441,7 +446,8 @@ constexpr bool kAblations = RVC_CONV_ABLATIONS != 0;
 // one lane, vector stores.  Layout per block (X6_STAMP_W words): 0 compute start, 1 memrealtime at start, 2 HW_ID,
 // 3 compute: prefetch issued, 4 compute: F16 scale barrier passed, 5 compute: chunk 0 barrier passed,
 // 6 compute: k-loop done, 7 compute: epilogue done, 8 loader start, 9 loader: F16 |max| published,
-// 10 loader: chunk 0 staged, 11 loader: loop done, 12 number of chunks; then per chunk c (< X6_STAMP_NC):
+// 10 loader: chunk 0 staged, 11 loader: loop done, 12 number of chunks, 14 compute: epilogue stores issued; then per
+// chunk c (< X6_STAMP_NC):
 // 16 + 4c: compute arrives at chunk c's barrier, +1 released, +2 loader arrives, +3 released.
 #ifndef RVC_CONV_STAMPS
 #define RVC_CONV_STAMPS 0
@@ -575,13 +581,16 @@ __device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const floa
     if (p.amax_out && !part) amax_publish(p.amax_out, amx);
 }
 
-template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false>
+// LF (split-fp16 on 8 compute waves, with the producer's |max|: amax_in): the loaders take ONLY the fast form (1: leaky
+// ReLU pre-activation, 2: none) -- a kernel of its own, so the general form's registers are not allocated beside it
+template <int FM, int FN, int WM, int WN, int X6_NI, int NP, bool F16, bool SA = false, int LF = 0>
 __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN, NP>())) void conv_x6_kernel(ConvParams p) {
     static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 compute waves");
     constexpr int NCW = WM * WN;  // compute waves; 4 loader waves follow them
     static_assert(NP == 6 || NP == 3 || NP == 1, "6, 3 or 1 passes");
     static_assert(!F16 || NP == 3, "split-fp16: 3 passes");
     static_assert(!SA || (NP == 6 && !F16), "split accumulators: 6-pass split-bf16");
+    static_assert(LF == 0 || (F16 && WM * WN == 8), "fast-only loaders: split-fp16 on 8 compute waves");
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int BM = 16 * FM * WM;
     constexpr int BN = 16 * FN * WN;
@@ -628,6 +637,19 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         return ch_beg + (c >= nck ? c - nck : c);
     };
 
+    // Staggered start (p.stagger): the blocks of a launch all do the same work, so the first round's blocks -- and the
+    // rounds that follow them on each CU -- reach their epilogues together, and the epilogue (residual loads, stores)
+    // then runs HBM-bound chip-wide while HBM sits idle through the MFMA loops (stamps, rb128_k11: 34k cycles of a 147k
+    // block with the residual, 16k without).  Delaying the first round's block i by a permutation of [0, stagger)
+    // spreads every later round's epilogues over the block period.
+    if (p.stagger) {
+        const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        if (lin < p.stagger_blocks) {
+            const unsigned long long t0 = X6_NOW();
+            const unsigned long long d = ((unsigned long long)((lin * 97) & 255) * (unsigned)p.stagger) >> 8;
+            while (X6_NOW() - t0 < d) __builtin_amdgcn_s_sleep(2);
+        }
+    }
     if (wave == 0) {
         X6_STAMP(0, X6_NOW());
         X6_STAMP(1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -854,7 +876,11 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         // (X6_F16FAST=1 builds the split-fp16 fast form too: its loader registers pushed the 128 x 256 kernel's spills
         // from 34 to 93 VGPRs and its prologue, under the amax read, from 19k to 61k cycles -- end to end neutral,
         // r5f; off)
-        if constexpr (!F16 || (NCW == 8 && X6_F16FAST)) {
+        if constexpr (LF == 1) {
+            loader(std::true_type{}, std::true_type{});
+        } else if constexpr (LF == 2) {
+            loader(std::true_type{}, std::false_type{});
+        } else if constexpr (!F16 || (NCW == 8 && X6_F16FAST)) {
             if ((!F16 || (p.amax_in && p.f16_fast)) && (Cig & 31) == 0 && p.in_scale == 1.f &&
                 (p.in_act == RVC_ACT_NONE || p.in_act == RVC_ACT_LRELU)) {
                 if (p.in_act == RVC_ACT_LRELU) loader(std::true_type{}, std::true_type{});
@@ -1095,7 +1121,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     }
 #if RVC_CONV_STAMPS
     if (wave == 0) {
-        __builtin_amdgcn_s_waitcnt(0);  // the epilogue's stores issued and retired
+        X6_STAMP(14, X6_NOW());         // the epilogue's stores issued
+        __builtin_amdgcn_s_waitcnt(0);  // ... and retired
         X6_STAMP(7, X6_NOW());
     }
 #endif
@@ -1129,12 +1156,19 @@ hipError_t launch(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int FM, int FN, int WM, int WN, int NP, bool F16 = false, bool SA = false>
+template <int FM, int FN, int WM, int WN, int NP, bool F16 = false, bool SA = false, int LF = 0>
 void launch_x6_np(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
     // loader items per thread sized to the staged span (unused items would still issue loads)
     const dim3 blk(64 * (WM * WN + 4));
-    if (4 * p.span <= 256 * 3) hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA>), grid, blk, lds, s, p);
-    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA>), grid, blk, lds, s, p);
+    if (4 * p.span <= 256 * 3)
+        hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 3, NP, F16, SA, LF>), grid, blk, lds, s, p);
+    else hipLaunchKernelGGL((conv_x6_kernel<FM, FN, WM, WN, 6, NP, F16, SA, LF>), grid, blk, lds, s, p);
+}
+
+// the fast-only split-fp16 loaders apply (conv_x6_kernel's LF): 1 = leaky ReLU input, 2 = none, 0 = no
+int x6_f16_fast_form(const ConvParams& p) {
+    if (!p.amax_in || !p.f16_fast || (p.Ci & 31) != 0 || p.in_scale != 1.f) return 0;
+    return p.in_act == RVC_ACT_LRELU ? 1 : (p.in_act == RVC_ACT_NONE ? 2 : 0);
 }
 
 // The tiles compiled with split accumulators (RVC_ARITH_FP32_SA): <= 64 rows on 4 / 8 waves and 128 x 128 on 8
@@ -1146,7 +1180,14 @@ constexpr bool x6_sa_tile(int FM, int FN, int WM, int WN) {
 
 template <int FM, int FN, int WM, int WN>
 hipError_t launch_x6(const ConvParams& p, dim3 grid, size_t lds, hipStream_t s) {
-    if (p.wx_passes == RVC_ARITH_F16X3) launch_x6_np<FM, FN, WM, WN, 3, true>(p, grid, lds, s);
+    if (p.wx_passes == RVC_ARITH_F16X3) {
+        const int lf = WM * WN == 8 ? x6_f16_fast_form(p) : 0;
+        if constexpr (WM * WN == 8) {
+            if (lf == 1) launch_x6_np<FM, FN, WM, WN, 3, true, false, 1>(p, grid, lds, s);
+            else if (lf == 2) launch_x6_np<FM, FN, WM, WN, 3, true, false, 2>(p, grid, lds, s);
+        }
+        if (lf == 0) launch_x6_np<FM, FN, WM, WN, 3, true>(p, grid, lds, s);
+    }
     else if (p.wx_passes == 1) launch_x6_np<FM, FN, WM, WN, 1>(p, grid, lds, s);
     else if (p.wx_passes == 3) launch_x6_np<FM, FN, WM, WN, 3>(p, grid, lds, s);
     else if (p.wx_passes == RVC_ARITH_FP32_SA) {
@@ -1185,7 +1226,9 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.amax_in = a->amax_in;
     p.amax_out = a->amax_out;
     static const int f16fast = getenv("RVC_X6_F16FAST") ? atoi(getenv("RVC_X6_F16FAST")) : 1;
-    p.f16_fast = f16fast;
+    p.f16_fast = g_f16_fast >= 0 ? g_f16_fast : f16fast;
+    p.stagger = 0;
+    p.stagger_blocks = 0;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -1349,6 +1392,13 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         p.tile_epi = !(tepi && plain) ? 0 : tile_bytes <= lds ? 1 : (cfg.WM % 2 == 0 && tile_bytes / 2 <= lds) ? 2 : 0;
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
+        // staggered start (RVC_X6_STAGGER shader cycles) when the launch runs more than one round of blocks per CU
+        static const int stagger = getenv("RVC_X6_STAGGER") ? atoi(getenv("RVC_X6_STAGGER")) : 0;
+        const int64_t nblk = (int64_t)grid.x * grid.y * grid.z;
+        if (stagger > 0 && nblk >= 2 * (int64_t)num_cus()) {
+            p.stagger = stagger;
+            p.stagger_blocks = num_cus();
+        }
         return RVC_OK;
     }
 
@@ -1547,6 +1597,11 @@ extern "C" int rvc_conv1d_set_splitk_target(int target) {
 static thread_local hipEvent_t g_probe_event = nullptr;
 
 extern "C" void rvc_conv1d_set_probe_event(void* hip_event) { g_probe_event = (hipEvent_t)hip_event; }
+
+extern "C" int rvc_conv1d_set_f16_fast(int on) {
+    g_f16_fast = on < 0 ? -1 : (on ? 1 : 0);
+    return RVC_OK;
+}
 
 extern "C" int rvc_conv1d_set_tile_epi(int on) {
     g_tile_epi = on < 0 ? -1 : (on ? 1 : 0);

@@ -20,6 +20,9 @@ import torch  # noqa: E402
 W = 256  # X6_STAMP_W
 SHAPES = [  # name, Ci, Co, K, dil, L, pre-activation (ResBlock convs: lrelu + residual; GEMMs: none)
     ("rb128_k11", 128, 128, 11, 5, 383760, True),
+    ("rb128_k11_nores", 128, 128, 11, 5, 383760, None),
+    ("rb128_k11_256blk", 128, 128, 11, 5, 256 * 256, True),  # one block per CU: the epilogue against HBM contention
+    ("rb128_k11_32blk", 128, 128, 11, 5, 32 * 256, True),
     ("rb128_k7", 128, 128, 7, 3, 383760, True),
     ("rb128_k3", 128, 128, 3, 1, 383760, True),
     ("rb256_k3", 256, 256, 3, 1, 95940, True),
@@ -54,6 +57,8 @@ def analyse(st, nblk, K, kname):
     res["loader_chunk0_med"] = float(np.median(d(9 if np.any(st[:, 9]) else 8, 10)))
     res["loop_med"] = float(np.median(d(5, 6)))
     res["epilogue_med"] = float(np.median(d(6, 7)))
+    if np.any(st[:, 14]):
+        res["epilogue_issue_med"] = float(np.median(d(6, 14)))
     nc = min(int(np.median(nch)), 60)
     comp, cwait, lbusy, lwait = [], [], [], []
     for c in range(nc):
@@ -121,7 +126,7 @@ def main():
         w = torch.randn(Co, Ci, K, generator=g) / (Ci * K) ** 0.5
         conv = ops.Conv(w, torch.randn(Co, generator=g), device="cuda")
         x = torch.randn(Ci, L, generator=g).cuda()
-        res = torch.randn(Co, L, generator=g).cuda() if rb else None
+        res = torch.randn(Co, L, generator=g).cuda() if rb else None  # rb None: the ResBlock conv minus its residual
         y = torch.empty(Co, L, device="cuda")
         p = d * (K - 1) // 2
         kw = dict(pad=p, dil=d, out=y, res=res)
@@ -129,7 +134,7 @@ def main():
             cell = ops.AmaxSlots(1, "cuda")
             cell.words[0] = int(np.float32(x.abs().max().item()).view(np.int32))
             kw["amax_in"] = cell[0]
-        if rb:
+        if rb is not False:
             kw.update(in_act=ops.ACT_LRELU, in_slope=0.1)
         for _ in range(3):
             conv(x, **kw)
@@ -156,7 +161,7 @@ def main():
         print(f"   block {r['block_cycles_med']:.0f} cyc = prologue {r['prologue_compute_med']:.0f}"
               + (f" (f16 scale wait {r['f16_scale_wait_med']:.0f}, loader pre-pass {r['loader_prepass_med']:.0f})"
                  if 'f16_scale_wait_med' in r else "")
-              + f" + loop {r['loop_med']:.0f} + epilogue {r['epilogue_med']:.0f};  loader chunk0 {r['loader_chunk0_med']:.0f}")
+              + f" + loop {r['loop_med']:.0f} + epilogue {r['epilogue_med']:.0f} (issued after {r.get('epilogue_issue_med', 0):.0f});  loader chunk0 {r['loader_chunk0_med']:.0f}")
         print(f"   CU period {r.get('cu_block_period_us_med', 0):.1f} us; next block starts "
               f"{r.get('next_block_start_after_end_cyc_med')} cyc after wave 0's epilogue stamp")
         print(f"   per chunk: compute {pc['compute_med']:.0f} + barrier wait {pc['barrier_wait_med']:.0f} (MFMA-bound "

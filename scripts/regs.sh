@@ -13,6 +13,6 @@ for line in sys.stdin:
     m = re.search(r"remark:\s+(VGPRs|AGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]|ScratchSize \[bytes/lane\]): (\d+)", line)
     if m and cur is not None: cur[m.group(1).split()[0] + ("S" if "Spill" in m.group(1) else "")] = m.group(2)
 for r in rows:
-    print(r["name"][:64].ljust(64), "V", r.get("VGPRs"), "A", r.get("AGPRs"), "spill", r.get("VGPRsS"),
+    print(r["name"][:80].ljust(80), "V", r.get("VGPRs"), "A", r.get("AGPRs"), "spill", r.get("VGPRsS"),
           "scratch", r.get("ScratchSize"), "occ", r.get("Occupancy"))'
 rm -f /tmp/regs_$$.o

@@ -433,6 +433,36 @@ def test_x6_tile_epilogue_bit_identical(ops, prec, Ci, Co, K, d, L, B, epi):
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
 
 
+@pytest.mark.parametrize("Ci,Co,K,d,L,act", [(128, 128, 11, 5, 40000, "lrelu"), (128, 128, 3, 1, 33333, "none"),
+                                             (256, 256, 7, 3, 9000, "lrelu"), (192, 160, 3, 1, 5000, "lrelu")])
+def test_x6_f16_fast_loader_bit_identical(ops, Ci, Co, K, d, L, act):
+    """The split-fp16 loaders' fast form (its own kernel, taken with the producer's |max| on the 8-compute-wave tiles)
+    stages the same fp16 pieces as the general form: same bits (rvc_conv1d_set_f16_fast toggles it)."""
+    g = gen(12)
+    x = torch.randn(Ci, L, generator=g).to(DEV)
+    w = torch.randn(Co, Ci, K, generator=g) / math.sqrt(Ci * K)
+    c = ops.Conv(w, torch.randn(Co, generator=g))
+    res = torch.randn(Co, L, generator=g).to(DEV)
+    cell = ops.AmaxSlots(1, DEV)
+    cell.words[0] = int(np.float32(x.abs().max().item()).view(np.int32))
+    lib = ops._lib.load()
+    outs = []
+    for on in (0, 1):
+        lib.rvc_conv1d_set_f16_fast(on)
+        try:
+            kw = dict(pad=d * (K - 1) // 2, dil=d, res=res, amax_in=cell[0])
+            if act == "lrelu":
+                kw.update(in_act=ops.ACT_LRELU, in_slope=0.1)
+            with ops.precision("f16x3"):
+                y = c(x, **kw)
+            assert ops.LAST_CONV_ENGINE == 1
+            torch.cuda.synchronize()
+            outs.append(y.cpu())
+        finally:
+            lib.rvc_conv1d_set_f16_fast(-1)
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+
+
 @pytest.mark.parametrize("B,N", [(1, 16000 * 3 + 123), (2, 8000), (1, 400)])
 def test_fe0_gn_gelu(ops, B, N):
     """ContentVec's first layer fused (rvc_fe0_gn_gelu: conv 1 -> 512, k10 s5, GroupNorm(512, 512), GELU) against
