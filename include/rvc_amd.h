@@ -359,6 +359,10 @@ int rvc_img_to_seq64(const double* img, double* x, int64_t B, int64_t C, int64_t
 /* bigru64_batched: rvc_bigru_batched in f64 (gi [2][768][T], whh [2][768][256], bhh [2][768], y [512][T] per
  * sequence); gran_ws: RVC_BIGRU64_GRAN_BYTES * min(B, 16) scratch (zeroed by the call); err as rvc_bigru. */
 #define RVC_BIGRU64_GRAN_BYTES 16384
+/* The f64 BiGRU's recurrence arithmetic, per thread: 1 = W_hh h and the gates in f32 (the default: its decision noise
+ * on the headline clip is 1.8e-9, three orders below the smallest exact margin; gi and y stay f64), 0 = all f64,
+ * -1 = back to RVC_BIGRU64_F32 (default 1). */
+int rvc_bigru64_set_f32(int on);
 int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double* whh, const double* bhh, double* y,
                         int64_t y_bs, void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream);
 /* Optional steps of VC.get_f0 between the raw f0 and the mel quantiser (convert.py:311-318), in

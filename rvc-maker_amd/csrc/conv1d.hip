@@ -824,14 +824,15 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 return m;
             };
             float am = 0.f;
-            if (FASTL || p.amax_in) {
+            const bool cell = FASTL || p.amax_in;  // block-uniform
+            if (cell) {
                 // the producer published |max| of the whole input tensor (amax side channel): no pre-pass (the fast
-                // form is only dispatched with amax_in, so its body never instantiates the pre-pass).  The cell is
-                // read before the chunk loads are issued: behind them (vmcnt counts in order) its wait would include
-                // two chunks' HBM latency
-                am = amax_read(p.amax_in) * fabsf(p.in_scale);
+                // form is only dispatched with amax_in, so its body never instantiates the pre-pass).  The chunk loads
+                // go first: the cell is read through the scalar cache (its own counter), so its latency -- a line
+                // the producer's atomics left at the memory side -- overlaps theirs
                 xload(pchunk(0), xr[0]);
                 xload(pchunk(1), xr[1]);
+                am = amax_read(p.amax_in) * fabsf(p.in_scale);
             } else if constexpr (!FASTL) {
                 for (int i = 2; i < nck; i += 2) {
                     xload(pchunk(i), xr[0]);
@@ -844,8 +845,14 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             }
             if (lane == 0) tmax[wave - NCW] = am;
             if (lw0) X6_STAMP(9, X6_NOW());
-            __syncthreads();  // tile max published
-            sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+            if (cell) {
+                // every loader wave read the same cell: the same scale, no agreement needed -- and the compute waves
+                // need it only in the epilogue, so they take it from tmax after the chunk-0 barrier (one barrier less)
+                sc = ldexpf(1.f, f16_exp(am));
+            } else {
+                __syncthreads();  // tile max published
+                sc = ldexpf(1.f, f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+            }
             xstore(pchunk(0), xr[0], xs);
         } else {
             xload(pchunk(0), xr[0]);
@@ -1012,11 +1019,16 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     float tile_rs = 1.f;
     if (wave == 0) X6_STAMP(3, X6_NOW());
     if constexpr (F16) {
-        __syncthreads();  // tile max published by the loaders
-        tile_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+        if (!(LF || p.amax_in)) {  // the loaders' agreed pre-pass maximum (the cell case: after the chunk-0 barrier)
+            __syncthreads();  // tile max published by the loaders
+            tile_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+        }
         if (wave == 0) X6_STAMP(4, X6_NOW());
     }
     __syncthreads();  // chunk 0 staged
+    if constexpr (F16) {
+        if (LF || p.amax_in) tile_rs = ldexpf(1.f, -f16_exp(fmaxf(fmaxf(tmax[0], tmax[1]), fmaxf(tmax[2], tmax[3]))));
+    }
     if (wave == 0) X6_STAMP(5, X6_NOW());
     const int nsteps = s_end - s_beg;
     int ci = 0, ct = 0;  // the computing k-step's logical (chunk index, tap index)
@@ -1394,8 +1406,9 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         // staggered start (RVC_X6_STAGGER shader cycles) when the launch runs more than one round of blocks per CU
         static const int stagger = getenv("RVC_X6_STAGGER") ? atoi(getenv("RVC_X6_STAGGER")) : 0;
+        static const int stagger_rounds = getenv("RVC_X6_STAGGER_ROUNDS") ? atoi(getenv("RVC_X6_STAGGER_ROUNDS")) : 2;
         const int64_t nblk = (int64_t)grid.x * grid.y * grid.z;
-        if (stagger > 0 && nblk >= 2 * (int64_t)num_cus()) {
+        if (stagger > 0 && nblk >= stagger_rounds * (int64_t)num_cus()) {
             p.stagger = stagger;
             p.stagger_blocks = num_cus();
         }

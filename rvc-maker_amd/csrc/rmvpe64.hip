@@ -1142,6 +1142,127 @@ __global__ __launch_bounds__(4096 / NWG) void bigru64_kernel(const double* gi, c
     }
 }
 
+// The recurrence in f32 behind the f64 interface (the default; RVC_BIGRU64_F32=0: bigru64_kernel, all f64): gi, W_hh, b_hh rounded to f32 on load, h in f32,
+// y widened to f64.  The round-5 stage study (scripts/rmvpe_stage_prec.py, profiles/r5_rmvpe_stage_prec.json) put the
+// f32 recurrence's decision noise at 1.8e-9 on the headline clip -- three orders below its smallest exact margin --
+// where the input projection W_ih (2.4e-5) and every U-Net level (>= 4e-8) stay f64.  NWG workgroups per direction
+// (4: 1024 threads, 64 units each, W_hh rows as 48 f32 registers per thread); with `spread`, the grid is 8 NWG blocks
+// of which the NWG blocks b = d + 8 k (k < NWG) serve direction d and the rest leave at once: blocks b and b + 8 are
+// dealt to the same XCD (MI355X_MICROARCH.md, dispatch; observed, speed only -- the hand-off is agent-scope either
+// way).  8-byte {tag, f32} granules as rmvpe.hip's f32 kernel, double-buffered by step parity, bounded spins.
+template <int NWG>
+__global__ __launch_bounds__(4096 / NWG) void bigru_mx_kernel(const double* gi, const double* whh, const double* bhh,
+                                                              double* y, unsigned long long* gran, int* err, int64_t T,
+                                                              unsigned spin_limit, int64_t gi_bs, int64_t y_bs,
+                                                              int spread) {
+    constexpr int UPW = G_H / NWG;
+    int d, j;
+    if (spread) {
+        const int slot = blockIdx.x & 7;
+        if (slot >= 2) return;
+        d = slot;
+        j = blockIdx.x >> 3;
+    } else {
+        d = blockIdx.x / NWG;
+        j = blockIdx.x % NWG;
+    }
+    gi += (int64_t)blockIdx.y * gi_bs;
+    y += (int64_t)blockIdx.y * y_bs;
+    gran += (int64_t)blockIdx.y * 2 * 2 * G_H;
+    const int tid = threadIdx.x;
+    const int ul = tid >> 4, s = tid & 15;
+    const int u = j * UPW + ul;
+    __shared__ float hs[2][G_H];
+    __shared__ int abort_flag;
+    if (tid == 0) abort_flag = 0;
+    const double* W = whh + (int64_t)d * 3 * G_H * G_H;
+    float wr[16], wz[16], wn[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        wr[i] = (float)W[(int64_t)u * G_H + 16 * s + i];
+        wz[i] = (float)W[(int64_t)(G_H + u) * G_H + 16 * s + i];
+        wn[i] = (float)W[(int64_t)(2 * G_H + u) * G_H + 16 * s + i];
+    }
+    // lane 0 of the unit's group: r's input projection and bias (and n's); lane 1: z's -- r and z in one evaluation
+    const int gsel = s == 1 ? 1 : 0;
+    const float bhg = (float)bhh[d * 3 * G_H + gsel * G_H + u], bhn = (float)bhh[d * 3 * G_H + 2 * G_H + u];
+    const double* G = gi + (int64_t)d * 3 * G_H * T;
+    unsigned long long* GR = gran + (int64_t)d * 2 * G_H;
+    float hprev = 0.f;
+    float gxg = 0.f, gxn = 0.f;
+    if (s < 2) {
+        const int64_t tau0 = d ? T - 1 : 0;
+        gxg = (float)G[(int64_t)(gsel * G_H + u) * T + tau0];
+        gxn = (float)G[(int64_t)(2 * G_H + u) * T + tau0];
+    }
+    if (tid < G_H) hs[0][tid] = 0.f;
+    __syncthreads();
+    for (int64_t t = 0; t < T; ++t) {
+        const int64_t tau = d ? T - 1 - t : t;
+        const int cur = (int)(t & 1);
+        if (t > 0) {
+            if (tid < G_H) {  // (wave-uniform) one granule per thread of the first 4 waves
+                unsigned long long* g = GR + ((t - 1) & 1) * G_H + tid;
+                unsigned long long v;
+                unsigned spins = 0;
+                for (;;) {
+                    v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)(v >> 32) == (uint32_t)t) break;
+                    if (++spins > spin_limit) {
+                        atomicExch(err, 1);
+                        abort_flag = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                hs[cur][tid] = __uint_as_float((uint32_t)v);
+            }
+            __syncthreads();
+            if (abort_flag) break;
+        }
+        float nxg = 0.f, nxn = 0.f;
+        if (s < 2 && t + 1 < T) {
+            const int64_t tn = d ? T - 2 - t : t + 1;
+            nxg = (float)G[(int64_t)(gsel * G_H + u) * T + tn];
+            nxn = (float)G[(int64_t)(2 * G_H + u) * T + tn];
+        }
+        // two interleaved FMA chains per gate (half the dependent latency of one 16-deep chain)
+        float pr = 0.f, pz = 0.f, pn = 0.f, qr = 0.f, qz = 0.f, qn = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            const float h0 = hs[cur][16 * s + i], h1 = hs[cur][16 * s + i + 1];
+            pr = fmaf(wr[i], h0, pr);
+            pz = fmaf(wz[i], h0, pz);
+            pn = fmaf(wn[i], h0, pn);
+            qr = fmaf(wr[i + 1], h1, qr);
+            qz = fmaf(wz[i + 1], h1, qz);
+            qn = fmaf(wn[i + 1], h1, qn);
+        }
+        pr += qr;
+        pz += qz;
+        pn += qn;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            pr += __shfl_xor(pr, o, 64);
+            pz += __shfl_xor(pz, o, 64);
+            pn += __shfl_xor(pn, o, 64);
+        }
+        // hardware exp2 / reciprocal (~1 ulp each): far inside the stage's noise budget
+        const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-(gxg + ((gsel ? pz : pr) + bhg))));
+        const float zz = __shfl_down(sg, 1, 64);  // lane 0 <- lane 1's z
+        if (s == 0) {
+            const float n = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * (gxn + sg * (pn + bhn))));
+            const float h = (hprev - n) * zz + n;
+            hprev = h;
+            const unsigned long long gv = ((unsigned long long)(uint32_t)(t + 1) << 32) | __float_as_uint(h);
+            __hip_atomic_store(GR + (t & 1) * G_H + u, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            y[(int64_t)(d * G_H + u) * T + tau] = (double)h;
+        }
+        gxg = nxg;
+        gxn = nxn;
+    }
+}
+
 constexpr int G_B_MAX = 16;  // sequences per launch (32 co-resident workgroups each)
 
 }  // namespace
@@ -1255,6 +1376,14 @@ extern "C" int rvc_img_to_seq64(const double* img, double* x, int64_t B, int64_t
 
 extern "C" unsigned rvc_bigru_set_spin_limit(unsigned limit);
 
+// per-thread override of the recurrence's arithmetic (rvc_bigru64_set_f32; -1 = RVC_BIGRU64_F32, default 1)
+static thread_local int g_bigru64_f32 = -1;
+
+extern "C" int rvc_bigru64_set_f32(int on) {
+    g_bigru64_f32 = on < 0 ? -1 : (on ? 1 : 0);
+    return RVC_OK;
+}
+
 extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double* whh, const double* bhh, double* y,
                                    int64_t y_bs, void* gran_ws, int* err, int64_t B, int64_t T, rvc_stream_t stream) {
     RVC_CHECK_ARG(gi && whh && bhh && y && gran_ws && err && T > 0 && T < (1ll << 31) && B > 0, "bigru64: bad args");
@@ -1267,9 +1396,37 @@ extern "C" int rvc_bigru64_batched(const double* gi, int64_t gi_bs, const double
     for (int64_t b0 = 0; b0 < B; b0 += G_B_MAX) {
         const int64_t nb = B - b0 < G_B_MAX ? B - b0 : G_B_MAX;
         RVC_HIP(hipMemsetAsync(gran_ws, 0, (size_t)nb * RVC_BIGRU64_GRAN_BYTES, s));
-        static const int nwg = getenv("RVC_BIGRU64_WG") && atoi(getenv("RVC_BIGRU64_WG")) == 8 ? 8 : 16;
+        static const int nwg_env = getenv("RVC_BIGRU64_WG") ? atoi(getenv("RVC_BIGRU64_WG")) : 16;
+        static const int nwg = nwg_env == 8 || nwg_env == 4 ? nwg_env : 16;
         static const int prio = getenv("RVC_BIGRU64_PRIO") ? atoi(getenv("RVC_BIGRU64_PRIO")) : 0;
-        if (nwg == 8)
+        // the f32 recurrence (bigru_mx_kernel): RVC_BIGRU64_F32=1, workgroups per direction RVC_BIGRU64_MXWG
+        // (4 / 8 / 16), XCD-spread placement RVC_BIGRU64_SPREAD (NWG 4 only)
+        static const int f32_env = getenv("RVC_BIGRU64_F32") ? atoi(getenv("RVC_BIGRU64_F32")) : 1;
+        const int f32 = g_bigru64_f32 >= 0 ? g_bigru64_f32 : f32_env;
+        static const int mxwg_env = getenv("RVC_BIGRU64_MXWG") ? atoi(getenv("RVC_BIGRU64_MXWG")) : 16;
+        static const int mxwg = mxwg_env == 8 || mxwg_env == 4 ? mxwg_env : 16;
+        static const int spread = getenv("RVC_BIGRU64_SPREAD") ? atoi(getenv("RVC_BIGRU64_SPREAD")) : 0;
+        if (f32) {
+            unsigned long long* gw = (unsigned long long*)gran_ws;
+            if (mxwg == 4 && spread)
+                hipLaunchKernelGGL(bigru_mx_kernel<4>, dim3(32, (unsigned)nb), dim3(1024), 0, s, gi + b0 * gi_bs, whh,
+                                   bhh, y + b0 * y_bs, gw, err, T, spin, gi_bs, y_bs, 1);
+            else if (mxwg == 4)
+                hipLaunchKernelGGL(bigru_mx_kernel<4>, dim3(8, (unsigned)nb), dim3(1024), 0, s, gi + b0 * gi_bs, whh,
+                                   bhh, y + b0 * y_bs, gw, err, T, spin, gi_bs, y_bs, 0);
+            else if (mxwg == 8)
+                hipLaunchKernelGGL(bigru_mx_kernel<8>, dim3(16, (unsigned)nb), dim3(512), 0, s, gi + b0 * gi_bs, whh,
+                                   bhh, y + b0 * y_bs, gw, err, T, spin, gi_bs, y_bs, 0);
+            else
+                hipLaunchKernelGGL(bigru_mx_kernel<16>, dim3(32, (unsigned)nb), dim3(256), 0, s, gi + b0 * gi_bs, whh,
+                                   bhh, y + b0 * y_bs, gw, err, T, spin, gi_bs, y_bs, 0);
+            RVC_HIP(hipGetLastError());
+            continue;
+        }
+        if (nwg == 4)
+            hipLaunchKernelGGL(bigru64_kernel<4>, dim3(2 * 4, (unsigned)nb), dim3(1024), 0, s, gi + b0 * gi_bs, whh, bhh,
+                               y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs, prio);
+        else if (nwg == 8)
             hipLaunchKernelGGL(bigru64_kernel<8>, dim3(2 * 8, (unsigned)nb), dim3(512), 0, s, gi + b0 * gi_bs, whh, bhh,
                                y + b0 * y_bs, (unsigned long long*)gran_ws, err, T, spin, gi_bs, y_bs, prio);
         else

@@ -130,6 +130,7 @@ SIGNATURES = {
     "rvc_conv1d_set_stamps": [c_void_p, c_int64],
     "rvc_conv1d_set_tile_epi": [c_int],
     "rvc_conv1d_set_f16_fast": [c_int],
+    "rvc_bigru64_set_f32": [c_int],
     "rvc_conv1d_set_splitk_target": [c_int],
     "rvc_stream_create_cu_mask": [c_void_p, c_int, POINTER(c_void_p)],
     "rvc_stream_destroy": [c_void_p],

@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--T", type=int, default=3232)
     ap.add_argument("--B", type=int, default=1)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--save", default="", help="write y (f64, .npy) for an offline comparison")
     args = ap.parse_args()
     from rvc_amd import ops
     dev, B, T = "cuda", args.B, args.T
@@ -36,6 +37,9 @@ def main():
     ms = e0.elapsed_time(e1) / args.reps
     print(f"bigru64 B={B} T={T}: {ms:.3f} ms ({ms * 1e3 / T:.3f} us/step) "
           f"err={int(err.item())} checksum={float(y.double().sum()):.12e}")
+    if args.save:
+        import numpy as np
+        np.save(args.save, y.cpu().numpy())
 
 
 if __name__ == "__main__":

@@ -23,6 +23,8 @@ SHAPES = [  # name, Ci, Co, K, dil, L, pre-activation (ResBlock convs: lrelu + r
     ("rb128_k11_nores", 128, 128, 11, 5, 383760, None),
     ("rb128_k11_256blk", 128, 128, 11, 5, 256 * 256, True),  # one block per CU: the epilogue against HBM contention
     ("rb128_k11_32blk", 128, 128, 11, 5, 32 * 256, True),
+    ("rb128_k11_128blk", 128, 128, 11, 5, 128 * 256, True),
+    ("rb128_k11_192blk", 128, 128, 11, 5, 192 * 256, True),
     ("rb128_k7", 128, 128, 7, 3, 383760, True),
     ("rb128_k3", 128, 128, 3, 1, 383760, True),
     ("rb256_k3", 256, 256, 3, 1, 95940, True),
