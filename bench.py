@@ -52,8 +52,9 @@ def pass_peak(passes):
     each product takes (6 / 8 split-bf16, 3 split-fp16 or bf16x3, 1 bf16)."""
     n = {16: 3, 7: 6}.get(passes, passes)  # RVC_ARITH_F16X3: 3 fp16 passes; RVC_ARITH_FP32_SA: 6 passes
     return PEAK_MFMA16_TFLOPS / n
-DTYPES = {"fp32": "f32-equivalent (split-bf16 6-pass MFMA; split-fp16 3-pass MFMA for k >= 7 convs and ResBlock "
-                  "pairs; f32 accumulate)",
+DTYPES = {"fp32": "f32-equivalent (split-fp16 3-pass MFMA for the generator's convs -- scale from the producer's "
+                  "published |max| -- and ResBlock pairs, split-bf16 6-pass MFMA elsewhere; f32 accumulate; RMVPE f64 "
+                  "with its GRU recurrence f32)",
           "fp32x6": "f32 (split-bf16 x6 MFMA, f32 accumulate)",
           "f16x3": "f32-equivalent (split-fp16 3-pass MFMA convs, power-of-2 scaled 22-bit operands, f32 accumulate)",
           "bf16x3": "bf16x3 (3-pass split-bf16 MFMA convs, f32 accumulate; f32 elsewhere)",

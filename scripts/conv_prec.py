@@ -4,6 +4,7 @@ reference executes).  RMVPE-like shapes (K = 3 taps over 16..512 channels, K = 1
 
     python scripts/conv_prec.py
 """
+import argparse
 import os
 import sys
 
