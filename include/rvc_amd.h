@@ -202,6 +202,8 @@ typedef struct rvc_attn_args {
  * workspace of rvc_attention_workspace_bytes(a) bytes (0 when not split). */
 int64_t rvc_attention_workspace_bytes(const rvc_attn_args* a);
 int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
+/* the same, also folding max |o| into a |max| cell (amax_out as rvc_layernorm_cf_amax; not with the relative band) */
+int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ elementwise
  * Memory-bound pieces of Synthesizer.infer (synthesizers.py:446-465).  All
@@ -213,6 +215,10 @@ int rvc_textenc_embed(const float* lin, const float* emb, const int64_t* pitch, 
 /* LayerNorm over channels of (x + res)                  synthesizers.py:170-181, fairseq.py:700 */
 int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out, int64_t B,
                      int64_t C, int64_t T, float eps, rvc_stream_t stream);
+/* the same, also folding max |out| into a |max| cell (amax_out: RVC_AMAX_SHARDS zeroed u32 words, the amax_in of the
+ * GEMM that reads out; ContentVec's LayerNorms, 256 < C <= 768) */
+int rvc_layernorm_cf_amax(const float* x, const float* res, const float* gamma, const float* beta, float* out,
+                          int64_t B, int64_t C, int64_t T, float eps, unsigned* amax_out, rvc_stream_t stream);
 /* GroupNorm(C, C) over time + affine (+ exact GELU)      fairseq.py:1149-1155,1183-1185 */
 int rvc_chnorm_gelu(const float* x, const float* gamma, const float* beta, float* out, int64_t B, int64_t C, int64_t L,
                     float eps, int gelu, rvc_stream_t stream);

@@ -32,6 +32,7 @@ struct AttnParams {
     int64_t q_bs, k_bs, v_bs, o_bs;  // batch strides
     int H, W, S, kps;                // heads, rel window, KV splits, keys per split (multiple of 64)
     float scale;
+    unsigned* amax_out;  // |max| cell of o (rvc_attention_amax) or null
 };
 
 // Grid (T/64, H, B*S).  The key range of a block is split blockIdx.z % S; with S > 1 the block
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
         __syncthreads();
     }
 
+    float amx = 0.f;  // amax_out: largest |o| this lane stores (the final output only, S == 1)
     if (qa < T) {
         const float inv = 1.f / l_run;
         float* O;
@@ -180,12 +182,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
         for (int f = 0; f < NF; ++f)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) O[(int64_t)(16 * f + lg * 4 + r) * ldo + qa] = acc_o[f][r] * inv;
+            for (int r = 0; r < 4; ++r) {
+                const float o = acc_o[f][r] * inv;
+                O[(int64_t)(16 * f + lg * 4 + r) * ldo + qa] = o;
+                amx = fmaxf(amx, fabsf(o));
+            }
         if (ML && lg == 0) {
             ML[qa] = m_run;
             ML[T + qa] = l_run;
         }
     }
+    if (p.amax_out && p.S == 1) amax_publish(p.amax_out, amx);  // every lane (the wave's shuffles)
 }
 
 // Merge S split-KV partials: o = sum_s o_s * l_s e^(m_s - m) / sum_s l_s e^(m_s - m).  Grid (T/64, H, B),
@@ -195,9 +202,10 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnParams p) {
     constexpr int NC = D / 4;
     const int h = blockIdx.y, b = blockIdx.z;
     const int64_t T = p.T;
-    const int64_t q = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t qv = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const int cg = threadIdx.x >> 6;
-    if (q >= T) return;
+    const bool ok = qv < T;  // (no early return: the amax shuffles need the whole wave)
+    const int64_t q = ok ? qv : T - 1;
     const int S = p.S;
     const float* wml = p.ws + (int64_t)gridDim.z * S * p.H * D * T;
     float m = -INFINITY;
@@ -215,8 +223,16 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnParams p) {
     }
     const float inv = 1.f / wsum;
     float* O = p.o + b * p.o_bs + h * p.o_hs;
+    float amx = 0.f;
+    if (ok) {
 #pragma unroll
-    for (int j = 0; j < NC; ++j) O[(int64_t)(cg + 4 * j) * p.ldc + q] = acc[j] * inv;
+        for (int j = 0; j < NC; ++j) {
+            O[(int64_t)(cg + 4 * j) * p.ldc + q] = acc[j] * inv;
+            amx = fmaxf(amx, fabsf(acc[j] * inv));
+        }
+    }
+    if (p.amax_out) amax_publish(p.amax_out, amx);
+    if (!ok) return;
     if (p.ml && cg == 0) {
         float* ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;
         ML[q] = m;
@@ -288,7 +304,13 @@ extern "C" int64_t rvc_attention_workspace_bytes(const rvc_attn_args* a) {
 }
 
 extern "C" int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
+    return rvc_attention_amax(a, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, void* ws, int64_t ws_bytes,
+                                  rvc_stream_t stream) {
     RVC_CHECK_ARG(a && a->q && a->k && a->v && a->o && a->T > 0 && a->H > 0 && a->B > 0, "attention: bad args");
+    RVC_CHECK_ARG(!amax_out || !a->rk, "attention: amax_out is not built for the relative band");
     RVC_CHECK_ARG(a->D == 64 || a->D == 96, "attention: head dim %d unsupported (64, 96)", a->D);
     RVC_CHECK_ARG(!a->rk || (a->ml && a->W >= 0 && a->W <= 15), "attention: rel band needs ml and W <= 15");
     RVC_CHECK_ARG(!a->ev || (a->rk && (2 * a->W + 1) * a->D <= 31 * 96), "attention: ev band too large");
@@ -298,6 +320,7 @@ extern "C" int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes,
     p.q_hs = a->q_hs; p.k_hs = a->k_hs; p.v_hs = a->v_hs; p.o_hs = a->o_hs;
     p.q_bs = a->q_bs; p.k_bs = a->k_bs; p.v_bs = a->v_bs; p.o_bs = a->o_bs;
     p.H = a->H; p.W = a->W; p.scale = a->scale;
+    p.amax_out = amax_out;
     attn_plan(a, p.S, p.kps);
     p.ws = nullptr;
     if (p.S > 1) {

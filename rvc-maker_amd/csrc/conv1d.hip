@@ -65,27 +65,6 @@ static thread_local int g_f16_fast = -1;
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
 
-// amax_out: the wave's largest |stored value| folded into the tensor's cell (atomic max of the f32 bits: for values
-// >= 0 the bit patterns order as the floats do).  A cell is RVC_AMAX_SHARDS words and each wave adds to one of them
-// (by block and wave): thousands of waves on ONE address serialise at the memory side (round 5: the generator ran
-// 904 -> 882 xRT with one word per tensor).  Called by every lane of a wave (the shuffles need them all).
-__device__ __forceinline__ void amax_publish(unsigned* amax_out, float m) {
-    m = wave_max(m);
-    const unsigned shard = (blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z + (threadIdx.x >> 6)) % RVC_AMAX_SHARDS;
-    if ((threadIdx.x & 63) == 0) atomicMax(amax_out + shard, __float_as_uint(m));
-}
-
-// the |max| of a cell: the largest of its shards, read through the scalar cache (wave-uniform address, s_load: it does
-// not queue behind the wave's vector loads in vmcnt order, and no shuffle)
-typedef const __attribute__((address_space(4))) unsigned* amax_const_ptr;  // constant space: s_load
-__device__ __forceinline__ float amax_read(const unsigned* cell) {
-    const amax_const_ptr c = (amax_const_ptr)cell;  // read-only for the whole launch
-    unsigned m = 0;
-#pragma unroll
-    for (int i = 0; i < RVC_AMAX_SHARDS; ++i) m = max(m, c[i]);
-    return __uint_as_float(m);
-}
-
 // Output column n -> store position t; -1 when the column is not stored (beyond ncols / Lout);
 // -(t + 2) for a border cell of a 2-D image, which is stored as 0 (the bordered [C][H+2][W+2]
 // images then need no zero-fill).  32-bit math: every per-batch extent here is < 2^31.

@@ -50,6 +50,7 @@ struct rvc_ctx {
     bool x6 = true, f16mix = true, fused_rb = true;  // RVC_AMD_X6 / RVC_AMD_F16MIX / RVC_AMD_FUSED_RB as ops.py
     bool amax = true;  // RVC_AMD_AMAX as synth.py: the generator's |max| side channel
     bool amax_f16all = true;  // RVC_AMD_AMAX_F16ALL as ops.py
+    bool cv_amax = true;      // RVC_AMD_CV_AMAX as contentvec.py: ContentVec's GEMMs take the producers' |max|
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;

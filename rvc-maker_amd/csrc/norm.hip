@@ -72,10 +72,11 @@ __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const
 // values (x + res) at once, keeps them in registers through the two-pass mean / variance (sums reduced over the
 // wave's 4 groups by shuffles, then over the 16 waves through LDS) and writes the normalised values from
 // them.  4x the waves of the LDS-tile form per column block, no tile round trip.
+// amax_out (or null): max |out| folded into a |max| cell (rvc_conv1d_args.amax_in of the GEMM that reads out)
 template <int CPT>
 __global__ __launch_bounds__(1024) void layernorm_cf_reg_kernel(const float* x, const float* res, const float* gamma,
                                                                 const float* beta, float* out, int C, int64_t T,
-                                                                float eps) {
+                                                                float eps, unsigned* amax_out) {
     const int tid = threadIdx.x;
     const int col = tid & 15, grp = tid >> 4, wv = tid >> 6;  // 16 columns x 64 channel groups
     const int b = blockIdx.y;
@@ -121,27 +122,44 @@ __global__ __launch_bounds__(1024) void layernorm_cf_reg_kernel(const float* x, 
 #pragma unroll
     for (int w = 0; w < 16; ++w) var += red[1][w][col];
     const float rstd = 1.0f / sqrtf(var / (float)C + eps);
-    if (!ok) return;
-    float* ob = out + (int64_t)b * C * T + t;
+    float* ob = out + (int64_t)b * C * T + tc;
+    float amx = 0.f;
 #pragma unroll
     for (int u = 0; u < CPT; ++u) {
         const int c = grp + 64 * u;
-        if (c < C) ob[(int64_t)c * T] = (v[u] - mean) * rstd * gamma[c] + beta[c];
+        if (ok && c < C) {
+            const float y = (v[u] - mean) * rstd * gamma[c] + beta[c];
+            ob[(int64_t)c * T] = y;
+            amx = fmaxf(amx, fabsf(y));
+        }
     }
+    if (amax_out) amax_publish(amax_out, amx);  // every lane (the wave's shuffles)
 }
 
 extern "C" int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out,
                                 int64_t B, int64_t C, int64_t T, float eps, rvc_stream_t stream) {
+    return rvc_layernorm_cf_amax(x, res, gamma, beta, out, B, C, T, eps, nullptr, stream);
+}
+
+extern "C" int rvc_layernorm_cf_amax(const float* x, const float* res, const float* gamma, const float* beta,
+                                     float* out, int64_t B, int64_t C, int64_t T, float eps, unsigned* amax_out,
+                                     rvc_stream_t stream) {
     RVC_CHECK_ARG(x && gamma && beta && out && B > 0 && C > 0 && T > 0, "layernorm_cf: bad args");
     RVC_CHECK_ARG(C <= 2048, "layernorm_cf: C=%lld > 2048", (long long)C);
     static const int reg = getenv("RVC_LN_REG") ? atoi(getenv("RVC_LN_REG")) : 1;
+    RVC_CHECK_ARG(!amax_out || (reg && C > 256 && C <= 768), "layernorm_cf: amax_out needs the register form "
+                  "(256 < C <= 768, RVC_LN_REG=1), C=%lld", (long long)C);
     // measured (scripts/micro.py norms): C=768 T=1599 19.6 -> 12.0 us, C=512 12.0 -> 9.0; C=192 T=3198 8.7 -> 9.2
     // (the LDS-tile form keeps C <= 256)
     if (reg && C > 256 && C <= 768) {
         const dim3 grid(cdiv(T, 16), (unsigned)B);
         hipStream_t s = (hipStream_t)stream;
-        if (C <= 512) hipLaunchKernelGGL(layernorm_cf_reg_kernel<8>, grid, dim3(1024), 0, s, x, res, gamma, beta, out, (int)C, T, eps);
-        else hipLaunchKernelGGL(layernorm_cf_reg_kernel<12>, grid, dim3(1024), 0, s, x, res, gamma, beta, out, (int)C, T, eps);
+        if (C <= 512)
+            hipLaunchKernelGGL(layernorm_cf_reg_kernel<8>, grid, dim3(1024), 0, s, x, res, gamma, beta, out, (int)C, T,
+                               eps, amax_out);
+        else
+            hipLaunchKernelGGL(layernorm_cf_reg_kernel<12>, grid, dim3(1024), 0, s, x, res, gamma, beta, out, (int)C,
+                               T, eps, amax_out);
         RVC_HIP(hipGetLastError());
         return RVC_OK;
     }

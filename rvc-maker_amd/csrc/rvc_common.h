@@ -40,6 +40,27 @@ RVC_DEV float wave_max(float v) {
     return v;
 }
 
+// amax_out: the wave's largest |stored value| folded into the tensor's cell (atomic max of the f32 bits: for values
+// >= 0 the bit patterns order as the floats do).  A cell is RVC_AMAX_SHARDS words and each wave adds to one of them
+// (by block and wave): thousands of waves on ONE address serialise at the memory side (round 5: the generator ran
+// 904 -> 882 xRT with one word per tensor).  Called by every lane of a wave (the shuffles need them all).
+RVC_DEV void amax_publish(unsigned* amax_out, float m) {
+    m = wave_max(m);
+    const unsigned shard = (blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z + (threadIdx.x >> 6)) % RVC_AMAX_SHARDS;
+    if ((threadIdx.x & 63) == 0) atomicMax(amax_out + shard, __float_as_uint(m));
+}
+
+// the |max| of a cell: the largest of its shards, read through the scalar cache (wave-uniform address, s_load: it does
+// not queue behind the wave's vector loads in vmcnt order, and no shuffle)
+typedef const __attribute__((address_space(4))) unsigned* amax_const_ptr;  // constant space: s_load
+RVC_DEV float amax_read(const unsigned* cell) {
+    const amax_const_ptr c = (amax_const_ptr)cell;  // read-only for the whole launch
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < RVC_AMAX_SHARDS; ++i) m = max(m, c[i]);
+    return __uint_as_float(m);
+}
+
 // thread-local error reporting for the C ABI
 void rvc_set_error(const char* fmt, ...);
 

@@ -117,10 +117,21 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
     }
     const int64_t T = L;
     float* x512 = bufs[(7 - 1) & 1];  // layer 6's output
-    RUN(rvc_layernorm_cf(x512, nullptr, M.ln_w, M.ln_b, x512, 1, 512, T, 1e-5f, s));
+    // |max| cells as contentvec.py (cv_amax): cell 0 the FE LayerNorm's, 1 the encoder LayerNorm's, then per layer i
+    // 4 i + 2 .. 5 (attention, ln1, fc1, ln2); one memset per forward
+    const int nl = out_layer < (int)M.layers.size() ? out_layer : (int)M.layers.size();
+    unsigned* cells = nullptr;
+    if (c->cv_amax) {
+        cells = reinterpret_cast<unsigned*>(sc.take((int64_t)(2 + 4 * nl) * RVC_AMAX_SHARDS));
+        RUN(hipMemsetAsync(cells, 0, sizeof(unsigned) * (2 + 4 * nl) * RVC_AMAX_SHARDS, s) == hipSuccess ? RVC_OK
+                                                                                                     : RVC_EHIP);
+    }
+    auto cell = [&](int k) { return cells ? cells + (int64_t)k * RVC_AMAX_SHARDS : nullptr; };
+    RUN(rvc_layernorm_cf_amax(x512, nullptr, M.ln_w, M.ln_b, x512, 1, 512, T, 1e-5f, cell(0), s));
     float* xp = sc.take(E * T);
     {
         CallOpts o;
+        o.amax_in = cell(0);
         RUN(conv(c, M, M.proj, x512, T, xp, o, s));
     }
     float* xe = sc.take(E * T);
@@ -132,17 +143,19 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
         o.res = xp;
         RUN(conv(c, M, M.pos_conv, xp, T, xe, o, s));
     }
-    RUN(rvc_layernorm_cf(xe, nullptr, M.enc_ln_w, M.enc_ln_b, xe, 1, E, T, 1e-5f, s));
+    RUN(rvc_layernorm_cf_amax(xe, nullptr, M.enc_ln_w, M.enc_ln_b, xe, 1, E, T, 1e-5f, cell(1), s));
     const int64_t H = M.heads, D = E / H;
     float* qkv = sc.take(3 * E * T);
     float* ob = sc.take(E * T);
     float* yb = sc.take(E * T);
     float* hb = sc.take(M.layers[0].fc1.Co * T);
-    const int nl = out_layer < (int)M.layers.size() ? out_layer : (int)M.layers.size();
     for (int li = 0; li < nl; ++li) {
         const CvLayer& Ly = M.layers[li];
-        CallOpts o;
-        RUN(conv(c, M, Ly.qkv, xe, T, qkv, o, s));
+        unsigned *c_in = cell(4 * li + 1), *c_at = cell(4 * li + 2), *c_l1 = cell(4 * li + 3),
+                 *c_f1 = cell(4 * li + 4), *c_l2 = cell(4 * li + 5);
+        CallOpts oq;
+        oq.amax_in = c_in;
+        RUN(conv(c, M, Ly.qkv, xe, T, qkv, oq, s));
         rvc_attn_args at;
         memset(&at, 0, sizeof(at));
         at.q = qkv;
@@ -163,15 +176,21 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
             MCHECK(need >= 0, "rvc_contentvec_forward: attention shape H=%lld D=%lld T=%lld unsupported", (long long)H,
                    (long long)D, (long long)T);
             MTRY(ensure_ws(M, need, s));
-            MTRY(rvc_attention(&at, need ? M.ws : nullptr, need, s));
+            MTRY(rvc_attention_amax(&at, c_at, need ? M.ws : nullptr, need, s));
         }
-        RUN(conv(c, M, Ly.o, ob, T, yb, o, s));
-        RUN(rvc_layernorm_cf(xe, yb, Ly.ln1g, Ly.ln1b, xe, 1, E, T, 1e-5f, s));
+        CallOpts oo;
+        oo.amax_in = c_at;
+        RUN(conv(c, M, Ly.o, ob, T, yb, oo, s));
+        RUN(rvc_layernorm_cf_amax(xe, yb, Ly.ln1g, Ly.ln1b, xe, 1, E, T, 1e-5f, c_l1, s));
         CallOpts og;
         og.out_act = RVC_ACT_GELU;
+        og.amax_in = c_l1;
+        og.amax_out = c_f1;
         RUN(conv(c, M, Ly.fc1, xe, T, hb, og, s));
-        RUN(conv(c, M, Ly.fc2, hb, T, yb, o, s));
-        RUN(rvc_layernorm_cf(xe, yb, Ly.ln2g, Ly.ln2b, xe, 1, E, T, 1e-5f, s));
+        CallOpts o2;
+        o2.amax_in = c_f1;
+        RUN(conv(c, M, Ly.fc2, hb, T, yb, o2, s));
+        RUN(rvc_layernorm_cf_amax(xe, yb, Ly.ln2g, Ly.ln2b, xe, 1, E, T, 1e-5f, c_l2, s));
     }
     if (final_proj && cf_out) {  // VC.features_device: final_proj on the channels-first features
         CallOpts o;

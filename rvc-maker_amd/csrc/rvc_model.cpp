@@ -391,6 +391,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->fused_rb = env_on("RVC_AMD_FUSED_RB");
     c->amax = env_on("RVC_AMD_AMAX");
     c->amax_f16all = env_on("RVC_AMD_AMAX_F16ALL");
+    c->cv_amax = env_on("RVC_AMD_CV_AMAX");
     *out = c;
     return RVC_OK;
 }

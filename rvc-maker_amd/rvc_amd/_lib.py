@@ -145,6 +145,9 @@ SIGNATURES = {
     "rvc_conv1d_pack_f16": [c_void_p, c_int64, c_int64, c_int, c_int64, c_void_p, POINTER(c_int), c_void_p],
     "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],
     "rvc_attention": [POINTER(AttnArgs), c_void_p, c_int64, c_void_p],
+    "rvc_attention_amax": [POINTER(AttnArgs), c_void_p, c_void_p, c_int64, c_void_p],
+    "rvc_layernorm_cf_amax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
+                              c_void_p, c_void_p],
     "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
                           c_void_p],
     "rvc_layernorm_cf": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,

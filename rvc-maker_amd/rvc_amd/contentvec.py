@@ -18,10 +18,16 @@ key gets softmax weight exactly 0 and the padded row is dropped, so this runs un
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
 from .ops import ACT_GELU, Conv
+
+# ContentVec's K = 1 GEMMs take their split-fp16 scale from the producers' published |max| (LayerNorm, attention, fc1);
+# RVC_AMD_CV_AMAX=0: the 6-pass split-bf16 arithmetic of round 4
+CV_AMAX = os.environ.get("RVC_AMD_CV_AMAX", "1") != "0"
 
 FE_LAYERS = [(512, 10, 5)] + [(512, 3, 2)] * 4 + [(512, 2, 2)] * 2
 
@@ -218,28 +224,37 @@ class ContentVecAMD:
             else:
                 x = self.fe[i](x, stride=s, out_act=ACT_GELU)
         T = x.shape[-1]
-        ops.layernorm_cf(x, None, self.ln[0], self.ln[1], x, B, 512, T)
-        x = self.proj(x)  # [(B)][768][T]
+        # |max| cells (CV_AMAX): every LayerNorm, attention and fc1 publishes its output's |max| and the K = 1 GEMM that
+        # reads it runs split-fp16 from that scale (ops.conv_passes), no pre-pass
+        nl = min(output_layer, len(self.layers))
+        cells = ops.AmaxSlots(2 + 4 * nl, dev) if CV_AMAX else None
+        cell = (lambda k: cells[k]) if CV_AMAX else (lambda k: None)
+        ops.layernorm_cf(x, None, self.ln[0], self.ln[1], x, B, 512, T, amax_out=cell(0))
+        x = self.proj(x, amax_in=cell(0))  # [(B)][768][T]
         E = self.E
         bs = (B,) if batched else ()
         x2 = torch.empty(*bs, E, T, device=dev)
         self.pos_conv(x, pad=self.pos_k // 2, Lout=T, out=x2, out_act=ACT_GELU, res=x)  # SamePad drops the last col
         x = x2
-        ops.layernorm_cf(x, None, self.enc_ln[0], self.enc_ln[1], x, B, E, T)
+        ops.layernorm_cf(x, None, self.enc_ln[0], self.enc_ln[1], x, B, E, T, amax_out=cell(1))
         H = self.heads
         D = E // H
         o = torch.empty(*bs, E, T, device=dev)
         y = torch.empty(*bs, E, T, device=dev)
-        for L in self.layers[:output_layer]:
-            qkv = L["qkv"](x)
+        for i, L in enumerate(self.layers[:output_layer]):
+            # layer i reads cell 4 i + 1 (the encoder LayerNorm's, then the previous layer's ln2) and fills 4 i + 2 .. 5
+            c_in, c_at, c_l1, c_f1, c_l2 = (cell(4 * i + 1), cell(4 * i + 2), cell(4 * i + 3), cell(4 * i + 4),
+                                            cell(4 * i + 5))
+            qkv = L["qkv"](x, amax_in=c_in)
             k, v = (qkv[:, E:], qkv[:, 2 * E:]) if batched else (qkv[E:], qkv[2 * E:])
             ops.attention(qkv, k, v, o, B=B, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
-                          o_hs=D * T, scale=D ** -0.5, q_bs=3 * E * T, k_bs=3 * E * T, v_bs=3 * E * T, o_bs=E * T)
-            L["o"](o, out=y)
-            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, E, T)
-            h = L["fc1"](x, out_act=ACT_GELU)
-            L["fc2"](h, out=y)
-            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, B, E, T)
+                          o_hs=D * T, scale=D ** -0.5, q_bs=3 * E * T, k_bs=3 * E * T, v_bs=3 * E * T, o_bs=E * T,
+                          amax_out=c_at)
+            L["o"](o, out=y, amax_in=c_at)
+            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, E, T, amax_out=c_l1)
+            h = L["fc1"](x, out_act=ACT_GELU, amax_in=c_l1, amax_out=c_f1)
+            L["fc2"](h, out=y, amax_in=c_f1)
+            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, B, E, T, amax_out=c_l2)
         return x
 
     # ------------------------------------------------------------------ reference API

@@ -395,7 +395,8 @@ def resblock_pair(x, y, c1: "Conv", c2: "Conv", dil: int, slope: float, accumula
 
 
 def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_bs=0, k_bs=0, v_bs=0, o_bs=0,
-              rk=None, ev=None, ml=None, W=0):
+              rk=None, ev=None, ml=None, W=0, amax_out=None):
+    """Flash attention (rvc_attention); ``amax_out``: a |max| cell (``AmaxSlots``) that receives max |o|."""
     a = _lib.AttnArgs()
     a.q, a.k, a.v, a.o, a.rk, a.ev, a.ml = _p(q), _p(k), _p(v), _p(o), _p(rk), _p(ev), _p(ml)
     a.B, a.H, a.D, a.T, a.ldc = B, H, D, T, ldc
@@ -407,7 +408,10 @@ def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_b
     if need < 0:
         raise ValueError(f"attention: unsupported shape H={H} D={D} T={T}")
     ws = _workspace(o.device, need, "attn") if need else None
-    check(lib.rvc_attention(ctypes.byref(a), _p(ws), need, _stream()), "attention")
+    if amax_out is not None:
+        check(lib.rvc_attention_amax(ctypes.byref(a), _p(amax_out), _p(ws), need, _stream()), "attention")
+    else:
+        check(lib.rvc_attention(ctypes.byref(a), _p(ws), need, _stream()), "attention")
     return o
 
 
@@ -417,11 +421,16 @@ def textenc_embed(lin, emb, pitch, out, B, C, T, scale, slope):
     return out
 
 
-def layernorm_cf(x, res, gamma, beta, out, B, C, T, eps=1e-5):
+def layernorm_cf(x, res, gamma, beta, out, B, C, T, eps=1e-5, amax_out=None):
+    """LayerNorm over channels of x (+ res); ``amax_out``: a |max| cell that receives max |out|."""
     if x.numel() < B * C * T or out.numel() < B * C * T or gamma.numel() < C:
         raise ValueError("layernorm_cf: size mismatch")
-    check(_lib.load().rvc_layernorm_cf(_p(x), _p(res), _p(gamma), _p(beta), _p(out), B, C, T, eps, _stream()),
-          "layernorm_cf")
+    if amax_out is not None:
+        check(_lib.load().rvc_layernorm_cf_amax(_p(x), _p(res), _p(gamma), _p(beta), _p(out), B, C, T, eps,
+                                                _p(amax_out), _stream()), "layernorm_cf")
+    else:
+        check(_lib.load().rvc_layernorm_cf(_p(x), _p(res), _p(gamma), _p(beta), _p(out), B, C, T, eps, _stream()),
+              "layernorm_cf")
     return out
 
 
