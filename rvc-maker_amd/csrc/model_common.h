@@ -51,6 +51,7 @@ struct rvc_ctx {
     bool amax = true;  // RVC_AMD_AMAX as synth.py: the generator's |max| side channel
     bool amax_f16all = true;  // RVC_AMD_AMAX_F16ALL as ops.py
     bool cv_amax = true;      // RVC_AMD_CV_AMAX as contentvec.py: ContentVec's GEMMs take the producers' |max|
+    bool amax_ups = true;     // RVC_AMD_AMAX_UPS as synth.py: the upsampling convs' inputs through |max| cells
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;

@@ -118,7 +118,8 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
     b.work = p.take(T);
     b.snoise = p.take(L);
     b.xpre = p.take((int64_t)g.upsample_initial_channel * T);
-    b.amax = p.take(kAmaxPerStage * 8 * RVC_AMAX_SHARDS);  // the |max| cells of the ResBlock stages (synth.py generator)
+    // the |max| cells of the ResBlock stages, then one per stage output and one for conv_pre (synth.py generator)
+    b.amax = p.take((kAmaxPerStage * 8 + 8 + 1) * RVC_AMAX_SHARDS);
     int64_t Lc = T;
     for (size_t i = 0; i < S.ups.size(); ++i) {
         Lc = convT_out_len(S.ups[i], Lc);
@@ -267,11 +268,17 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     float* xcur = A + bf.xpre;
     unsigned* amax = reinterpret_cast<unsigned*>(A + bf.amax);
     const bool use_amax = c->amax && (int64_t)S.ups.size() <= 8;
-    if (use_amax) MHIP(hipMemsetAsync(amax, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * kAmaxPerStage * S.ups.size(), s));
+    const int64_t nst = (int64_t)S.ups.size();
+    if (use_amax)
+        MHIP(hipMemsetAsync(amax, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * (kAmaxPerStage * nst + nst + 1), s));
+    // the stage outputs' cells and conv_pre's, after the stages' own (synth.py's out_cell)
+    auto out_cell = [&](int64_t k) { return use_amax ? amax + RVC_AMAX_SHARDS * (kAmaxPerStage * nst + k) : nullptr; };
+    unsigned* x_cell = out_cell(nst);
     {
         CallOpts o;
         o.pad = 3;
         o.bias2 = gc + 4 * 6 * H;
+        o.amax_out = x_cell;
         MTRY(conv(c, S, S.conv_pre, z, T, xcur, o, s));
     }
     int64_t Lcur = T;
@@ -286,7 +293,9 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         ou.in_act = RVC_ACT_LRELU;
         ou.in_slope = kLreluSlope;
         ou.in_scale = scale_in;
+        ou.amax_in = c->amax_ups ? x_cell : nullptr;
         MTRY(conv(c, S, S.ups[i], xcur, Lcur, y, ou, s));
+        x_cell = nullptr;
         CallOpts on;
         on.Lout = Li;
         on.stride = S.noise_stride[i];
@@ -351,6 +360,10 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
                 if (last) {
                     nxt = xs;
                     o2.accumulate = j > 0;
+                    if (j == nk - 1 && use_amax) {  // the stage output's final values: its |max| cell
+                        o2.amax_out = out_cell((int64_t)i);
+                        x_cell = o2.amax_out;
+                    }
                 } else {
                     nxt = cur != xa ? xa : xb;
                     nxt_cell = cell && ncell < kAmaxPerStage ? cell + RVC_AMAX_SHARDS * ncell++ : nullptr;
@@ -392,6 +405,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->amax = env_on("RVC_AMD_AMAX");
     c->amax_f16all = env_on("RVC_AMD_AMAX_F16ALL");
     c->cv_amax = env_on("RVC_AMD_CV_AMAX");
+    c->amax_ups = env_on("RVC_AMD_AMAX_UPS");
     *out = c;
     return RVC_OK;
 }

@@ -31,6 +31,8 @@ LRELU_SLOPE = 0.1
 # the generator's |max| side channel (RVC_AMD_AMAX=0: per-tile pre-passes, the round-4 form; rvc_model.cpp reads the
 # same switch): cells per upsample stage -- y, then each unfused pair's c1 output and non-last c2 output
 AMAX = os.environ.get("RVC_AMD_AMAX", "1") != "0"
+# the upsampling convs' inputs through |max| cells too (conv_pre's output, each unfused stage's output; A/B switch)
+AMAX_UPS = os.environ.get("RVC_AMD_AMAX_UPS", "1") != "0"
 AMAX_PER_STAGE = 16
 
 
@@ -194,17 +196,23 @@ class SynthesizerAMD:
         har = torch.empty(B, L, device=dev)
         work = torch.empty(B, T, device=dev)
         ops.sine_source(nsff0, sine_noise, har, work, B, T, self.upp, float(self.sr), self.lin_w, self.lin_b)
-        x = self.conv_pre(z.reshape(B, self.inter, T), pad=3, bias2=gdec)
+        nst = len(self.ur)
+        cells = ops.AmaxSlots(AMAX_PER_STAGE * nst + nst + 1, dev) if AMAX else None
+        # cells after the stages' own: one per stage for its output xs (published by the last resblock's last c2 when
+        # that pair is unfused), one for conv_pre's output -- the upsampling convs' inputs
+        out_cell = (lambda k: cells[AMAX_PER_STAGE * nst + k]) if AMAX else (lambda k: None)
+        x = self.conv_pre(z.reshape(B, self.inter, T), pad=3, bias2=gdec, amax_out=out_cell(nst))
+        x_cell = out_cell(nst)
         scale = 1.0
         nk = len(self.rks)
         # the |max| side channel (ops.AmaxSlots, include/rvc_amd.h): in each stage y (written last by the noise conv),
         # every unfused c1 output t1 and every non-last c2 output publish their |max|, and the convs reading them take
         # their split-fp16 activation scale from it -- no per-tile pre-pass, so split-fp16 pays at k = 3 and 256
         # channels too (rvc_model.cpp mirrors this cell by cell)
-        cells = ops.AmaxSlots(AMAX_PER_STAGE * len(self.ur), dev) if AMAX else None
-        for i in range(len(self.ur)):
+        for i in range(nst):
             up = self.ups[i]
-            y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale)
+            y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale, amax_in=x_cell if AMAX_UPS else None)
+            x_cell = None
             Li = y.shape[-1]
             nc, s, pad = self.noise[i]
             base = AMAX_PER_STAGE * i
@@ -236,8 +244,12 @@ class SynthesizerAMD:
                     c1(cur, pad=(kk * d - d) // 2, dil=d, out=t1, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
                        amax_in=cur_cell, amax_out=t1_cell)
                     if m == len(pairs) - 1:
+                        # the last resblock's last c2 writes the stage output's final values: its |max| cell
+                        xo_cell = out_cell(i) if j == nk - 1 else None
                         c2(t1, pad=(kk - 1) // 2, out=xs, res=cur, in_act=ACT_LRELU, in_slope=LRELU_SLOPE,
-                           accumulate=(j > 0), amax_in=t1_cell)
+                           accumulate=(j > 0), amax_in=t1_cell, amax_out=xo_cell)
+                        if xo_cell is not None:
+                            x_cell = xo_cell
                         cur_cell = None
                     else:
                         nxt = xa if cur is not xa else xb
