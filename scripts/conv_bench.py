@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--only", type=str, default="", help="comma list of shape indices")
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--check", action="store_true", help="compare each shape with the f32-MFMA engine")
+    ap.add_argument("--amax", action="store_true", help="hand each conv its input's |max| cell (the generator's "
+                                                        "amax side channel: split-fp16 without the tile pre-pass)")
     args = ap.parse_args()
     from rvc_amd import ops
     ops.set_precision(args.precision)
@@ -40,7 +42,13 @@ def main():
         res = torch.randn(C, L, generator=g).cuda()
         y = torch.empty(C, L, device="cuda")
         p = d * (K - 1) // 2
-        fn = lambda: conv(x, pad=p, dil=d, out=y, res=res, in_act=ops.ACT_LRELU, in_slope=0.1)  # noqa: E731
+        akw = {}
+        if args.amax:
+            import numpy as np
+            cell = ops.AmaxSlots(1, "cuda")
+            cell.words[0] = int(np.float32(x.abs().max().item()).view(np.int32))
+            akw["amax_in"] = cell[0]
+        fn = lambda: conv(x, pad=p, dil=d, out=y, res=res, in_act=ops.ACT_LRELU, in_slope=0.1, **akw)  # noqa: E731
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

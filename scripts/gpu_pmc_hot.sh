@@ -8,7 +8,7 @@ SETS=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_AC
 i=0
 for set in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $O/pc$i -o run -- python3 scripts/conv_bench.py --only 4 --reps 3 > $O/c$i.log 2>&1 || { echo "conv pass $i failed"; tail -3 $O/c$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $O/pc$i -o run -- python3 scripts/conv_bench.py --only 4 --reps 3 ${CB_ARGS:-} > $O/c$i.log 2>&1 || { echo "conv pass $i failed"; tail -3 $O/c$i.log; exit 1; }
   timeout -s KILL 180 rocprofv3 --pmc $set --output-format csv -d $O/pr$i -o run -- python3 scripts/rb_bench.py --reps 2 > $O/r$i.log 2>&1 || { echo "rb pass $i failed"; tail -3 $O/r$i.log; exit 1; }
 done
 python3 scripts/pmc_summary.py $O conv_x6 > $O/summary_conv.txt; python3 scripts/pmc_summary.py $O resblock_x6 > $O/summary_rb.txt
