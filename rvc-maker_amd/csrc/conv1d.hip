@@ -1248,7 +1248,7 @@ int num_cus() {
 // split-K policy shared by both engines: split the chunk range when the tile grid underfills the chip
 // per-thread override of the split-K target grid (rvc_conv1d_set_splitk_target; -1 = the process default)
 static thread_local int g_splitk_target = -1;
-// per-thread override of the x6 tile epilogue (rvc_conv1d_set_tile_epi; -1 = RVC_X6_TILE_EPI, default on)
+// per-thread override of the x6 tile epilogue (rvc_conv1d_set_tile_epi; -1 = RVC_X6_TILE_EPI, default off)
 static thread_local int g_tile_epi = -1;
 
 void split_k(ConvParams& p, int64_t tiles, int nch, int per_cu = 2) {

@@ -60,7 +60,9 @@ namespace synthm {
 int64_t convT_out_len(const ConvW& cw, int64_t Lin) { return (Lin - 1) * cw.u - 2 * cw.tpad + cw.Kfull; }
 
 int rb_passes(const rvc_ctx* c, int K) {
-    if (c->prec == RVC_PREC_FP32 && c->f16mix && K >= 7) return RVC_ARITH_F16X3;
+    // the smallest split-fp16 kernel size (RVC_AMD_RB_F16_KMIN as ops.py, default 3)
+    static const int kmin = getenv("RVC_AMD_RB_F16_KMIN") ? atoi(getenv("RVC_AMD_RB_F16_KMIN")) : 3;
+    if (c->prec == RVC_PREC_FP32 && c->f16mix && K >= kmin) return RVC_ARITH_F16X3;
     return base_passes(c);
 }
 

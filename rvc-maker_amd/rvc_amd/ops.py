@@ -353,10 +353,15 @@ FUSED_RB = os.environ.get("RVC_AMD_FUSED_RB", "1") != "0"
 RB_PASSES = (6, 3, 1, F16X3)  # pass sets the fused kernel takes
 
 
+# the fused pair's smallest split-fp16 kernel size (RVC_AMD_RB_F16_KMIN, A/B switch): 3 since round 5 (C = 64 K = 3
+# pairs 371 -> 327 us, C = 32 250 -> 231, clip stream +0.6 %; scripts/gpu_r5_rbk3.sh), 7 before
+RB_F16_KMIN = int(os.environ.get("RVC_AMD_RB_F16_KMIN", "3"))
+
+
 def rb_passes(K):
-    """The fused ResBlock pair's pass set under the current precision: "fp32" mixes in split-fp16 for k >= 7
-    (measured 7-8 % faster there, slower at k = 3)."""
-    if _PRECISION == "fp32" and F16_MIX and K >= 7:
+    """The fused ResBlock pair's pass set under the current precision: "fp32" mixes in split-fp16 for
+    k >= RB_F16_KMIN (round 2: 7-8 % faster at k >= 7 and slower at k = 3; round 5: faster at k = 3 too)."""
+    if _PRECISION == "fp32" and F16_MIX and K >= RB_F16_KMIN:
         return F16X3
     return PASSES[_PRECISION]
 
