@@ -102,9 +102,23 @@ typedef struct rvc_conv1d_args {
        max |y| over every value the launch stores (atomic maxes of the f32 bits, spread over the words; the caller
        zeroes the cell before the producing launch), and amax_in (or NULL) is such a cell for x: a split-fp16
        launch (RVC_ARITH_F16X3) then takes its activation scale from the largest word (times |in_scale|: an upper
-       bound of |pre(x)|) instead of a per-tile |max| pre-pass over its input. */
+       bound of |pre(x)|) instead of a per-tile |max| pre-pass over its input.
+       A batched launch (B > 1) takes B consecutive cells, one per batch element: element b's at
+       amax + b * RVC_AMAX_SHARDS (round 6), so a clip's scale never depends on the other clips of its batch. */
     const unsigned* amax_in;
     unsigned* amax_out;
+    /* Fused source conv (round 6; NULL src_x = none): every stored output y[b][m][t] also adds
+       sum_k src_w[k][m] * src_x[b][t * src_stride - src_pad + k] + src_b[m] (zero outside [0, src_len)), after the
+       residual and accumulate operands -- a 1-input-channel conv of src_K taps over a [B][src_len] signal (batch
+       stride src_bstride, 0 = src_len; src_w KM-packed [src_K][Co] as a Ci = 1 conv weight, src_b [Co] or NULL).
+       The NSF generator's x = ups(x) + noise_convs(har) (synthesizers.py:156) in the upsampling conv's epilogue:
+       no separate launch reading and rewriting the stage output.  The k-sum is an fmaf chain in tap order from 0,
+       then + src_b, so it equals the separate 1-channel conv with accumulate. */
+    const float* src_x;
+    const float* src_w;
+    const float* src_b;
+    int src_K, src_stride, src_pad, _pad1;
+    int64_t src_len, src_bstride;
 } rvc_conv1d_args;
 
 /* Split-K (chosen by the library when the tile grid would underfill the 256 CUs) needs a caller-owned
@@ -202,7 +216,8 @@ typedef struct rvc_attn_args {
  * workspace of rvc_attention_workspace_bytes(a) bytes (0 when not split). */
 int64_t rvc_attention_workspace_bytes(const rvc_attn_args* a);
 int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
-/* the same, also folding max |o| into a |max| cell (amax_out as rvc_layernorm_cf_amax; not with the relative band) */
+/* the same, also folding max |o| into a |max| cell per batch element (amax_out as rvc_layernorm_cf_amax; not with the
+ * relative band) */
 int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 
 /* ------------------------------------------------------------------ elementwise
@@ -215,8 +230,8 @@ int rvc_textenc_embed(const float* lin, const float* emb, const int64_t* pitch, 
 /* LayerNorm over channels of (x + res)                  synthesizers.py:170-181, fairseq.py:700 */
 int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out, int64_t B,
                      int64_t C, int64_t T, float eps, rvc_stream_t stream);
-/* the same, also folding max |out| into a |max| cell (amax_out: RVC_AMAX_SHARDS zeroed u32 words, the amax_in of the
- * GEMM that reads out; ContentVec's LayerNorms, 256 < C <= 768) */
+/* the same, also folding max |out| into a |max| cell (amax_out: RVC_AMAX_SHARDS zeroed u32 words per batch element, the
+ * amax_in of the GEMM that reads out; ContentVec's LayerNorms -- any C <= 2048, both LayerNorm forms) */
 int rvc_layernorm_cf_amax(const float* x, const float* res, const float* gamma, const float* beta, float* out,
                           int64_t B, int64_t C, int64_t T, float eps, unsigned* amax_out, rvc_stream_t stream);
 /* GroupNorm(C, C) over time + affine (+ exact GELU)      fairseq.py:1149-1155,1183-1185 */
@@ -230,6 +245,11 @@ int64_t rvc_fe0_ws_bytes(int64_t B, int64_t C, int64_t T);
 int rvc_fe0_gn_gelu(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km, int64_t C, int K,
                     int stride, const float* gamma, const float* beta, float* out, float eps, int gelu, void* ws,
                     int64_t ws_bytes, rvc_stream_t stream);
+/* the same, also folding max |out| into a |max| cell per batch element (amax_out as rvc_layernorm_cf_amax): layer 1's
+ * split-fp16 conv takes its activation scale from it (round 6).  C <= 819 (the per-channel LDS records), K <= 16. */
+int rvc_fe0_gn_gelu_amax(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km, int64_t C, int K,
+                         int stride, const float* gamma, const float* beta, float* out, float eps, int gelu,
+                         unsigned* amax_out, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* z_p = m + exp(logs) * noise * nscale, stats = [m; logs]  synthesizers.py:449 */
 int rvc_prior_sample(const float* stats, const float* noise, float* zp, int64_t B, int64_t C, int64_t T, float nscale,
                      rvc_stream_t stream);
@@ -515,8 +535,11 @@ int rvc_crepe_smooth_coarse(const float* f0_raw, const float* pd_raw, int64_t T,
  *                              mixed with split-fp16 where measured faster), _FP32X6, _FP32SA, _F16X3,
  *                              _BF16X3, _BF16.  RMVPE has its own setting (below).
  *   rvc_ctx_set_rmvpe_precision RMVPE's arithmetic, read by the next rvc_load_rmvpe: RVC_PREC_FP64 (default: the
- *                              whole network in f64, rmvpe64.hip -- the f0 decisions of the exact model) or a
- *                              conv precision above for the f32 form (_FP32SA: round 3's split-accumulator convs).
+ *                              network in f64, rmvpe64.hip -- the f0 decisions of the exact model -- with ONE
+ *                              exception: the BiGRU recurrence runs in f32 behind the f64 interface (f64 inputs, f64
+ *                              output; its decision noise 1.8e-9, profiles/r5_rmvpe_stage_prec.json); all-f64 is
+ *                              rvc_bigru64_set_f32(0) or RVC_BIGRU64_F32=0), or a conv precision above for the
+ *                              f32 form (_FP32SA: round 3's split-accumulator convs).
  *   rvc_load_synth             params = the .pth "weight" dict (train.py:729-742) as named HOST arrays,
  *                              f32 or f16; weight-norm pairs (x.weight_g / x.weight_v) are folded at load
  *                              (torch._weight_norm, dim 0), already-folded x.weight is taken as is.

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
             ML[T + qa] = l_run;
         }
     }
-    if (p.amax_out && p.S == 1) amax_publish(p.amax_out, amx);  // every lane (the wave's shuffles)
+    if (p.amax_out && p.S == 1) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
 }
 
 // Merge S split-KV partials: o = sum_s o_s * l_s e^(m_s - m) / sum_s l_s e^(m_s - m).  Grid (T/64, H, B),
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnParams p) {
             amx = fmaxf(amx, fabsf(acc[j] * inv));
         }
     }
-    if (p.amax_out) amax_publish(p.amax_out, amx);
+    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
     if (!ok) return;
     if (p.ml && cg == 0) {
         float* ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;

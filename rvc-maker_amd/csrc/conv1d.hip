@@ -54,6 +54,12 @@ struct ConvParams {
     unsigned* amax_out;       // or null: max |y| over the stored values (atomic max of the f32 bits)
     int stagger;              // x6: the first round of blocks starts spread over this many shader cycles (0 = off)
     int stagger_blocks;       // ... the blocks of that round (one per CU)
+    // fused 1-channel source conv (rvc_conv1d_args.src_*): y += conv(src_x, src_w)[m][t] + src_b[m] in the epilogue
+    const float* src_x;
+    const float* src_w;  // KM [src_K][Co]
+    const float* src_b;
+    int src_K, src_stride, src_pad;
+    int64_t src_len, src_bstride;
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
@@ -79,6 +85,21 @@ __device__ __forceinline__ int out_pos(const ConvParams& p, int64_t n, int phase
     return t;
 }
 
+// The fused source conv of one output (m, t): sum_k src_w[k][m] * src[t * stride - pad + k] (zero outside the signal)
+// as an fmaf chain in tap order from 0, then + src_b[m] -- the k order and roundings of the 1-input-channel conv on the
+// f32 MFMA engine (v_mfma_f32_16x16x4_f32 is an exact fmaf chain), which this replaces (the NSF generator's
+// noise_convs, synthesizers.py:156: x = ups(x) + noise_convs(har)).
+__device__ __forceinline__ float src_term(const ConvParams& p, const float* sx, int64_t m, int t) {
+    const int64_t q0 = (int64_t)t * p.src_stride - p.src_pad;
+    float s = 0.f;
+    for (int k = 0; k < p.src_K; ++k) {
+        const int64_t q = q0 + k;
+        const float xv = (q >= 0 && q < p.src_len) ? sx[q] : 0.f;
+        s = fmaf(p.src_w[(int64_t)k * p.Co + m], xv, s);
+    }
+    return s + (p.src_b ? p.src_b[m] : 0.f);
+}
+
 // Branch-free epilogue for one element: every load is issued unconditionally from a clamped
 // address (a per-element guarded load makes hipcc branch and wait vmcnt(0) per element).
 // returns the value stored (0 when nothing is stored: a border cell stores 0, a column past the end nothing)
@@ -92,6 +113,7 @@ __device__ __forceinline__ float epilogue_store(const ConvParams& p, float acc, 
     if (p.res) v += p.res[b * p.res_bstride + o];
     float* yb = p.y + b * p.y_bstride;
     if (p.accumulate) v += yb[o];
+    if (p.src_x && ok) v += src_term(p, p.src_x + b * p.src_bstride, m, t);
     if (ok) yb[o] = v;
     else if (t <= -2) yb[m * p.Lout + (-t - 2)] = 0.f;  // 2-D border cell
     return ok ? v : 0.f;
@@ -181,6 +203,44 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
 #pragma unroll
                 for (int j = 0; j < FN; ++j) av[0][j][r] += yb[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
         }
+        if (p.src_x) {
+            // the fused source conv (src_term's chain): taps outer, the fragment's 4 rows x FN columns as running sums;
+            // each step's loads (FN signal samples shared by the 4 rows, 4 weights shared by the columns) issued together
+            const float* sx = p.src_x + b * p.src_bstride;
+            int64_t q0[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) q0[j] = (int64_t)(tcol[j] >= 0 ? tcol[j] : 0) * p.src_stride - p.src_pad;
+            float ns[FN][4];
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ns[j][r] = 0.f;
+            const int64_t len = p.src_len;
+#pragma unroll 2
+            for (int k = 0; k < p.src_K; ++k) {
+                float xv[FN], wv[4];
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int64_t q = q0[j] + k;
+                    xv[j] = sx[q < 0 ? 0 : (q >= len ? len - 1 : q)];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) wv[r] = p.src_w[(int64_t)k * p.Co + mrow[r]];
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int64_t q = q0[j] + k;
+                    const float x = (q >= 0 && q < len) ? xv[j] : 0.f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) ns[j][r] = fmaf(wv[r], x, ns[j][r]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float sb = p.src_b ? p.src_b[mrow[r]] : 0.f;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) av[0][j][r] += ns[j][r] + sb;
+            }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -193,7 +253,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
                 }
             }
     }
-    if (p.amax_out) amax_publish(p.amax_out, amx);
+    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // the batch element's cell
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -538,7 +598,7 @@ __device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const floa
                 amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
             }
         }
-        if (p.amax_out && !part) amax_publish(p.amax_out, amx);
+        if (p.amax_out && !part) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
         return;
     }
     // edge tile (the last column tile) or unaligned rows: element by element, lanes along the row
@@ -557,7 +617,7 @@ __device__ __forceinline__ void x6_tile_epilogue(const ConvParams& p, const floa
             amx = fmaxf(amx, fabsf(v));
         }
     }
-    if (p.amax_out && !part) amax_publish(p.amax_out, amx);
+    if (p.amax_out && !part) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
 }
 
 // LF (split-fp16 on 8 compute waves, with the producer's |max|: amax_in): the loaders take ONLY the fast form (1: leaky
@@ -811,7 +871,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
                 // the producer's atomics left at the memory side -- overlaps theirs
                 xload(pchunk(0), xr[0]);
                 xload(pchunk(1), xr[1]);
-                am = amax_read(p.amax_in) * fabsf(p.in_scale);
+                am = amax_read(p.amax_in + (int64_t)b * RVC_AMAX_SHARDS) * fabsf(p.in_scale);  // the element's cell
             } else if constexpr (!FASTL) {
                 for (int i = 2; i < nck; i += 2) {
                     xload(pchunk(i), xr[0]);
@@ -1133,7 +1193,7 @@ __global__ void conv_splitk_reduce(ConvParams p) {
     float s = 0.f;
     for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
     const float v = epilogue_store(p, s, bp / p.nphase, m, out_pos(p, n, bp % p.nphase));
-    if (p.amax_out) amax_publish(p.amax_out, fabsf(v));
+    if (p.amax_out) amax_publish(p.amax_out + (int64_t)(bp / p.nphase) * RVC_AMAX_SHARDS, fabsf(v));
 }
 
 struct Cfg {
@@ -1220,6 +1280,14 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.f16_fast = g_f16_fast >= 0 ? g_f16_fast : f16fast;
     p.stagger = 0;
     p.stagger_blocks = 0;
+    p.src_x = a->src_x;
+    p.src_w = a->src_w;
+    p.src_b = a->src_b;
+    p.src_K = a->src_K;
+    p.src_stride = a->src_stride;
+    p.src_pad = a->src_pad;
+    p.src_len = a->src_len;
+    p.src_bstride = a->src_bstride ? a->src_bstride : a->src_len;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -1314,6 +1382,10 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
     const int64_t Cig = a->Ci / a->groups;
     const int64_t ncols = a->ncols > 0 ? a->ncols : a->Lout;
     fill_common(a, p);
+    RVC_CHECK_ARG(!a->src_x || (a->src_w && a->src_K > 0 && a->src_K <= 4096 && a->src_stride > 0 && a->src_pad >= 0 &&
+                                a->src_len > 0 && a->src_bstride >= 0 && !a->wrap),
+                  "conv1d: bad fused source conv (src_K=%d src_stride=%d src_pad=%d src_len=%lld)", a->src_K,
+                  a->src_stride, a->src_pad, (long long)a->src_len);
     if (a->ntoff) {
         RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
         for (int i = 0; i < a->K; ++i) RVC_CHECK_ARG(a->toff[i] >= 0, "conv1d: negative tap offset");
@@ -1379,7 +1451,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         const int tepi = g_tile_epi >= 0 ? g_tile_epi : tepi_env;
         const size_t tile_bytes = (size_t)BM * (BN + 4) * 4;
         const bool plain = a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&
-                           BN <= 128;
+                           BN <= 128 && !a->src_x;
         p.tile_epi = !(tepi && plain) ? 0 : tile_bytes <= lds ? 1 : (cfg.WM % 2 == 0 && tile_bytes / 2 <= lds) ? 2 : 0;
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");

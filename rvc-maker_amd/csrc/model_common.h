@@ -52,6 +52,9 @@ struct rvc_ctx {
     bool amax_f16all = true;  // RVC_AMD_AMAX_F16ALL as ops.py
     bool cv_amax = true;      // RVC_AMD_CV_AMAX as contentvec.py: ContentVec's GEMMs take the producers' |max|
     bool amax_ups = true;     // RVC_AMD_AMAX_UPS as synth.py: the upsampling convs' inputs through |max| cells
+    bool amax_s2 = true;      // RVC_AMD_AMAX_S2 as ops.py: stride-2 convs with a producer's |max| in split-fp16
+    bool fe_amax = true;      // RVC_AMD_FE_AMAX as contentvec.py: the feature extractor's convs through |max| cells
+    bool fused_noise = true;  // RVC_AMD_FUSED_NOISE as synth.py: noise_convs fused into the upsampling convs
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;
@@ -293,8 +296,9 @@ inline int base_passes(const rvc_ctx* c) { return c->prec == RVC_PREC_FP32 ? 6 :
 
 // amax: the input's |max| comes from its producer (the amax side channel): split-fp16 for every stride-1 1-D conv
 inline int conv_passes(const rvc_ctx* c, int K, int64_t Cig, int stride, bool two_d, bool amax = false) {
-    if (c->prec == RVC_PREC_FP32 && c->f16mix && stride == 1 && !two_d &&
-        ((amax && c->amax_f16all) || (K >= 7 && Cig <= 256) || (K >= 3 && Cig >= 64 && Cig <= 128)))
+    if (c->prec == RVC_PREC_FP32 && c->f16mix && !two_d &&
+        ((stride == 1 && ((amax && c->amax_f16all) || (K >= 7 && Cig <= 256) || (K >= 3 && Cig >= 64 && Cig <= 128))) ||
+         (stride == 2 && amax && c->amax_f16all && c->amax_s2)))
         return RVC_ARITH_F16X3;
     return base_passes(c);
 }
@@ -339,6 +343,11 @@ struct CallOpts {
     int toff[16] = {0};
     const unsigned* amax_in = nullptr;  // the |max| side channel (rvc_conv1d_args.amax_in / amax_out)
     unsigned* amax_out = nullptr;
+    // the fused 1-channel source conv (rvc_conv1d_args.src_*; ops.conv1d's src): its weights, signal and geometry
+    const ConvW* src = nullptr;
+    const float* src_x = nullptr;
+    int src_stride = 1, src_pad = 0;
+    int64_t src_len = 0;
 };
 
 inline int conv(rvc_ctx* c, ModelBase& m, const ConvW& cw, const float* x, int64_t Lin, float* y, const CallOpts& o,
@@ -372,6 +381,16 @@ inline int conv(rvc_ctx* c, ModelBase& m, const ConvW& cw, const float* x, int64
     for (int i = 0; i < o.ntoff; ++i) a.toff[i] = o.toff[i];
     a.amax_in = o.amax_in;
     a.amax_out = o.amax_out;
+    if (o.src) {
+        a.src_x = o.src_x;
+        a.src_w = o.src->w;
+        a.src_b = o.src->b;
+        a.src_K = o.src->K;
+        a.src_stride = o.src_stride;
+        a.src_pad = o.src_pad;
+        a.src_len = o.src_len;
+        a.src_bstride = o.src_len;
+    }
     int stride = o.stride;
     if (cw.nphase > 1) {  // ConvT as u phase convs (ops.ConvT.__call__)
         const int64_t Lout = (Lin - 1) * cw.u - 2 * cw.tpad + cw.Kfull;

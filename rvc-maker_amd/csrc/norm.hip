@@ -14,7 +14,7 @@ constexpr int LN_UNROLL = 24;
 
 __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const float* res, const float* gamma,
                                                            const float* beta, float* out, int C, int64_t T,
-                                                           float eps) {
+                                                           float eps, unsigned* amax_out) {
     extern __shared__ __attribute__((aligned(16))) float tile[];  // [C][17]
     const int tid = threadIdx.x;
     const int col = tid & 15, grp = tid >> 4;  // 16 columns x 16 channel groups
@@ -62,9 +62,16 @@ __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const
     float var = 0.f;
     for (int g = 0; g < 16; ++g) var += red[g * 17 + col];
     const float rstd = 1.0f / sqrtf(var / (float)C + eps);
-    if (!ok) return;
     float* ob = out + (int64_t)b * C * T;
-    for (int c = grp; c < C; c += 16) ob[(int64_t)c * T + t] = (tile[c * 17 + col] - mean) * rstd * gamma[c] + beta[c];
+    float amx = 0.f;  // amax_out: largest |stored value| of this thread
+    if (ok) {
+        for (int c = grp; c < C; c += 16) {
+            const float y = (tile[c * 17 + col] - mean) * rstd * gamma[c] + beta[c];
+            ob[(int64_t)c * T + t] = y;
+            amx = fmaxf(amx, fabsf(y));
+        }
+    }
+    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
 }
 
 // Register-resident form for the path's small column counts (ContentVec: 1599 columns, TextEncoder: 3198):
@@ -133,7 +140,7 @@ __global__ __launch_bounds__(1024) void layernorm_cf_reg_kernel(const float* x, 
             amx = fmaxf(amx, fabsf(y));
         }
     }
-    if (amax_out) amax_publish(amax_out, amx);  // every lane (the wave's shuffles)
+    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
 }
 
 extern "C" int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out,
@@ -147,8 +154,6 @@ extern "C" int rvc_layernorm_cf_amax(const float* x, const float* res, const flo
     RVC_CHECK_ARG(x && gamma && beta && out && B > 0 && C > 0 && T > 0, "layernorm_cf: bad args");
     RVC_CHECK_ARG(C <= 2048, "layernorm_cf: C=%lld > 2048", (long long)C);
     static const int reg = getenv("RVC_LN_REG") ? atoi(getenv("RVC_LN_REG")) : 1;
-    RVC_CHECK_ARG(!amax_out || (reg && C > 256 && C <= 768), "layernorm_cf: amax_out needs the register form "
-                  "(256 < C <= 768, RVC_LN_REG=1), C=%lld", (long long)C);
     // measured (scripts/micro.py norms): C=768 T=1599 19.6 -> 12.0 us, C=512 12.0 -> 9.0; C=192 T=3198 8.7 -> 9.2
     // (the LDS-tile form keeps C <= 256)
     if (reg && C > 256 && C <= 768) {
@@ -165,7 +170,7 @@ extern "C" int rvc_layernorm_cf_amax(const float* x, const float* res, const flo
     }
     size_t lds = (size_t)(C + 16) * 17 * 4;
     hipLaunchKernelGGL(layernorm_cf_kernel, dim3(cdiv(T, 16), (unsigned)B), dim3(256), lds, (hipStream_t)stream, x,
-                       res, gamma, beta, out, (int)C, T, eps);
+                       res, gamma, beta, out, (int)C, T, eps, amax_out);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }
@@ -243,17 +248,17 @@ extern "C" int rvc_chnorm_gelu(const float* x, const float* gamma, const float* 
 // the [C][T] conv output's HBM round trip: the conv (K FMAs per output) is cheap enough to compute twice.
 //   fe0_stats:  per (time tile, channel) f64 sum / sum of squares of the conv outputs  -> ws partials
 //   fe0_final:  per channel, the partials in tile order -> mean, 1 / sqrt(var + eps)
-//   fe0_apply:  the conv again (the same fmaf chain, so the same bits), normalise, GELU, one coalesced write
+//   fe0_apply:  the conv again (the same fmaf chain, so the same bits), normalise, GELU, one coalesced write, and
+//               (amax_out) the output's |max| into a cell for the split-fp16 conv of layer 1
 // The separate conv + chnorm_gelu wrote the 210 MB output of a 32 s input at 0.4 TB/s and read it twice.
-// w is the conv's K-major packed weight ([K][C], ops.Conv / ConvW); x the 16 kHz signal [B][N] (batch stride xbs).
+// Round 6: the tap loops are fully unrolled to FE0_KMAX with a uniform k < K guard -- with a run-time trip count the
+// per-thread weight / sample arrays were indexed dynamically and lived in scratch (round 5: 273 + 389 us per 32 s
+// input for stats + apply), and fe0_final issues its partial loads in batches (one dependent HBM round trip per tile
+// made it 125 us).  w is the conv's K-major packed weight ([K][C], ops.Conv / ConvW); x the 16 kHz signal [B][N]
+// (batch stride xbs).
 constexpr int FE0_TT = 256;   // frames per tile
 constexpr int FE0_KMAX = 16;  // taps (ContentVec: 10)
-
-__device__ __forceinline__ float fe0_conv(const float* w, const float* xw, int c, int C, int K) {
-    float y = 0.f;
-    for (int k = 0; k < K; ++k) y = fmaf(w[k * C + c], xw[k], y);
-    return y;
-}
+constexpr int FE0_CW = 20;    // fe0_apply's LDS record per channel: K_MAX taps, then mean, rstd, gamma, beta
 
 __global__ __launch_bounds__(512) void fe0_stats_kernel(const float* x, int64_t xbs, int64_t T, const float* w, int C,
                                                         int K, int S, double* part) {
@@ -267,11 +272,14 @@ __global__ __launch_bounds__(512) void fe0_stats_kernel(const float* x, int64_t 
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         float wr[FE0_KMAX];
-        for (int k = 0; k < K; ++k) wr[k] = w[k * C + c];
+#pragma unroll
+        for (int k = 0; k < FE0_KMAX; ++k) wr[k] = k < K ? w[k * C + c] : 0.f;
         double s = 0.0, q = 0.0;
         for (int t = 0; t < nt; ++t) {
             float y = 0.f;
-            for (int k = 0; k < K; ++k) y = fmaf(wr[k], xs[t * S + k], y);
+#pragma unroll
+            for (int k = 0; k < FE0_KMAX; ++k)
+                if (k < K) y = fmaf(wr[k], xs[t * S + k], y);
             s += y;
             q += (double)y * y;
         }
@@ -283,14 +291,22 @@ __global__ __launch_bounds__(512) void fe0_stats_kernel(const float* x, int64_t 
 
 __global__ __launch_bounds__(256) void fe0_final_kernel(const double* part, int ntile, int C, int64_t T, float eps,
                                                         float* stat) {
+    constexpr int U = 16;  // partial loads in flight per thread
     const int b = blockIdx.y;
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
+    const double2* pb = reinterpret_cast<const double2*>(part) + (int64_t)b * ntile * C + c;
     double s = 0.0, q = 0.0;
-    for (int i = 0; i < ntile; ++i) {
-        const double* pp = part + (((int64_t)b * ntile + i) * C + c) * 2;
-        s += pp[0];
-        q += pp[1];
+    for (int i0 = 0; i0 < ntile; i0 += U) {
+        double2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = pb[(int64_t)min(i0 + u, ntile - 1) * C];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u < ntile) {  // tile order, as before
+                s += v[u].x;
+                q += v[u].y;
+            }
     }
     const double mean = s / (double)T;
     const double var = fmax(q / (double)T - mean * mean, 0.0);
@@ -300,30 +316,52 @@ __global__ __launch_bounds__(256) void fe0_final_kernel(const double* part, int 
 
 __global__ __launch_bounds__(256) void fe0_apply_kernel(const float* x, int64_t xbs, int64_t T, const float* w, int C,
                                                         int K, int S, const float* stat, const float* gamma,
-                                                        const float* beta, float* out, int gelu) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // w [K][C], then (mean, rstd, gamma, beta) [C][4]
-    float* ws = sm;
-    float* cs = sm + K * C;
+                                                        const float* beta, float* out, int gelu, unsigned* amax_out) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // per channel: w[0..K_MAX), mean, rstd, gamma, beta
     const int b = blockIdx.y;
-    for (int i = threadIdx.x; i < K * C; i += blockDim.x) ws[i] = w[i];
+    for (int i = threadIdx.x; i < C * FE0_KMAX; i += blockDim.x) {
+        const int c = i / FE0_KMAX, k = i - c * FE0_KMAX;
+        sm[c * FE0_CW + k] = k < K ? w[k * C + c] : 0.f;
+    }
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        cs[4 * c] = stat[((int64_t)b * C + c) * 2];
-        cs[4 * c + 1] = stat[((int64_t)b * C + c) * 2 + 1];
-        cs[4 * c + 2] = gamma[c];
-        cs[4 * c + 3] = beta[c];
+        sm[c * FE0_CW + FE0_KMAX] = stat[((int64_t)b * C + c) * 2];
+        sm[c * FE0_CW + FE0_KMAX + 1] = stat[((int64_t)b * C + c) * 2 + 1];
+        sm[c * FE0_CW + FE0_KMAX + 2] = gamma[c];
+        sm[c * FE0_CW + FE0_KMAX + 3] = beta[c];
     }
     __syncthreads();
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
+    const bool ok = t < T;
+    const int64_t tc = ok ? t : T - 1;
     float xw[FE0_KMAX];
-    const float* xb = x + b * xbs + t * S;
-    for (int k = 0; k < K; ++k) xw[k] = xb[k];
-    float* ob = out + (int64_t)b * C * T + t;
+    const float* xb = x + b * xbs + tc * S;
+#pragma unroll
+    for (int k = 0; k < FE0_KMAX; ++k) xw[k] = k < K ? xb[k] : 0.f;
+    float* ob = out + (int64_t)b * C * T + tc;
+    float amx = 0.f;
     for (int c = 0; c < C; ++c) {
-        const float y = fe0_conv(ws, xw, c, C, K);
-        const float v = (y - cs[4 * c]) * cs[4 * c + 1] * cs[4 * c + 2] + cs[4 * c + 3];
-        ob[(int64_t)c * T] = gelu ? act_apply(v, RVC_ACT_GELU, 0.f) : v;
+        const float4* rec = reinterpret_cast<const float4*>(sm + c * FE0_CW);  // same address in every lane: broadcast
+        float wr[FE0_KMAX + 4];
+#pragma unroll
+        for (int i = 0; i < FE0_CW / 4; ++i) {
+            const float4 v = rec[i];
+            wr[4 * i] = v.x;
+            wr[4 * i + 1] = v.y;
+            wr[4 * i + 2] = v.z;
+            wr[4 * i + 3] = v.w;
+        }
+        float y = 0.f;
+#pragma unroll
+        for (int k = 0; k < FE0_KMAX; ++k)
+            if (k < K) y = fmaf(wr[k], xw[k], y);  // fe0_stats' chain
+        const float v = (y - wr[FE0_KMAX]) * wr[FE0_KMAX + 1] * wr[FE0_KMAX + 2] + wr[FE0_KMAX + 3];
+        const float o = gelu ? act_apply(v, RVC_ACT_GELU, 0.f) : v;
+        if (ok) {
+            ob[(int64_t)c * T] = o;
+            amx = fmaxf(amx, fabsf(o));
+        }
     }
+    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
 }
 
 extern "C" int64_t rvc_fe0_ws_bytes(int64_t B, int64_t C, int64_t T) {
@@ -332,14 +370,19 @@ extern "C" int64_t rvc_fe0_ws_bytes(int64_t B, int64_t C, int64_t T) {
     return B * ntile * C * 2 * 8 + B * C * 2 * 4 + 256;
 }
 
-extern "C" int rvc_fe0_gn_gelu(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km, int64_t C,
-                               int K, int stride, const float* gamma, const float* beta, float* out, float eps,
-                               int gelu, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
-    RVC_CHECK_ARG(x && w_km && gamma && beta && out && ws && B > 0 && C > 0 && C <= 4096 && K > 0 &&
-                      K <= FE0_KMAX && stride > 0 && stride <= 8 && N >= K,
+extern "C" int rvc_fe0_gn_gelu_amax(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km,
+                                    int64_t C, int K, int stride, const float* gamma, const float* beta, float* out,
+                                    float eps, int gelu, unsigned* amax_out, void* ws, int64_t ws_bytes,
+                                    rvc_stream_t stream) {
+    RVC_CHECK_ARG(x && w_km && gamma && beta && out && ws && B > 0 && C > 0 && K > 0 && K <= FE0_KMAX && stride > 0 &&
+                      stride <= 8 && N >= K,
                   "fe0_gn_gelu: bad args");
+    // fe0_apply stages C records of FE0_CW floats in LDS: C <= 2048 (160 KB per CU; 64 KB per block by default)
+    RVC_CHECK_ARG((int64_t)C * FE0_CW * 4 <= 64 * 1024, "fe0_gn_gelu: C=%lld too large (<= %d)", (long long)C,
+                  64 * 1024 / (FE0_CW * 4));
     const int64_t T = (N - K) / stride + 1;
     RVC_CHECK_ARG(ws_bytes >= rvc_fe0_ws_bytes(B, C, T), "fe0_gn_gelu: workspace too small");
+    RVC_CHECK_ARG(((uintptr_t)ws & 15) == 0, "fe0_gn_gelu: workspace must be 16-B aligned");
     const int64_t xbs = x_bstride ? x_bstride : N;
     const int ntile = (int)((T + FE0_TT - 1) / FE0_TT);
     double* part = (double*)ws;
@@ -349,9 +392,16 @@ extern "C" int rvc_fe0_gn_gelu(const float* x, int64_t B, int64_t N, int64_t x_b
                        part);
     hipLaunchKernelGGL(fe0_final_kernel, dim3((unsigned)((C + 255) / 256), (unsigned)B), dim3(256), 0, s, part, ntile,
                        (int)C, T, eps, stat);
-    const size_t lds = (size_t)(K * C + 4 * C) * 4;
+    const size_t lds = (size_t)C * FE0_CW * 4;
     hipLaunchKernelGGL(fe0_apply_kernel, dim3((unsigned)((T + 255) / 256), (unsigned)B), dim3(256), lds, s, x, xbs, T,
-                       w_km, (int)C, K, stride, stat, gamma, beta, out, gelu);
+                       w_km, (int)C, K, stride, stat, gamma, beta, out, gelu, amax_out);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
+}
+
+extern "C" int rvc_fe0_gn_gelu(const float* x, int64_t B, int64_t N, int64_t x_bstride, const float* w_km, int64_t C,
+                               int K, int stride, const float* gamma, const float* beta, float* out, float eps,
+                               int gelu, void* ws, int64_t ws_bytes, rvc_stream_t stream) {
+    return rvc_fe0_gn_gelu_amax(x, B, N, x_bstride, w_km, C, K, stride, gamma, beta, out, eps, gelu, nullptr, ws,
+                                ws_bytes, stream);
 }

@@ -99,17 +99,32 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
     bufs[0] = sc.take(512 * L0);
     bufs[1] = sc.take(512 * L0);
     float* fe0ws = sc.take((rvc_fe0_ws_bytes(1, 512, L0) + 3) / 4);
+    // |max| cells as contentvec.py (cv_amax): cell 0 the FE LayerNorm's, 1 the encoder LayerNorm's, then per layer i
+    // 4 i + 2 .. 5 (attention, ln1, fc1, ln2), then (fe_amax) the feature extractor's layers 0-5; one memset per forward
+    const int nl = out_layer < (int)M.layers.size() ? out_layer : (int)M.layers.size();
+    const int nfe = 6;
+    unsigned* cells = nullptr;
+    if (c->cv_amax) {
+        cells = reinterpret_cast<unsigned*>(sc.take((int64_t)(2 + 4 * nl + nfe) * RVC_AMAX_SHARDS));
+        RUN(hipMemsetAsync(cells, 0, sizeof(unsigned) * (2 + 4 * nl + nfe) * RVC_AMAX_SHARDS, s) == hipSuccess
+                ? RVC_OK
+                : RVC_EHIP);
+    }
+    auto cell = [&](int k) { return cells ? cells + (int64_t)k * RVC_AMAX_SHARDS : nullptr; };
+    auto fe_cell = [&](int i) { return c->fe_amax ? cell(2 + 4 * nl + i) : nullptr; };
     for (int i = 0; i < 7; ++i) {
         const int k = kFeLayers[i][1], st = kFeLayers[i][2];
         const int64_t Lo = (L - k) / st + 1;
         float* y = bufs[i & 1];
         if (i == 0) {  // conv + GroupNorm + GELU fused (rvc_fe0_gn_gelu, as contentvec.py)
-            RUN(rvc_fe0_gn_gelu(x, 1, L, 0, M.fe[0].w, 512, k, st, M.gn_w, M.gn_b, y, 1e-5f, 1, fe0ws,
-                                rvc_fe0_ws_bytes(1, 512, Lo), s));
+            RUN(rvc_fe0_gn_gelu_amax(x, 1, L, 0, M.fe[0].w, 512, k, st, M.gn_w, M.gn_b, y, 1e-5f, 1, fe_cell(0), fe0ws,
+                                     rvc_fe0_ws_bytes(1, 512, Lo), s));
         } else {
             CallOpts o;
             o.stride = st;
             o.out_act = RVC_ACT_GELU;
+            o.amax_in = fe_cell(i - 1);
+            o.amax_out = i < nfe ? fe_cell(i) : nullptr;
             RUN(conv(c, M, M.fe[i], x, L, y, o, s));
         }
         x = y;
@@ -117,16 +132,6 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
     }
     const int64_t T = L;
     float* x512 = bufs[(7 - 1) & 1];  // layer 6's output
-    // |max| cells as contentvec.py (cv_amax): cell 0 the FE LayerNorm's, 1 the encoder LayerNorm's, then per layer i
-    // 4 i + 2 .. 5 (attention, ln1, fc1, ln2); one memset per forward
-    const int nl = out_layer < (int)M.layers.size() ? out_layer : (int)M.layers.size();
-    unsigned* cells = nullptr;
-    if (c->cv_amax) {
-        cells = reinterpret_cast<unsigned*>(sc.take((int64_t)(2 + 4 * nl) * RVC_AMAX_SHARDS));
-        RUN(hipMemsetAsync(cells, 0, sizeof(unsigned) * (2 + 4 * nl) * RVC_AMAX_SHARDS, s) == hipSuccess ? RVC_OK
-                                                                                                     : RVC_EHIP);
-    }
-    auto cell = [&](int k) { return cells ? cells + (int64_t)k * RVC_AMAX_SHARDS : nullptr; };
     RUN(rvc_layernorm_cf_amax(x512, nullptr, M.ln_w, M.ln_b, x512, 1, 512, T, 1e-5f, cell(0), s));
     float* xp = sc.take(E * T);
     {

@@ -291,24 +291,34 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         const int64_t slab = (C * Li + 63) & ~int64_t(63);
         float* R = A + bf.reg[i & 1];
         float *y = R, *xa = R + slab, *xb = R + 2 * slab, *xs = R + 3 * slab, *t1 = R + 4 * slab;
+        // the |max| side channel (synth.py generator): y, each unfused c1 output and each non-last c2 output publish
+        // their |max|; the convs that read them take their split-fp16 scale from it
+        unsigned* cell = use_amax ? amax + RVC_AMAX_SHARDS * kAmaxPerStage * i : nullptr;
+        int ncell = 1;
         CallOpts ou;
         ou.in_act = RVC_ACT_LRELU;
         ou.in_slope = kLreluSlope;
         ou.in_scale = scale_in;
         ou.amax_in = c->amax_ups ? x_cell : nullptr;
+        if (c->fused_noise) {  // y = ups(x) + noise_convs(har) in one launch (synth.py FUSED_NOISE)
+            ou.src = &S.noise[i];
+            ou.src_x = har;
+            ou.src_stride = S.noise_stride[i];
+            ou.src_pad = S.noise_pad[i];
+            ou.src_len = L;
+            ou.amax_out = cell;
+        }
         MTRY(conv(c, S, S.ups[i], xcur, Lcur, y, ou, s));
         x_cell = nullptr;
-        CallOpts on;
-        on.Lout = Li;
-        on.stride = S.noise_stride[i];
-        on.pad = S.noise_pad[i];
-        on.accumulate = 1;
-        // the |max| side channel (synth.py generator): y, each unfused c1 output and each non-last c2 output publish
-        // their |max|; the convs that read them take their split-fp16 scale from it
-        unsigned* cell = use_amax ? amax + RVC_AMAX_SHARDS * kAmaxPerStage * i : nullptr;
-        int ncell = 1;
-        if (cell) on.amax_out = cell;
-        MTRY(conv(c, S, S.noise[i], har, L, y, on, s));
+        if (!c->fused_noise) {
+            CallOpts on;
+            on.Lout = Li;
+            on.stride = S.noise_stride[i];
+            on.pad = S.noise_pad[i];
+            on.accumulate = 1;
+            if (cell) on.amax_out = cell;
+            MTRY(conv(c, S, S.noise[i], har, L, y, on, s));
+        }
         for (int j = 0; j < nk; ++j) {
             const int kk = g.resblock_kernel_sizes[j];
             const std::vector<Pair>& pairs = S.res[i][j];
@@ -408,6 +418,9 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->amax_f16all = env_on("RVC_AMD_AMAX_F16ALL");
     c->cv_amax = env_on("RVC_AMD_CV_AMAX");
     c->amax_ups = env_on("RVC_AMD_AMAX_UPS");
+    c->amax_s2 = env_on("RVC_AMD_AMAX_S2");
+    c->fe_amax = env_on("RVC_AMD_FE_AMAX");
+    c->fused_noise = env_on("RVC_AMD_FUSED_NOISE");
     *out = c;
     return RVC_OK;
 }

@@ -28,7 +28,10 @@ class Conv1dArgs(ctypes.Structure):
                 ("in_scale", c_float), ("in_slope", c_float), ("out_slope", c_float), ("out_scale", c_float),
                 ("ntoff", c_int), ("wrap", c_int), ("toff", c_int * 16),
                 ("wx", c_void_p), ("wx_nmf", c_int), ("wx_passes", c_int),
-                ("amax_in", c_void_p), ("amax_out", c_void_p)]
+                ("amax_in", c_void_p), ("amax_out", c_void_p),
+                ("src_x", c_void_p), ("src_w", c_void_p), ("src_b", c_void_p),
+                ("src_K", c_int), ("src_stride", c_int), ("src_pad", c_int), ("_pad1", c_int),
+                ("src_len", c_int64), ("src_bstride", c_int64)]
 
 
 class Conv64Args(ctypes.Structure):
@@ -156,6 +159,8 @@ SIGNATURES = {
     "rvc_fe0_ws_bytes": [c_int64, c_int64, c_int64],
     "rvc_fe0_gn_gelu": [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p,
                         c_float, c_int, c_void_p, c_int64, c_void_p],
+    "rvc_fe0_gn_gelu_amax": [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p,
+                             c_void_p, c_float, c_int, c_void_p, c_void_p, c_int64, c_void_p],
     "rvc_prior_sample": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p],
     "rvc_gate": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],
     "rvc_flip_channels": [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p],

@@ -28,6 +28,9 @@ from .ops import ACT_GELU, Conv
 # ContentVec's K = 1 GEMMs take their split-fp16 scale from the producers' published |max| (LayerNorm, attention, fc1);
 # RVC_AMD_CV_AMAX=0: the 6-pass split-bf16 arithmetic of round 4
 CV_AMAX = os.environ.get("RVC_AMD_CV_AMAX", "1") != "0"
+# round 6: the feature extractor's convs publish and read cells too (layer 0's fused GELU output, then each stride-2
+# conv + GELU), so layers 1-6 run split-fp16; RVC_AMD_FE_AMAX=0: 6-pass split-bf16 there (the round-5 form)
+FE_AMAX = os.environ.get("RVC_AMD_FE_AMAX", "1") != "0"
 
 FE_LAYERS = [(512, 10, 5)] + [(512, 3, 2)] * 4 + [(512, 2, 2)] * 2
 
@@ -218,17 +221,22 @@ class ContentVecAMD:
         batched = wav.dim() == 2
         B, N = (wav.shape[0], wav.shape[1]) if batched else (1, wav.numel())
         x = wav.reshape(B, 1, N) if batched else wav.view(1, N)
+        # |max| cells (CV_AMAX): every LayerNorm, attention and fc1 publishes its output's |max| and the K = 1 GEMM that
+        # reads it runs split-fp16 from that scale (ops.conv_passes), no pre-pass; so do the feature extractor's layers
+        # 0-5 (round 6): layers 1-6 (stride 2) run split-fp16 from their input's cell (cells 2 + 4 nl + i)
+        nl = min(output_layer, len(self.layers))
+        nfe = len(FE_LAYERS) - 1
+        cells = ops.AmaxSlots(2 + 4 * nl + nfe, dev, B) if CV_AMAX else None
+        cell = (lambda k: cells[k]) if CV_AMAX else (lambda k: None)
+        fe_cell = (lambda i: cells[2 + 4 * nl + i]) if CV_AMAX and FE_AMAX else (lambda i: None)
         for i, (c, k, s) in enumerate(FE_LAYERS):
             if i == 0:  # conv + GroupNorm + GELU in one pass over the signal (rvc_fe0_gn_gelu)
-                x = ops.fe0_gn_gelu(wav.contiguous(), self.fe[0].w, self.gn[0], self.gn[1], B, N, c, k, s)
+                x = ops.fe0_gn_gelu(wav.contiguous(), self.fe[0].w, self.gn[0], self.gn[1], B, N, c, k, s,
+                                    amax_out=fe_cell(0))
             else:
-                x = self.fe[i](x, stride=s, out_act=ACT_GELU)
+                x = self.fe[i](x, stride=s, out_act=ACT_GELU, amax_in=fe_cell(i - 1),
+                               amax_out=fe_cell(i) if i < nfe else None)
         T = x.shape[-1]
-        # |max| cells (CV_AMAX): every LayerNorm, attention and fc1 publishes its output's |max| and the K = 1 GEMM that
-        # reads it runs split-fp16 from that scale (ops.conv_passes), no pre-pass
-        nl = min(output_layer, len(self.layers))
-        cells = ops.AmaxSlots(2 + 4 * nl, dev) if CV_AMAX else None
-        cell = (lambda k: cells[k]) if CV_AMAX else (lambda k: None)
         ops.layernorm_cf(x, None, self.ln[0], self.ln[1], x, B, 512, T, amax_out=cell(0))
         x = self.proj(x, amax_in=cell(0))  # [(B)][768][T]
         E = self.E

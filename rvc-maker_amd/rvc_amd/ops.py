@@ -70,6 +70,9 @@ F16_MIX = os.environ.get("RVC_AMD_F16MIX", "1") != "0"
 # where conv_passes picks it anyway; the cell then just replaces the per-tile pre-pass)
 AMAX_F16ALL = os.environ.get("RVC_AMD_AMAX_F16ALL", "1") != "0"
 AMAX_SHARDS = 64  # RVC_AMAX_SHARDS: u32 words per |max| cell
+# round 6: the stride-2 convs with a producer's |max| (ContentVec's feature extractor) in split-fp16 too
+# (RVC_AMD_AMAX_S2=0: 6-pass split-bf16 there, the round-5 form; rvc_model_common's conv_passes reads the same switch)
+AMAX_S2 = os.environ.get("RVC_AMD_AMAX_S2", "1") != "0"
 
 
 def conv_passes(K, Ci, stride=1, two_d=False, amax=False):
@@ -78,8 +81,9 @@ def conv_passes(K, Ci, stride=1, two_d=False, amax=False):
     input channels, and k = 3 at 64-128 channels; 6-pass at k = 3 over 256 or 32 channels) -- and every stride-1
     1-D conv whose input's |max| comes from its producer (``amax``: no per-tile pre-pass, which is what made the
     short-tap and wide convs slower in split-fp16)."""
-    if _PRECISION == "fp32" and F16_MIX and stride == 1 and not two_d and \
-            ((amax and AMAX_F16ALL) or (K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128)):
+    if _PRECISION == "fp32" and F16_MIX and not two_d and \
+            ((stride == 1 and ((amax and AMAX_F16ALL) or (K >= 7 and Ci <= 256) or (K >= 3 and 64 <= Ci <= 128))) or
+             (stride == 2 and amax and AMAX_F16ALL and AMAX_S2)):
         return F16X3
     return PASSES[_PRECISION]
 _PRECISION = os.environ.get("RVC_AMD_PRECISION", "fp32")
@@ -210,19 +214,31 @@ class ConvT:
 
 
 class AmaxSlots:
-    """n |max| cells (the conv engine's amax side channel, AMAX_SHARDS words each) for one pass, zeroed by one
-    launch: ``s[k]`` is cell k, handed to a producer as ``amax_out`` and to its consumers as ``amax_in``."""
+    """n |max| cells (the conv engine's amax side channel, AMAX_SHARDS words each) for one pass of B batch elements,
+    zeroed by one launch: ``s[k]`` is cell k -- B consecutive cells, one per batch element (element b's |max| at word
+    b * AMAX_SHARDS: a clip's split-fp16 scale never depends on the other clips of its batch) -- handed to a producer
+    as ``amax_out`` and to its consumers as ``amax_in``."""
 
-    def __init__(self, n, device):
-        self.words = torch.zeros(n * AMAX_SHARDS, dtype=torch.int32, device=device)
+    def __init__(self, n, device, B=1):
+        self.B = B
+        self.words = torch.zeros(n * B * AMAX_SHARDS, dtype=torch.int32, device=device)
 
     def __getitem__(self, k):
-        return self.words[k * AMAX_SHARDS:(k + 1) * AMAX_SHARDS]
+        w = self.B * AMAX_SHARDS
+        return self.words[k * w:(k + 1) * w]
+
+
+def amax_value(cell, b=0):
+    """The |max| a cell holds for batch element b (the largest of its words, read back as f32)."""
+    import numpy as np
+    words = cell[b * AMAX_SHARDS:(b + 1) * AMAX_SHARDS].cpu().numpy().astype(np.int32)
+    return float(words.view(np.float32).max())
 
 
 LAST_CONV_FLOPS = 0.0
 LAST_CONV_ENGINE = 0  # 0 = f32 MFMA engine, 1 = split-bf16 (x6) engine
 LAST_CONV_PASSES = 0  # the split-operand launch's pass set (PASSES values; F16X3 = split-fp16), 0 = f32 engine
+LAST_CONV_WS = 0  # its split-K workspace bytes (0 = not split)
 _WS = {}
 _WS_PRIVATE = None  # a workspace store owned by a captured graph (private_workspaces)
 
@@ -277,16 +293,20 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
            nphase=1, ostride=1, ooffset=0, out=None, res=None, in_act=ACT_NONE, in_slope=0.0, in_scale=1.0,
            out_act=ACT_NONE, out_slope=0.0, out_scale=1.0, accumulate=False, B=None, Lin=None, x_bstride=0,
            w_bstride=0, y_bstride=0, res_bstride=0, toff=None, wrap=0, flops=None, wx=None, wx_nmf=0,
-           amax_in=None, amax_out=None):
+           amax_in=None, amax_out=None, src=None):
     """y = conv(pre(x)) with fused epilogue.  x: [B][Ci][Lin] device f32 (t contiguous).
 
-    ``amax_out`` / ``amax_in``: one-word device tensors (``AmaxSlots``) of the |max| side channel -- the launch
-    folds max |y| into ``amax_out`` (zeroed beforehand), and a split-fp16 launch takes its activation scale from
-    ``amax_in`` (the producer's word for x) instead of a per-tile pre-pass (include/rvc_amd.h).
+    ``amax_out`` / ``amax_in``: cells of the |max| side channel (``AmaxSlots``: AMAX_SHARDS words per batch element)
+    -- the launch folds max |y| into ``amax_out`` (zeroed beforehand), and a split-fp16 launch takes its activation
+    scale from ``amax_in`` (the producer's cell for x) instead of a per-tile pre-pass (include/rvc_amd.h).
+
+    ``src`` = (conv, signal [B][N], stride, pad): the fused source conv -- every stored output also adds
+    ``conv(signal)[m][t]`` of a 1-input-channel ``ops.Conv`` (the NSF generator's noise_convs, synthesizers.py:156),
+    the same bits as that conv run separately with ``accumulate`` (rvc_conv1d_args.src_*).
 
     ``flops`` is the launch's ALGORITHMIC FLOP count for roofline accounting (recorded in
     LAST_CONV_FLOPS); the default is 2*B*Co*(Ci/g)*K*(valid outputs)."""
-    global LAST_CONV_FLOPS, LAST_CONV_ENGINE, LAST_CONV_PASSES
+    global LAST_CONV_FLOPS, LAST_CONV_ENGINE, LAST_CONV_PASSES, LAST_CONV_WS
     if B is None:
         B, Cx, Lx = _shape3(x)
         if Lin is None:
@@ -330,6 +350,19 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
             a.toff[i] = int(v)
     a.wrap = wrap
     a.amax_in, a.amax_out = _p(amax_in), _p(amax_out)
+    for cell in (amax_in, amax_out):
+        if cell is not None and cell.numel() < B * AMAX_SHARDS:
+            raise ValueError(f"conv1d: a |max| cell needs {AMAX_SHARDS} words per batch element (B={B})")
+    if src is not None:
+        sconv, sig, s_stride, s_pad = src
+        if sconv.Ci != 1 or sconv.groups != 1 or sconv.Co != Co:
+            raise ValueError("conv1d: src needs a 1-input-channel conv with the output's channels")
+        s_len = sig.shape[-1]
+        if sig.dim() not in (1, 2) or (sig.dim() == 2 and sig.shape[0] != B) or not sig.is_contiguous() or \
+                (sig.dim() == 1 and B != 1):
+            raise ValueError("conv1d: src signal must be contiguous [B][N]")
+        a.src_x, a.src_w, a.src_b = _p(sig), _p(sconv.w), _p(sconv.b)
+        a.src_K, a.src_stride, a.src_pad, a.src_len, a.src_bstride = sconv.K, s_stride, s_pad, s_len, s_len
     if wx is not None:
         passes = conv_passes(K, Ci // groups, stride, toff is not None, amax_in is not None)
         a.wx, a.wx_nmf, a.wx_passes = ctypes.c_void_p(wx.data_ptr(passes)), wx_nmf, passes
@@ -342,6 +375,7 @@ def conv1d(x, w, Ci, Co, K, *, bias=None, bias2=None, stride=1, pad=0, dil=1, gr
     if need < 0:
         raise RuntimeError(f"rvc_amd: conv1d plan failed: {lib.rvc_last_error().decode()}")
     ws = _workspace(out.device, need) if need else None
+    LAST_CONV_WS = need
     LAST_CONV_ENGINE = lib.rvc_conv1d_engine(ctypes.byref(a))
     LAST_CONV_PASSES = a.wx_passes if LAST_CONV_ENGINE == 1 else 0
     check(lib.rvc_conv1d(ctypes.byref(a), _p(ws), need, _stream()), "conv1d")
@@ -447,16 +481,19 @@ def chnorm_gelu(x, gamma, beta, out, B, C, L, eps=1e-5, gelu=True):
     return out
 
 
-def fe0_gn_gelu(wav, w_km, gamma, beta, B, N, C, K, stride, eps=1e-5, gelu=True, x_bstride=0):
+def fe0_gn_gelu(wav, w_km, gamma, beta, B, N, C, K, stride, eps=1e-5, gelu=True, x_bstride=0, amax_out=None):
     """ContentVec's first layer fused: conv(1 -> C, k K, stride) of wav [B][N] + GroupNorm(C, C) + affine + GELU
-    -> [B][C][T] (rvc_fe0_gn_gelu; w_km: the K-major packed conv weight [K][C], ops.Conv.w)."""
+    -> [B][C][T] (rvc_fe0_gn_gelu; w_km: the K-major packed conv weight [K][C], ops.Conv.w); ``amax_out``: a |max|
+    cell (``AmaxSlots``) that receives max |out| per batch element (rvc_fe0_gn_gelu_amax)."""
     lib = _lib.load()
     T = (N - K) // stride + 1
     out = torch.empty(B, C, T, device=wav.device) if B > 1 else torch.empty(C, T, device=wav.device)
     need = lib.rvc_fe0_ws_bytes(B, C, T)
     ws = _workspace(wav.device, need, kind="fe0")
-    check(lib.rvc_fe0_gn_gelu(_p(wav), B, N, x_bstride, _p(w_km), C, K, stride, _p(gamma), _p(beta), _p(out), eps,
-                              int(gelu), _p(ws), need, _stream()), "fe0_gn_gelu")
+    if amax_out is not None and amax_out.numel() < B * AMAX_SHARDS:
+        raise ValueError("fe0_gn_gelu: amax_out needs a cell per batch element")
+    check(lib.rvc_fe0_gn_gelu_amax(_p(wav), B, N, x_bstride, _p(w_km), C, K, stride, _p(gamma), _p(beta), _p(out),
+                                   eps, int(gelu), _p(amax_out), _p(ws), need, _stream()), "fe0_gn_gelu")
     return out
 
 

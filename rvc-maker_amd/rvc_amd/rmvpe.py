@@ -15,8 +15,10 @@ into the convolutions on the host at load.  On the device:
             -> Linear 512->360 + sigmoid -> f64 decode + coarse pitch (rmvpe_decode)
 
 Arithmetic (``precision``, RVC_RMVPE_PRECISION): "f64" (the default) runs every step above in f64 -- the convs on
-the f64 matrix cores (rmvpe64.hip), the BiGRU recurrence in f64 -- and rounds only the salience to f32 for the
-decode.  RMVPE's f0 is a per-frame decision (argmax over 360 bins, 0.03 voicing threshold) and on the headline
+the f64 matrix cores (rmvpe64.hip) -- except the BiGRU recurrence, which runs in f32 behind the f64 interface (f64
+gate inputs and output; round 5: its decision noise is 1.8e-9 against the headline clip's smallest margin 3.2e-6,
+profiles/r5_rmvpe_stage_prec.json; the all-f64 recurrence is ``rvc_bigru64_set_f32(0)`` / RVC_BIGRU64_F32=0) -- and
+rounds only the salience to f32 for the decode.  RMVPE's f0 is a per-frame decision (argmax over 360 bins, 0.03 voicing threshold) and on the headline
 clip the exact model's top two bins are 3.2e-6 apart at one frame, while every f32 evaluation errs by up to
 1.7e-4 (the reference's own at other thread counts included): only an f64 network takes the exact model's
 decisions everywhere.  "fp32sa" / any ops.PASSES name runs the f32 form (split-bf16 MFMA convs,

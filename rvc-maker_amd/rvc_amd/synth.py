@@ -8,8 +8,8 @@ All compute runs in librvc_amd.so kernels on the current torch stream:
   TextEncoder  conv1d(K=1) + textenc_embed + 6 x [fused QKV conv, rel-pos flash attention,
                conv_o, LN, FFN (conv k3 ReLU, conv k3), LN] + proj + prior_sample
   flow^-1      4 x [flip, pre, WaveNet(3 x conv k5 + gate + res/skip convs), post (fused x1 - m)]
-  NSF-HiFiGAN  sine_source, conv_pre(+cond), 4 x [ConvT (polyphase, lrelu fused on staging)
-               + noise_conv (accumulate) + 3 ResBlocks (lrelu fused, residual / running sum
+  NSF-HiFiGAN  sine_source, conv_pre(+cond), 4 x [ConvT (polyphase, lrelu fused on staging, noise_conv fused in
+               its epilogue) + 3 ResBlocks (lrelu fused, residual / running sum
                fused in the epilogue; at 32 / 64 channels each conv pair is one fused launch,
                csrc/resblock.hip)], conv_post (lrelu 0.01 + tanh fused)
 
@@ -34,6 +34,9 @@ AMAX = os.environ.get("RVC_AMD_AMAX", "1") != "0"
 # the upsampling convs' inputs through |max| cells too (conv_pre's output, each unfused stage's output; A/B switch)
 AMAX_UPS = os.environ.get("RVC_AMD_AMAX_UPS", "1") != "0"
 AMAX_PER_STAGE = 16
+# round 6: noise_convs[i](har) fused into ups[i]'s epilogue (x = ups(x) + noise_convs(har), synthesizers.py:156: one
+# launch writes the stage input once, the same bits); RVC_AMD_FUSED_NOISE=0: the separate accumulating launch (A/B)
+FUSED_NOISE = os.environ.get("RVC_AMD_FUSED_NOISE", "1") != "0"
 
 
 def fold_weight_norm(weight: dict) -> dict:
@@ -197,7 +200,7 @@ class SynthesizerAMD:
         work = torch.empty(B, T, device=dev)
         ops.sine_source(nsff0, sine_noise, har, work, B, T, self.upp, float(self.sr), self.lin_w, self.lin_b)
         nst = len(self.ur)
-        cells = ops.AmaxSlots(AMAX_PER_STAGE * nst + nst + 1, dev) if AMAX else None
+        cells = ops.AmaxSlots(AMAX_PER_STAGE * nst + nst + 1, dev, B) if AMAX else None
         # cells after the stages' own: one per stage for its output xs (published by the last resblock's last c2 when
         # that pair is unfused), one for conv_pre's output -- the upsampling convs' inputs
         out_cell = (lambda k: cells[AMAX_PER_STAGE * nst + k]) if AMAX else (lambda k: None)
@@ -211,14 +214,21 @@ class SynthesizerAMD:
         # channels too (rvc_model.cpp mirrors this cell by cell)
         for i in range(nst):
             up = self.ups[i]
-            y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale, amax_in=x_cell if AMAX_UPS else None)
-            x_cell = None
-            Li = y.shape[-1]
             nc, s, pad = self.noise[i]
             base = AMAX_PER_STAGE * i
             ncell = 1
-            nc(har.view(B, 1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True,
-               amax_out=cells[base] if cells else None)
+            if FUSED_NOISE:  # y = ups(x) + noise_convs(har) in one launch, which publishes y's |max|
+                y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale,
+                       amax_in=x_cell if AMAX_UPS else None, src=(nc, har, s, pad),
+                       amax_out=cells[base] if cells else None)
+                Li = y.shape[-1]
+            else:
+                y = up(x, in_act=ACT_LRELU, in_slope=LRELU_SLOPE, in_scale=scale,
+                       amax_in=x_cell if AMAX_UPS else None)
+                Li = y.shape[-1]
+                nc(har.view(B, 1, L), Lout=Li, stride=s, pad=pad, out=y, accumulate=True,
+                   amax_out=cells[base] if cells else None)
+            x_cell = None
             C = self.chans[i]
             t1 = None  # c1 output of the unfused pairs
             xa = torch.empty(B, C, Li, device=dev)

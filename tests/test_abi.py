@@ -28,7 +28,7 @@ def test_binding_covers_header():
 
 def test_struct_layouts_match_header():
     # sizes of the POD structs as the C compiler lays them out (checked by a tiny host probe below)
-    assert ctypes.sizeof(_lib.Conv1dArgs) == 6 * 8 + 10 * 8 + 12 * 4 + 4 * 4 + 18 * 4 + 8 + 2 * 4 + 2 * 8
+    assert ctypes.sizeof(_lib.Conv1dArgs) == 6 * 8 + 10 * 8 + 12 * 4 + 4 * 4 + 18 * 4 + 8 + 2 * 4 + 2 * 8 + 3 * 8 + 4 * 4 + 2 * 8
     assert ctypes.sizeof(_lib.AttnArgs) == 7 * 8 + 13 * 8 + 4 * 4
 
 

@@ -155,6 +155,26 @@ def test_stream_bit_identical_to_per_clip(models):
     vc.check_errors()
 
 
+def test_stream_host_out_30s_bit_identical_to_per_call(models):
+    """The bench's form of the stream -- 30 s clips, each output copied to pinned host memory on the synthesizer's
+    stream (host_out) -- against vc.pipeline_device per clip (the per-call form the headline parity test runs):
+    every clip's host copy equals the per-call waveform bit for bit."""
+    hub, _, net_g, vc = models
+    xs = clips(2, 30.0, 900)
+    vc.seed = 21
+    host = [torch.empty(30 * 48000 + 48000, dtype=torch.float32).pin_memory() for _ in xs]
+    outs = vc.pipeline_device_stream(hub, net_g, 0, xs, 0, "v2", 0.33, host_out=host)
+    torch.cuda.synchronize()
+    for k, x in enumerate(xs):
+        vc.seed = 21 + k
+        ref = vc.pipeline_device(hub, net_g, 0, x, 0, "v2", 0.33).cpu()
+        n = ref.numel()
+        assert outs[k].numel() == n and n <= host[k].numel()
+        assert torch.equal(host[k][:n], ref), (k, (host[k][:n] - ref).abs().max().item())
+    vc.seed = 0
+    vc.check_errors()
+
+
 def test_batched_stream_bit_identical_to_batch(models):
     """pipeline_device_stream(batch=3) over 5 clips = pipeline_device_batch of groups [0:3], [3:5] (same
     batched front-end launches, seeds self.seed + k)."""
