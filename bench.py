@@ -21,8 +21,10 @@ child process, one rank per GPU); under an external launcher WORLD_SIZE must equ
 
 Prints ONE JSON line on rank 0 (contract in the task statement): metric/value = output
 audio-seconds per wall-second for the whole job, plus "roofline" for the dominant kernel
-family (the f32-MFMA implicit-GEMM conv engine, measured live with HIP events on its stream)
-and "cpu_baseline" (the torch-CPU oracle on a bounded clip, rank 0, N=1 only).
+family (the split-operand MFMA conv engine: conv_x6_kernel + the fused ResBlock pairs; algorithmic FLOPs over the
+device's own kernel stamps of one instrumented per-call pass, torch.profiler, with the HIP-event time beside it),
+its "families" (attention on the f32 MFMA, the BiGRU's us per step against its hand-off floor, and the HBM GB/s of
+LayerNorm / fe0 / STFT / filtfilt), and "cpu_baseline" (the torch-CPU oracle on a bounded clip, rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -86,6 +88,7 @@ class ConvProbe:
         self.orig_64 = ops.conv64
         self.orig_w64 = ops.wino64
         self.rec = []
+        self.aux = []  # (family, algorithmic FLOPs, algorithmic HBM bytes, frames) of the non-conv kernels (families())
 
     def __enter__(self):
         import ctypes
@@ -144,6 +147,49 @@ class ConvProbe:
         self.ops.resblock_pair = wrapped_rb
         self.ops.conv64 = wrapped_64
         self.ops.wino64 = wrapped_w64
+        # the other kernel families of the pass (roofline "families"): algorithmic work per call, timed by the
+        # profiler pass (their device stamps); no events around them
+        ops = self.ops
+        self.saved = {n: getattr(ops, n) for n in ("attention", "layernorm_cf", "fe0_gn_gelu", "bigru64_batched",
+                                                   "stft_mag64")}
+        self.saved_filt = ops.FiltFilt.__call__
+        aux = self.aux
+
+        def attention(q, k, v, o, *, B, H, D, T, **kw):
+            # softmax(Q K^T) V: 4 T^2 D FLOP per head (the reference's dense scores and PV); the relative band (rk, ev:
+            # the TextEncoder) adds 2 * 2 T (2W + 1) D; bytes: q, k, v read and o written once
+            fl = 4.0 * B * H * T * T * D + (4.0 * B * H * T * (2 * kw.get("W", 0) + 1) * D if kw.get("rk") is not None
+                                            else 0.0)
+            aux.append(("attention_d%d" % D, fl, 4.0 * 4 * B * H * D * T, T))
+            return self.saved["attention"](q, k, v, o, B=B, H=H, D=D, T=T, **kw)
+
+        def layernorm_cf(x, res, gamma, beta, out, B, C, T, *a, **kw):
+            aux.append(("layernorm", 0.0, 4.0 * B * C * T * (2 + (res is not None)), T))
+            return self.saved["layernorm_cf"](x, res, gamma, beta, out, B, C, T, *a, **kw)
+
+        def fe0_gn_gelu(wav, w_km, gamma, beta, B, N, C, K, stride, *a, **kw):
+            T = (N - K) // stride + 1
+            # the conv twice (statistics, then apply) over the signal; bytes: the signal (twice) and the output once
+            aux.append(("fe0", 2 * 2.0 * B * C * K * T, 4.0 * B * (2 * N + C * T), T))
+            return self.saved["fe0_gn_gelu"](wav, w_km, gamma, beta, B, N, C, K, stride, *a, **kw)
+
+        def bigru64_batched(gi, whh, bhh, y, gran, err, B, T):
+            aux.append(("bigru", 0.0, 8.0 * B * (1536 + 512) * T, T))
+            return self.saved["bigru64_batched"](gi, whh, bhh, y, gran, err, B, T)
+
+        def stft_mag64(x, win, mag, N, F, nfft, hop):
+            aux.append(("stft", 0.0, 4.0 * N + 8.0 * F * (nfft // 2 + 1), F))
+            return self.saved["stft_mag64"](x, win, mag, N, F, nfft, hop)
+
+        def filt_call(fself, x, tpad, want_f64=False):
+            N = x.numel()
+            aux.append(("filtfilt", 0.0, 4.0 * N + 4.0 * (N + 2 * tpad) + (8.0 * (N + 2 * tpad) if want_f64 else 0), N))
+            return self.saved_filt(fself, x, tpad, want_f64)
+
+        for n, f in (("attention", attention), ("layernorm_cf", layernorm_cf), ("fe0_gn_gelu", fe0_gn_gelu),
+                     ("bigru64_batched", bigru64_batched), ("stft_mag64", stft_mag64)):
+            setattr(ops, n, f)
+        ops.FiltFilt.__call__ = filt_call
         return self
 
     def __exit__(self, *exc):
@@ -151,6 +197,9 @@ class ConvProbe:
         self.ops.resblock_pair = self.orig_rb
         self.ops.conv64 = self.orig_64
         self.ops.wino64 = self.orig_w64
+        for n, f in self.saved.items():
+            setattr(self.ops, n, f)
+        self.ops.FiltFilt.__call__ = self.saved_filt
 
     @staticmethod
     def _bytes(a, k, out):
@@ -205,9 +254,21 @@ def _pass_set(name):
     return 16 if f16 else (7 if sa else np_)
 
 
-def profiler_kernel_times(fn):
+# kernel families beside the split-operand conv engine (the roofline's "families"): name prefix -> family
+FAMILY_KERNELS = (("attn_fwd_kernel<64>", "attention_d64"), ("attn_combine_kernel<64>", "attention_d64"),
+                  ("attn_fwd_kernel<96>", "attention_d96"), ("attn_combine_kernel<96>", "attention_d96"),
+                  ("attn_relv_band_kernel", "attention_d96"), ("bigru", "bigru"), ("layernorm_cf", "layernorm"),
+                  ("fe0_", "fe0"), ("filt_", "filtfilt"), ("stft_mag_kernel", "stft"))
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+# the BiGRU step's hand-off floor: the fastest step measured for this exchange (both directions
+# XCD-local, f32 recurrence, 1.43 us alone) -- the device-coherent granule round trip every step pays
+BIGRU_FLOOR_US = 1.43
+
+
+def profiler_kernel_times(fn, families=None):
     """{pass set: (launches, device ms)} of the split-operand kernels one call of ``fn`` launches, from
-    torch.profiler's device records; None when the profiler is unavailable (or rocprofv3 already traces)."""
+    torch.profiler's device records; None when the profiler is unavailable (or rocprofv3 already traces).
+    ``families`` (a dict) receives {family: [launches, device ms]} of the FAMILY_KERNELS of the same call."""
     if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
         return None
     try:
@@ -219,6 +280,13 @@ def profiler_kernel_times(fn):
         out = {}
         for e in prof.events():
             name = e.name.replace("(anonymous namespace)::", "").replace("void ", "")
+            if families is not None:
+                for pre, fam in FAMILY_KERNELS:
+                    if name.startswith(pre):
+                        g = families.setdefault(fam, [0, 0.0])
+                        g[0] += 1
+                        g[1] += e.time_range.elapsed_us() * 1e-3
+                        break
             if not (name.startswith("conv_x6_kernel<") or name.startswith("resblock_x6_kernel<")):
                 continue
             g = out.setdefault(_pass_set(name), [0, 0.0])
@@ -228,6 +296,46 @@ def profiler_kernel_times(fn):
     except Exception as exc:  # noqa: BLE001 -- a missing tracer leaves the event timing in place
         print(f"bench.py: torch.profiler unavailable ({exc}); roofline from HIP events", file=sys.stderr)
         return None
+
+
+def family_rooflines(aux, fam_ms):
+    """The roofline entries of the kernel families beside the conv engine, from one pass: algorithmic work per family
+    (ConvProbe.aux) over its device kernel time (profiler_kernel_times' families)."""
+    tot = {}
+    for fam, fl, by, T in aux:
+        t = tot.setdefault(fam, [0.0, 0.0, 0, 0])
+        t[0] += fl
+        t[1] += by
+        t[2] += 1
+        t[3] += T
+    out = {}
+    for fam, (fl, by, calls, T) in sorted(tot.items()):
+        if fam not in fam_ms:
+            continue
+        n, ms = fam_ms[fam]
+        e = {"calls": calls, "launches": n, "kernel_ms": round(ms, 4)}
+        if fam.startswith("attention"):
+            tf = fl / (ms * 1e-3) / 1e12
+            e.update(bound="mfma", achieved=round(tf, 2), peak=PEAK_F32_MFMA_TFLOPS, unit="TFLOP/s",
+                     frac=round(tf / PEAK_F32_MFMA_TFLOPS, 4), gflop=round(fl / 1e9, 2),
+                     kernel=("ContentVec MHA 12 x 64 (fairseq.py:355)" if fam == "attention_d64" else
+                             "TextEncoder rel-pos MHA 2 x 96, window 10, + its rel-v band kernel (synthesizers.py:227-251)")
+                     + ": flash attention on the f32 MFMA (v_mfma_f32_16x16x4_f32), split-KV + combine; FLOPs = "
+                       "4 T^2 D per head (+ the relative band)")
+        elif fam == "bigru":
+            us = ms * 1e3 / max(T, 1)
+            e.update(bound="latency", unit="us/step", achieved=round(us, 3), floor=BIGRU_FLOOR_US,
+                     frac=round(BIGRU_FLOOR_US / us, 4), steps=T,
+                     kernel="RMVPE BiGRU recurrence (RMVPE.py:254-260): 16 workgroups per direction, one device-"
+                            "coherent granule hand-off per step; floor = the fastest measured step of this exchange "
+                            "(DESIGN.md §7), frac = floor / achieved")
+        else:
+            gbs = by / (ms * 1e-3) / 1e9
+            e.update(bound="latency (sequential IIR)" if fam == "filtfilt" else "hbm", unit="GB/s",
+                     achieved=round(gbs, 1), peak=HBM_PEAK_GBS, frac=round(gbs / HBM_PEAK_GBS, 4),
+                     algorithmic_mb=round(by / 1e6, 2))
+        out[fam] = e
+    return out
 
 
 def park_gpu(seconds):
@@ -589,8 +697,9 @@ def main():
         timing = "HIP events around each launch (bench.py ConvProbe)"
         # the same pass again under torch.profiler, whose kernel records are the device's own start / end stamps
         # (what rocprofv3's kernel trace reads): the events above add a few us of their own to every launch
+        fam_ms = {}
         prof = profiler_kernel_times(lambda: vc.pipeline_device(hub, net_g, 0, audio_dev, 0, "v2", 0.33, index,
-                                                                args.index_rate, args.f0))
+                                                                args.index_rate, args.f0), fam_ms)
         if prof and sum(v[0] for v in prof.values()) == n:
             ev_ms = {p: g[1] for p, g in groups.items()}
             for p, g in groups.items():
@@ -636,7 +745,9 @@ def main():
                                "note": "the f64 RMVPE's convs (rmvpe64.hip: conv64_kernel with its split-K reduce, and "
                                        "the Winograd F(4x4,3x3) convs at their direct-conv algorithmic FLOPs); peak = "
                                        "the f64 matrix spec, measured_ceiling = what the chip sustains in f64 on real "
-                                       "operands (power-bound, DESIGN.md §4 conv64)"}}
+                                       "operands (power-bound, DESIGN.md §4 conv64)"},
+                # the other kernel families of the same per-call pass, device kernel stamps (torch.profiler)
+                "families": family_rooflines(probe.aux, fam_ms) if fam_ms else None}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()

@@ -135,6 +135,9 @@ void rvc_conv1d_set_probe_event(void* hip_event);
 /* Diagnostic build only (-DRVC_CONV_STAMPS=1, scripts/conv_stamps.py): the split-operand conv engine's per-block
  * phase stamps (s_memtime) go to buf ([bytes / 2048][256] u64); returns -1 in a production build. */
 int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
+/* The same for the fused ResBlock pair (rvc_resblock_pair): per workgroup, per tile phase stamps (scripts/rb_stamps.py);
+ * -1 in a production build. */
+int rvc_resblock_set_stamps(void* buf, int64_t bytes);
 /* The split-operand engine's epilogue form for this thread's launches: 1 = the tile epilogue through LDS (on the
  * 128-wide tiles where it needs no extra LDS), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI (default 0).  Both give the same bits (tests/test_gpu_ops.py);
  * an A/B switch for measurements in one process. */

@@ -33,7 +33,38 @@ struct RbParams {
     int L, K, dil, nmf1, nmf2, accumulate;
     int B;             // clips: tiles are numbered clip-major, tile g = clip g / ntc, time tile g % ntc
     float slope;
+#if RVC_CONV_STAMPS
+    unsigned long long* stamps;  // diagnostic build only: [block][RB_STAMP_W] s_memtime stamps (rvc_resblock_set_stamps)
+    int64_t stamp_blocks;
+#endif
 };
+
+// In-kernel stamps (diagnostic build -DRVC_CONV_STAMPS=1 only; scripts/rb_stamps.py): compute wave 0 and the first
+// loader wave record s_memtime at each tile's phase boundaries into a buffer of their own (never an output), one lane,
+// vector stores.  Per block (RB_STAMP_W words), tile k < RB_STAMP_NT at 8 k + : 0 S0 passed (tile start), 1 c1's last
+// k-step issued, 2 B_T passed (split-fp16: T's |max| agreed), 3 S1 passed (T written), 4 c2's last k-step issued,
+// 5 c2 epilogue issued, 6 loader: tile k+1's loads issued, 7 loader: tile k+1 staged into X; then 248 block start,
+// 249 HW_ID, 250 XCC_ID, 251 tiles, 252 memrealtime at start, 253 compute done.
+#ifndef RVC_CONV_STAMPS
+#define RVC_CONV_STAMPS 0
+#endif
+constexpr int RB_STAMP_W = 256, RB_STAMP_NT = 31;
+#if RVC_CONV_STAMPS
+#define RB_STAMP(slot, val)                                                                       \
+    do {                                                                                           \
+        if (p.stamps && lane == 0 && (int64_t)blockIdx.x < p.stamp_blocks && (slot) < RB_STAMP_W) \
+            p.stamps[(int64_t)blockIdx.x * RB_STAMP_W + (slot)] = (val);                           \
+    } while (0)
+#else
+#define RB_STAMP(slot, val) \
+    do {                    \
+    } while (0)
+#endif
+#define RB_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#if RVC_CONV_STAMPS
+unsigned long long* g_rb_stamps = nullptr;
+int64_t g_rb_stamp_blocks = 0;
+#endif
 
 #ifndef RB_YREG
 #define RB_YREG 1  // accumulate operands loaded at S1 into registers (else in the epilogue)
@@ -103,6 +134,13 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     const int ntiles = p.B * ntc;
     const int my_n = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave == 0) {
+        RB_STAMP(248, RB_NOW());
+        RB_STAMP(249, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));   // HW_ID
+        RB_STAMP(250, (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)));  // XCC_ID
+        RB_STAMP(251, (unsigned long long)my_n);
+        RB_STAMP(252, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 
     if (wave >= 8) {
         // ---------------- loader waves.  Tile k+1's raw x is loaded into registers after S0(k) (while c1
@@ -205,6 +243,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             // unconditional (the last tile reloads itself): every path issues the same loads, which keeps
             // hipcc's vmcnt bookkeeping exact across the loop (a guarded load made it wait vmcnt(0))
             xload(blockIdx.x + (more ? k + 1 : k) * gridDim.x);
+            if (wave == 8 && k < RB_STAMP_NT) RB_STAMP(8 * k + 6, RB_NOW());
             if constexpr (F16) {
                 __syncthreads();  // B_T(k): the compute waves' T max (c1 epilogue)
                 if (more) publish_max((k + 1) & 1);
@@ -212,6 +251,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             __syncthreads();  // S1(k): c1 of tile k done -> X free
             if constexpr (F16) take_scale((k + 1) & 1);
             if (more) xstore(blockIdx.x + (k + 1) * gridDim.x);
+            if (wave == 8 && k < RB_STAMP_NT) RB_STAMP(8 * k + 7, RB_NOW());
         }
         return;
     }
@@ -319,6 +359,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                     yb = p.y + (int64_t)cb * C * L;
                     xres = p.x + (int64_t)cb * C * L;
                     __syncthreads();  // S0(k)
+                    if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k, RB_NOW());
 #pragma unroll
                     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -328,6 +369,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                 else compute(Ts + ch * (TW * NPL * 4), t, NF2, abuf[u]);        // c2 over T
                 if (!two && last_ch) {
                     // ---- c1 epilogue: + bias, lrelu, zero outside [0, L) (c2's padding) -> T (split planes)
+                    if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 1, RB_NOW());
                     float tsc = 1.f;
                     if constexpr (F16) {
                         // T values in place (unscaled), their |max| over the 8 compute waves, T's scale
@@ -354,6 +396,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                         m = wave_max(m);
                         if (lane == 0) tmaxs[wave] = m;
                         __syncthreads();  // B_T(k)
+                        if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 2, RB_NOW());
                         float tm = 0.f;
 #pragma unroll
                         for (int w = 0; w < 8; ++w) tm = fmaxf(tm, tmaxs[w]);
@@ -398,6 +441,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                         }
                     }
                     __syncthreads();  // S1(k): T written; X free for the loaders
+                    if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 3, RB_NOW());
                     if (YREG && p.accumulate) {
 #pragma unroll
                         for (int i = 0; i < FM; ++i)
@@ -412,6 +456,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                     }
                 }
                 if (two && last_ch) {
+                    if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 4, RB_NOW());
                     // ---- c2 epilogue: + bias, + residual (from R) (+ accumulate) -> y
 #pragma unroll
                     for (int i = 0; i < FM; ++i) {
@@ -432,6 +477,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                             }
                         }
                     }
+                    if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 5, RB_NOW());
                 }
             }
             if (++t == K) {  // step the computing k-step: tap, chunk, conv, tile
@@ -444,6 +490,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             }
         }
     }
+    if (wave == 0) RB_STAMP(253, RB_NOW());
 }
 
 template <int C, int NP, bool F16 = false>
@@ -517,6 +564,10 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     p.accumulate = a->accumulate;
     p.slope = a->slope;
     p.B = a->B > 1 ? a->B : 1;
+#if RVC_CONV_STAMPS
+    p.stamps = g_rb_stamps;
+    p.stamp_blocks = g_rb_stamp_blocks;
+#endif
     hipStream_t s = (hipStream_t)stream;
     if (a->C == 32) {
         if (a->passes == RVC_ARITH_F16X3) return launch_rb<32, 3, true>(p, s);
@@ -533,4 +584,18 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     if (a->passes == 6) return launch_rb<64, 6>(p, s);
     if (a->passes == 3) return launch_rb<64, 3>(p, s);
     return launch_rb<64, 1>(p, s);
+}
+
+// Diagnostic build only (-DRVC_CONV_STAMPS=1): the fused pair's per-tile phase stamps go to buf ([bytes / 2048][256]
+// u64, one row per workgroup); returns -1 in a production build (no stamps compiled).
+extern "C" int rvc_resblock_set_stamps(void* buf, int64_t bytes) {
+#if RVC_CONV_STAMPS
+    g_rb_stamps = (unsigned long long*)buf;
+    g_rb_stamp_blocks = buf ? bytes / (8 * RB_STAMP_W) : 0;
+    return 0;
+#else
+    (void)buf;
+    (void)bytes;
+    return -1;
+#endif
 }
