@@ -222,6 +222,15 @@ int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes, rvc_stream
 /* the same, also folding max |o| into a |max| cell per batch element (amax_out as rvc_layernorm_cf_amax; not with the
  * relative band) */
 int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, void* ws, int64_t ws_bytes, rvc_stream_t stream);
+/* Round 6: with amax_in (the |max| cell of q, k and v -- the QKV projection's published cell, one per batch element)
+ * both products run in split-fp16 on the fp16 matrix cores (power-of-2 scaled operands split into 11 + 11 bit fp16
+ * pieces, hH + hL + lH, f32 accumulation: ~2^-22 relative per product, the conv engine's arithmetic); NULL amax_in =
+ * the f32-MFMA kernel.  amax_out as rvc_attention_amax. */
+int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in, unsigned* amax_out, void* ws, int64_t ws_bytes,
+                     rvc_stream_t stream);
+/* This thread's choice for rvc_attention_ex with amax_in: 1 split-fp16, 0 the f32 kernel, -1 RVC_ATTN_F16 (default 1).
+ * A/B and test knob. */
+int rvc_attention_set_f16(int on);
 
 /* ------------------------------------------------------------------ elementwise
  * Memory-bound pieces of Synthesizer.infer (synthesizers.py:446-465).  All

@@ -15,6 +15,8 @@
 // elsewhere).  The matching value term is added by rvc_attn_relv_band afterwards, which
 // needs the per-query softmax max / sum written to ML.
 #include "rvc_common.h"
+#include "x6_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -33,6 +35,7 @@ struct AttnParams {
     int H, W, S, kps;                // heads, rel window, KV splits, keys per split (multiple of 64)
     float scale;
     unsigned* amax_out;  // |max| cell of o (rvc_attention_amax) or null
+    const unsigned* amax_in;  // |max| cell of q, k, v (rvc_attention_ex: the split-fp16 kernel) or null
 };
 
 // Grid (T/64, H, B*S).  The key range of a block is split blockIdx.z % S; with S > 1 the block
@@ -195,6 +198,262 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
     if (p.amax_out && p.S == 1) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
 }
 
+// ---------------------------------------------------------------- split-fp16 attention (round 6)
+// The same flash attention with both products on the fp16 matrix cores (v_mfma_f32_16x16x32_f16, f32 accumulation)
+// in the split-fp16 arithmetic of the conv engine (x6_common.h split2h): every operand is scaled by a power of 2 into
+// fp16's range and split exactly into h + l (11 + 11 significant bits), and each product keeps hH + hL + lH (~2^-22
+// relative).  The scales: q' = q * scale and k, v from the producer's published |max| of the QKV tensor (amax_in, the
+// K = 1 GEMM's cell); the probabilities P in [0, 1] by 2^14 (their small values stay normal).  All undone exactly
+// (powers of 2) before the softmax and in the epilogue.  32 fp16 MACs per MFMA lane-cycle against 1 for the f32 MFMA:
+// at 3 passes the products cost ~1/10 of the f32 kernel's MFMA time.
+// Layouts (conflict-free by the guide's bank rule for ds_read_b128 / ds_write_b128, scripts/attn_banks.py):
+//   Ks [chunk of 32 channels][64 keys][2 planes][4 groups of 8 channels] (uint4): the A operand of S^T = K^T Q';
+//   Vs [D channel rows][2 planes][8 octets of 8 keys] (uint4): the A operand of O^T = V P^T.
+// The S^T fragment rows are assigned to keys so that P^T's C layout IS the next product's B operand: fragment f row
+// m <-> key 32 (f >> 1) + 8 (m >> 2) + 4 (f & 1) + (m & 3), so lane (query, group g) holds keys 32 s + 8 g .. + 7 of
+// key step s -- 8 consecutive keys, as Vs delivers them.
+constexpr int AF_KT = 64;  // keys per tile
+
+__device__ __forceinline__ int af_key(int f, int m) {
+    return 32 * (f >> 1) + 8 * (m >> 2) + 4 * (f & 1) + (m & 3);
+}
+__device__ __forceinline__ int af_ks(int pos, int q, int g) {
+    return pos * 8 + ((4 * q + g) ^ (((pos >> 1) & 1) | (((pos >> 3) & 3) << 1)));
+}
+__device__ __forceinline__ int af_vs(int r, int q, int u) {
+    return r * 16 + 8 * (q ^ (r & 1)) + (u ^ (r & 7));
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
+    constexpr int NC = D / 32;        // 32-channel chunks: k-steps of S^T
+    constexpr int NF = D / 16;        // output channel fragments
+    constexpr int VI = D * 8 / 256;   // V staging items (channel row, key octet) per thread
+    static_assert(D % 32 == 0 && (D * 8) % 256 == 0, "D = 64 or 96");
+    __shared__ uint4 Ks[NC * AF_KT * 8];
+    __shared__ uint4 Vs[D * 16];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = blockIdx.y;
+    const int split = blockIdx.z % p.S, b = blockIdx.z / p.S;
+    const int64_t T = p.T;
+    const int lq = lane & 15, lg = lane >> 4;
+    const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
+    const int64_t qa = q0 + lq;
+    const int64_t kbeg = (int64_t)split * p.kps;
+    const int64_t kend = kbeg + p.kps < T ? kbeg + p.kps : T;
+    const float* Q = p.q + b * p.q_bs + h * p.q_hs;
+    const float* K = p.k + b * p.k_bs + h * p.k_hs;
+    const float* V = p.v + b * p.v_bs + h * p.v_hs;
+
+    // power-of-2 scales from the batch element's |max| cell (max |q|, |k|, |v| of the projection)
+    const float amax = amax_read(p.amax_in + (int64_t)b * RVC_AMAX_SHARDS);
+    const int eq = f16_exp(amax * p.scale), ek = f16_exp(amax), ev = f16_exp(amax);
+    const float sq = ldexpf(1.f, eq), sk = ldexpf(1.f, ek), sv = ldexpf(1.f, ev);
+    const float s_un = ldexpf(1.f, -(eq + ek));
+    const float o_un = ldexpf(1.f, -(ev + 14));
+
+    // Q' as the B operand of every S^T fragment (loop-invariant): chunk c, lane (query lq, group lg) -> channels
+    // 32 c + 8 lg .. + 7
+    uint4 qh[NC], ql[NC];
+    {
+        const int64_t qc = qa < T ? qa : T - 1;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = Q[(int64_t)(32 * c + 8 * lg + e) * p.ldc + qc] * p.scale * sq;
+            uint32_t hw[4], lw[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) split2h_pk(v[2 * e2], v[2 * e2 + 1], hw[e2], lw[e2]);
+            qh[c] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            ql[c] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        }
+    }
+
+    // staging: K item (key sj, group sg) of each chunk -- 8 channel rows, coalesced over the 64 keys of a wave; V item
+    // (channel row, key octet) -- 8 consecutive keys of one row
+    // The loads go through buffer resources over the head's D rows: K's channel row in the scalar offset and the key in
+    // one 32-bit lane offset shared by every K load, V's row and key octet in one lane offset per item and the key in
+    // the immediate -- no 64-bit address per load (those set the register count, not the tiles).  A V key past T reads
+    // the next row (masked at the store) or 0 past the range.  (D ldc < 2^29: checked on the host.)
+    const int sj = tid & 63, sg = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ldc = (int)p.ldc;
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, D * ldc * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, D * ldc * 4, 0x00020000);
+    float kr[NC][8], vr[VI][8];
+    auto gload = [&](int64_t kt) __attribute__((always_inline)) {
+        const int ko = (int)(kt + sj < T ? kt + sj : T - 1) * 4;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                kr[c][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         krs, ko, (32 * c + 8 * sg + e) * ldc * 4, 0));
+#pragma unroll
+        for (int it = 0; it < VI; ++it) {
+            const int idx = tid + 256 * it, row = idx >> 3, u = idx & 7;
+            const int vo = (row * ldc + (int)kt + 8 * u) * 4;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                vr[it][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, vo + 4 * e, 0, 0));
+        }
+    };
+    auto sstore = [&](int64_t kt) __attribute__((always_inline)) {
+        const bool okk = kt + sj < kend;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            uint32_t hw[4], lw[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2)
+                split2h_pk(okk ? kr[c][2 * e2] * sk : 0.f, okk ? kr[c][2 * e2 + 1] * sk : 0.f, hw[e2], lw[e2]);
+            Ks[c * AF_KT * 8 + af_ks(sj, 0, sg)] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            Ks[c * AF_KT * 8 + af_ks(sj, 1, sg)] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        }
+#pragma unroll
+        for (int it = 0; it < VI; ++it) {
+            const int idx = tid + 256 * it, row = idx >> 3, u = idx & 7;
+            uint32_t hw[4], lw[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+                const bool o0 = kt + 8 * u + 2 * e2 < kend, o1 = kt + 8 * u + 2 * e2 + 1 < kend;
+                split2h_pk(o0 ? vr[it][2 * e2] * sv : 0.f, o1 ? vr[it][2 * e2 + 1] * sv : 0.f, hw[e2], lw[e2]);
+            }
+            Vs[af_vs(row, 0, u)] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            Vs[af_vs(row, 1, u)] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        }
+    };
+
+    floatx4 acc_o[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc_o[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+    const float* RK = p.rk ? p.rk + ((int64_t)b * p.H + h) * (2 * p.W + 1) * T : nullptr;
+
+    gload(kbeg);
+    sstore(kbeg);
+    __syncthreads();
+    for (int64_t kt = kbeg; kt < kend; kt += AF_KT) {
+        const bool more = kt + AF_KT < kend;
+        if (more) gload(kt + AF_KT);
+        // S^T fragments: rows = keys af_key(f, .), columns = this wave's 16 queries
+        floatx4 s[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int krow = af_key(f, lq);
+            floatx4 a4 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const uint4 ah = Ks[c * AF_KT * 8 + af_ks(krow, 0, lg)];
+                const uint4 al = Ks[c * AF_KT * 8 + af_ks(krow, 1, lg)];
+                a4 = mfma_f16(ah, qh[c], a4);
+                a4 = mfma_f16(ah, ql[c], a4);
+                a4 = mfma_f16(al, qh[c], a4);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[f][r] = a4[r] * s_un;
+        }
+        // element (f, r) of this lane: key kt + af_key(f, 4 lg + r), query qa
+        if (RK && kt - (q0 + 15) <= p.W && kt + AF_KT - 1 - q0 >= -p.W) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t key = kt + af_key(f, 4 * lg + r);
+                    const int64_t d = key - qa;
+                    const bool in = d >= -p.W && d <= p.W && qa < T && key < T;
+                    const float rv = RK[(in ? d + p.W : 0) * T + (qa < T ? qa : 0)];
+                    s[f][r] += in ? rv : 0.f;
+                }
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (kt + af_key(f, 4 * lg + r) >= kend) s[f][r] = -INFINITY;
+                mloc = fmaxf(mloc, s[f][r]);
+            }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = expf(m_run - m_new);
+        float lsum = 0.f;
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float e = expf(s[f][r] - m_new);
+                s[f][r] = e;
+                lsum += e;
+            }
+        lsum += __shfl_xor(lsum, 16, 64);
+        lsum += __shfl_xor(lsum, 32, 64);
+        l_run = l_run * alpha + lsum;
+        m_run = m_new;
+        // P^T as the B operand of key step st: keys 32 st + 8 lg + i = fragment 2 st (i < 4) / 2 st + 1 (i >= 4)
+        uint4 ph[2], pl[2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            uint32_t hw[4], lw[4];
+            split2h_pk(s[2 * st][0] * 16384.f, s[2 * st][1] * 16384.f, hw[0], lw[0]);
+            split2h_pk(s[2 * st][2] * 16384.f, s[2 * st][3] * 16384.f, hw[1], lw[1]);
+            split2h_pk(s[2 * st + 1][0] * 16384.f, s[2 * st + 1][1] * 16384.f, hw[2], lw[2]);
+            split2h_pk(s[2 * st + 1][2] * 16384.f, s[2 * st + 1][3] * 16384.f, hw[3], lw[3]);
+            ph[st] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            pl[st] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc_o[f] *= alpha;
+#pragma unroll
+        for (int fc = 0; fc < NF; ++fc) {
+            const int row = 16 * fc + lq;
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const uint4 ah = Vs[af_vs(row, 0, 4 * st + lg)];
+                const uint4 al = Vs[af_vs(row, 1, 4 * st + lg)];
+                acc_o[fc] = mfma_f16(ah, ph[st], acc_o[fc]);
+                acc_o[fc] = mfma_f16(ah, pl[st], acc_o[fc]);
+                acc_o[fc] = mfma_f16(al, ph[st], acc_o[fc]);
+            }
+        }
+        __syncthreads();
+        if (more) sstore(kt + AF_KT);
+        __syncthreads();
+    }
+
+    float amx = 0.f;
+    if (qa < T) {
+        const float inv = 1.f / l_run;
+        float* O;
+        int64_t ldo;
+        float* ML = nullptr;
+        if (p.S > 1) {
+            const int64_t bs = (int64_t)b * p.S + split;
+            O = p.ws + (bs * p.H + h) * D * T;
+            ldo = T;
+            ML = p.ws + (int64_t)gridDim.z * p.H * D * T + (bs * p.H + h) * 2 * T;
+        } else {
+            O = p.o + b * p.o_bs + h * p.o_hs;
+            ldo = p.ldc;
+            if (p.ml) ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float o = acc_o[f][r] * o_un * inv;
+                O[(int64_t)(16 * f + lg * 4 + r) * ldo + qa] = o;
+                amx = fmaxf(amx, fabsf(o));
+            }
+        if (ML && lg == 0) {
+            ML[qa] = m_run;
+            ML[T + qa] = l_run;
+        }
+    }
+    if (p.amax_out && p.S == 1) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
+}
+
 // Merge S split-KV partials: o = sum_s o_s * l_s e^(m_s - m) / sum_s l_s e^(m_s - m).  Grid (T/64, H, B),
 // block 256 = 64 queries (coalesced) x 4 channel groups; each thread keeps D/4 channel sums.
 template <int D>
@@ -309,6 +568,19 @@ extern "C" int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes,
 
 extern "C" int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, void* ws, int64_t ws_bytes,
                                   rvc_stream_t stream) {
+    return rvc_attention_ex(a, nullptr, amax_out, ws, ws_bytes, stream);
+}
+
+// per-thread override of the split-fp16 kernel (rvc_attention_set_f16; -1 = RVC_ATTN_F16, default on)
+static thread_local int g_attn_f16 = -1;
+
+extern "C" int rvc_attention_set_f16(int on) {
+    g_attn_f16 = on < 0 ? -1 : (on ? 1 : 0);
+    return RVC_OK;
+}
+
+extern "C" int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in, unsigned* amax_out, void* ws,
+                                int64_t ws_bytes, rvc_stream_t stream) {
     RVC_CHECK_ARG(a && a->q && a->k && a->v && a->o && a->T > 0 && a->H > 0 && a->B > 0, "attention: bad args");
     RVC_CHECK_ARG(!amax_out || !a->rk, "attention: amax_out is not built for the relative band");
     RVC_CHECK_ARG(a->D == 64 || a->D == 96, "attention: head dim %d unsupported (64, 96)", a->D);
@@ -321,6 +593,9 @@ extern "C" int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, vo
     p.q_bs = a->q_bs; p.k_bs = a->k_bs; p.v_bs = a->v_bs; p.o_bs = a->o_bs;
     p.H = a->H; p.W = a->W; p.scale = a->scale;
     p.amax_out = amax_out;
+    p.amax_in = amax_in;
+    static const int f16_env = getenv("RVC_ATTN_F16") ? atoi(getenv("RVC_ATTN_F16")) : 1;
+    const bool f16 = amax_in && (g_attn_f16 >= 0 ? g_attn_f16 : f16_env);
     attn_plan(a, p.S, p.kps);
     p.ws = nullptr;
     if (p.S > 1) {
@@ -330,9 +605,13 @@ extern "C" int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, vo
         p.ws = (float*)ws;
     }
     RVC_CHECK_ARG(a->B * p.S < 65536 && a->H < 65536, "attention: grid too large");
+    RVC_CHECK_ARG(!f16 || (int64_t)a->D * p.ldc < (1ll << 29), "attention: split-fp16 needs D * ldc < 2^29");
     dim3 grid(cdiv(a->T, 64), (unsigned)a->H, (unsigned)(a->B * p.S));
     hipStream_t s = (hipStream_t)stream;
-    if (a->D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
+    if (f16) {
+        if (a->D == 64) hipLaunchKernelGGL(attn_f16_kernel<64>, grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(attn_f16_kernel<96>, grid, dim3(256), 0, s, p);
+    } else if (a->D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(attn_fwd_kernel<96>, grid, dim3(256), 0, s, p);
     RVC_HIP(hipGetLastError());
     if (p.S > 1) {

@@ -55,6 +55,7 @@ struct rvc_ctx {
     bool amax_s2 = true;      // RVC_AMD_AMAX_S2 as ops.py: stride-2 convs with a producer's |max| in split-fp16
     bool fe_amax = true;      // RVC_AMD_FE_AMAX as contentvec.py: the feature extractor's convs through |max| cells
     bool fused_noise = true;  // RVC_AMD_FUSED_NOISE as synth.py: noise_convs fused into the upsampling convs
+    bool attn_f16 = true;     // RVC_AMD_ATTN_F16 as contentvec.py / synth.py: QKV |max| cells, split-fp16 attention
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;

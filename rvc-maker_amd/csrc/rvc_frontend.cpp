@@ -104,9 +104,9 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
     const int nl = out_layer < (int)M.layers.size() ? out_layer : (int)M.layers.size();
     const int nfe = 6;
     unsigned* cells = nullptr;
-    if (c->cv_amax) {
-        cells = reinterpret_cast<unsigned*>(sc.take((int64_t)(2 + 4 * nl + nfe) * RVC_AMAX_SHARDS));
-        RUN(hipMemsetAsync(cells, 0, sizeof(unsigned) * (2 + 4 * nl + nfe) * RVC_AMAX_SHARDS, s) == hipSuccess
+    if (c->cv_amax) {  // (+ one QKV cell per layer: contentvec.py's ATTN_F16)
+        cells = reinterpret_cast<unsigned*>(sc.take((int64_t)(2 + 5 * nl + nfe) * RVC_AMAX_SHARDS));
+        RUN(hipMemsetAsync(cells, 0, sizeof(unsigned) * (2 + 5 * nl + nfe) * RVC_AMAX_SHARDS, s) == hipSuccess
                 ? RVC_OK
                 : RVC_EHIP);
     }
@@ -158,8 +158,10 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
         const CvLayer& Ly = M.layers[li];
         unsigned *c_in = cell(4 * li + 1), *c_at = cell(4 * li + 2), *c_l1 = cell(4 * li + 3),
                  *c_f1 = cell(4 * li + 4), *c_l2 = cell(4 * li + 5);
+        unsigned* c_qkv = c->attn_f16 ? cell(2 + 4 * nl + nfe + li) : nullptr;
         CallOpts oq;
         oq.amax_in = c_in;
+        oq.amax_out = c_qkv;
         RUN(conv(c, M, Ly.qkv, xe, T, qkv, oq, s));
         rvc_attn_args at;
         memset(&at, 0, sizeof(at));
@@ -181,7 +183,7 @@ int cv_one(rvc_ctx* c, ContentVec& M, Scratch& sc, const float* wav, int64_t N, 
             MCHECK(need >= 0, "rvc_contentvec_forward: attention shape H=%lld D=%lld T=%lld unsupported", (long long)H,
                    (long long)D, (long long)T);
             MTRY(ensure_ws(M, need, s));
-            MTRY(rvc_attention_amax(&at, c_at, need ? M.ws : nullptr, need, s));
+            MTRY(rvc_attention_ex(&at, c_qkv, c_at, need ? M.ws : nullptr, need, s));
         }
         CallOpts oo;
         oo.amax_in = c_at;

@@ -87,7 +87,7 @@ constexpr int kAmaxPerStage = 16;
 
 struct Bufs {
     int64_t phone_cf, lin, x, tmp, o, ml, qkv, rk, ffh, stats, znoise, zp, fb0, fb1, h, acts, outacc, xin, gc, har, work,
-        snoise, xpre, amax, reg[2];
+        snoise, xpre, amax, tcell, reg[2];
     std::vector<int64_t> Li;
     int64_t stage_floats = 0, total = 0;
 };
@@ -122,6 +122,7 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
     b.xpre = p.take((int64_t)g.upsample_initial_channel * T);
     // the |max| cells of the ResBlock stages, then one per stage output and one for conv_pre (synth.py generator)
     b.amax = p.take((kAmaxPerStage * 8 + 8 + 1) * RVC_AMAX_SHARDS);
+    b.tcell = p.take((int64_t)S.layers.size() * RVC_AMAX_SHARDS);  // the TextEncoder's QKV |max| cells
     int64_t Lc = T;
     for (size_t i = 0; i < S.ups.size(); ++i) {
         Lc = convT_out_len(S.ups[i], Lc);
@@ -166,9 +167,16 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     }
     MTRY(rvc_textenc_embed(lin, S.emb_pitch, pitch, x, 1, H, T, (float)sqrt((double)H), 0.1f, s));
     const float scale = (float)(1.0 / sqrt((double)kc));
-    for (const Layer& Ly : S.layers) {
+    // QKV |max| cells (synth.py text_encoder): the attention runs split-fp16 from them
+    unsigned* tcells = c->attn_f16 ? reinterpret_cast<unsigned*>(A + bf.tcell) : nullptr;
+    if (tcells) MHIP(hipMemsetAsync(tcells, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * S.layers.size(), s));
+    for (size_t li = 0; li < S.layers.size(); ++li) {
+        const Layer& Ly = S.layers[li];
+        unsigned* c_qkv = tcells ? tcells + RVC_AMAX_SHARDS * li : nullptr;
         CallOpts o;
+        o.amax_out = c_qkv;
         MTRY(conv(c, S, Ly.qkv, x, T, qkv, o, s));
+        o.amax_out = nullptr;
         CallOpts orl;
         orl.B = nh;
         orl.x_bstride = kc * T;
@@ -196,7 +204,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         MCHECK(need >= 0, "rvc_synth_infer: attention shape H=%lld D=%lld T=%lld unsupported", (long long)nh,
                (long long)kc, (long long)T);
         MTRY(ensure_ws(S, need, s));
-        MTRY(rvc_attention(&at, need ? S.ws : nullptr, need, s));
+        MTRY(rvc_attention_ex(&at, c_qkv, nullptr, need ? S.ws : nullptr, need, s));
         MTRY(conv(c, S, Ly.o, ob, T, tmp, o, s));
         MTRY(rvc_layernorm_cf(x, tmp, Ly.ln1g, Ly.ln1b, x, 1, H, T, 1e-5f, s));
         CallOpts f1;
@@ -421,6 +429,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->amax_s2 = env_on("RVC_AMD_AMAX_S2");
     c->fe_amax = env_on("RVC_AMD_FE_AMAX");
     c->fused_noise = env_on("RVC_AMD_FUSED_NOISE");
+    c->attn_f16 = env_on("RVC_AMD_ATTN_F16");
     *out = c;
     return RVC_OK;
 }

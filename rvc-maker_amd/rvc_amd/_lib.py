@@ -150,6 +150,8 @@ SIGNATURES = {
     "rvc_attention_workspace_bytes": [POINTER(AttnArgs)],
     "rvc_attention": [POINTER(AttnArgs), c_void_p, c_int64, c_void_p],
     "rvc_attention_amax": [POINTER(AttnArgs), c_void_p, c_void_p, c_int64, c_void_p],
+    "rvc_attention_ex": [POINTER(AttnArgs), c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    "rvc_attention_set_f16": [c_int],
     "rvc_layernorm_cf_amax": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
                               c_void_p, c_void_p],
     "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,

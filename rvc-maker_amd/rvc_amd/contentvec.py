@@ -31,6 +31,9 @@ CV_AMAX = os.environ.get("RVC_AMD_CV_AMAX", "1") != "0"
 # round 6: the feature extractor's convs publish and read cells too (layer 0's fused GELU output, then each stride-2
 # conv + GELU), so layers 1-6 run split-fp16; RVC_AMD_FE_AMAX=0: 6-pass split-bf16 there (the round-5 form)
 FE_AMAX = os.environ.get("RVC_AMD_FE_AMAX", "1") != "0"
+# round 6: the attention's two products in split-fp16 from the QKV projection's published |max| (RVC_AMD_ATTN_F16=0:
+# the f32-MFMA kernel; synth.py and both native hosts read the same switch)
+ATTN_F16 = os.environ.get("RVC_AMD_ATTN_F16", "1") != "0"
 
 FE_LAYERS = [(512, 10, 5)] + [(512, 3, 2)] * 4 + [(512, 2, 2)] * 2
 
@@ -226,7 +229,9 @@ class ContentVecAMD:
         # 0-5 (round 6): layers 1-6 (stride 2) run split-fp16 from their input's cell (cells 2 + 4 nl + i)
         nl = min(output_layer, len(self.layers))
         nfe = len(FE_LAYERS) - 1
-        cells = ops.AmaxSlots(2 + 4 * nl + nfe, dev, B) if CV_AMAX else None
+        # ... and (round 6) each layer's QKV projection publishes max |q|, |k|, |v| (cells 2 + 4 nl + nfe + i): the
+        # attention runs split-fp16 from it (ops.attention amax_in)
+        cells = ops.AmaxSlots(2 + 5 * nl + nfe, dev, B) if CV_AMAX else None
         cell = (lambda k: cells[k]) if CV_AMAX else (lambda k: None)
         fe_cell = (lambda i: cells[2 + 4 * nl + i]) if CV_AMAX and FE_AMAX else (lambda i: None)
         for i, (c, k, s) in enumerate(FE_LAYERS):
@@ -253,11 +258,12 @@ class ContentVecAMD:
             # layer i reads cell 4 i + 1 (the encoder LayerNorm's, then the previous layer's ln2) and fills 4 i + 2 .. 5
             c_in, c_at, c_l1, c_f1, c_l2 = (cell(4 * i + 1), cell(4 * i + 2), cell(4 * i + 3), cell(4 * i + 4),
                                             cell(4 * i + 5))
-            qkv = L["qkv"](x, amax_in=c_in)
+            c_qkv = cell(2 + 4 * nl + nfe + i) if ATTN_F16 else None
+            qkv = L["qkv"](x, amax_in=c_in, amax_out=c_qkv)
             k, v = (qkv[:, E:], qkv[:, 2 * E:]) if batched else (qkv[E:], qkv[2 * E:])
             ops.attention(qkv, k, v, o, B=B, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
                           o_hs=D * T, scale=D ** -0.5, q_bs=3 * E * T, k_bs=3 * E * T, v_bs=3 * E * T, o_bs=E * T,
-                          amax_out=c_at)
+                          amax_out=c_at, amax_in=c_qkv)
             L["o"](o, out=y, amax_in=c_at)
             ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, E, T, amax_out=c_l1)
             h = L["fc1"](x, out_act=ACT_GELU, amax_in=c_l1, amax_out=c_f1)

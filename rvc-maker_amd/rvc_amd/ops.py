@@ -434,8 +434,10 @@ def resblock_pair(x, y, c1: "Conv", c2: "Conv", dil: int, slope: float, accumula
 
 
 def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_bs=0, k_bs=0, v_bs=0, o_bs=0,
-              rk=None, ev=None, ml=None, W=0, amax_out=None):
-    """Flash attention (rvc_attention); ``amax_out``: a |max| cell (``AmaxSlots``) that receives max |o|."""
+              rk=None, ev=None, ml=None, W=0, amax_out=None, amax_in=None):
+    """Flash attention (rvc_attention_ex); ``amax_out``: a |max| cell (``AmaxSlots``) that receives max |o|;
+    ``amax_in``: the cell holding max |q|, |k|, |v| (the QKV projection's) -- both products then run in split-fp16
+    on the fp16 matrix cores (round 6; ``rvc_attention_set_f16`` / RVC_ATTN_F16=0 keep the f32 kernel)."""
     a = _lib.AttnArgs()
     a.q, a.k, a.v, a.o, a.rk, a.ev, a.ml = _p(q), _p(k), _p(v), _p(o), _p(rk), _p(ev), _p(ml)
     a.B, a.H, a.D, a.T, a.ldc = B, H, D, T, ldc
@@ -447,10 +449,10 @@ def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_b
     if need < 0:
         raise ValueError(f"attention: unsupported shape H={H} D={D} T={T}")
     ws = _workspace(o.device, need, "attn") if need else None
-    if amax_out is not None:
-        check(lib.rvc_attention_amax(ctypes.byref(a), _p(amax_out), _p(ws), need, _stream()), "attention")
-    else:
-        check(lib.rvc_attention(ctypes.byref(a), _p(ws), need, _stream()), "attention")
+    for cell in (amax_in, amax_out):
+        if cell is not None and cell.numel() < B * AMAX_SHARDS:
+            raise ValueError("attention: a |max| cell needs AMAX_SHARDS words per batch element")
+    check(lib.rvc_attention_ex(ctypes.byref(a), _p(amax_in), _p(amax_out), _p(ws), need, _stream()), "attention")
     return o
 
 

@@ -37,6 +37,8 @@ AMAX_PER_STAGE = 16
 # round 6: noise_convs[i](har) fused into ups[i]'s epilogue (x = ups(x) + noise_convs(har), synthesizers.py:156: one
 # launch writes the stage input once, the same bits); RVC_AMD_FUSED_NOISE=0: the separate accumulating launch (A/B)
 FUSED_NOISE = os.environ.get("RVC_AMD_FUSED_NOISE", "1") != "0"
+# round 6: the TextEncoder's rel-pos attention in split-fp16 from the QKV projection's |max| (contentvec.ATTN_F16)
+ATTN_F16 = os.environ.get("RVC_AMD_ATTN_F16", "1") != "0"
 
 
 def fold_weight_norm(weight: dict) -> dict:
@@ -147,15 +149,18 @@ class SynthesizerAMD:
         ml = torch.empty(B, nh, 2, T, device=dev)
         rk = torch.empty(B, nh, 21, T, device=dev)
         scale = 1.0 / math.sqrt(kc)
-        for L in self.layers:
-            qkv = L["qkv"](x)
+        # round 6: each layer's QKV projection publishes max |q|, |k|, |v| and the attention runs split-fp16 from it
+        tcells = ops.AmaxSlots(len(self.layers), dev, B) if ATTN_F16 else None
+        for li, L in enumerate(self.layers):
+            c_qkv = tcells[li] if tcells else None
+            qkv = L["qkv"](x, amax_out=c_qkv)
             for b in range(B):  # Rk of clip b's heads: one K=1 conv over its nh query slices
                 L["relk"](qkv[b] if B > 1 else qkv, B=nh, Lin=T, x_bstride=kc * T, Lout=T, out_scale=scale,
                           out=rk[b])
             qb = qkv.view(B, 3 * H, T)
             ops.attention(qb, qb[:, H:], qb[:, 2 * H:], o, B=B, H=nh, D=kc, T=T, ldc=T, q_hs=kc * T,
                           k_hs=kc * T, v_hs=kc * T, o_hs=kc * T, q_bs=3 * H * T, k_bs=3 * H * T, v_bs=3 * H * T,
-                          o_bs=H * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10)
+                          o_bs=H * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10, amax_in=c_qkv)
             y = L["o"](o, out=tmp)
             ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, H, T)
             h = L["ffn1"](x, pad=(self.ksz - 1) // 2, out_act=ACT_RELU)

@@ -239,3 +239,74 @@ def test_consumer_peak_in_last_ragged_tile(Ci, Co, K, d, L):
     rel, rel32 = rms(y - ref), rms(f32 - ref)
     assert float(rel.max()) < 2.0 ** -18, float(rel.max())
     assert bool((rel <= 8 * rel32 + 1e-6).all()), (float(rel.max()), float(rel32.max()))
+
+
+def _mha_ref64(q, k, v, H, D, T, scale):
+    """softmax(q' k^T) v in f64 per head, q [B][H*D][T] -> [B][H*D][T]."""
+    B = q.shape[0]
+    qh = q.double().view(B, H, D, T).transpose(2, 3) * scale
+    kh = k.double().view(B, H, D, T).transpose(2, 3)
+    vh = v.double().view(B, H, D, T).transpose(2, 3)
+    o = torch.softmax(qh @ kh.transpose(2, 3), -1) @ vh
+    return o.transpose(2, 3).reshape(B, H * D, T)
+
+
+@pytest.mark.parametrize("H,D,T,B", [(12, 64, 333, 1), (12, 64, 1599, 1), (12, 64, 640, 2), (2, 96, 257, 1),
+                                     (2, 96, 3198, 1)])
+def test_attention_split_f16(H, D, T, B):
+    """The split-fp16 attention (rvc_attention_ex with the QKV projection's |max| cell): against torch f64, within 4x
+    the f32-MFMA kernel's own error (+ 1e-6 of the output scale), and its |max| cell exact.  Covers one and several
+    key splits, a ragged last key / query tile and batch."""
+    g = gen(T + H)
+    qkv = torch.randn(B, 3 * H * D, T, generator=g)
+    qkv[:, :, T // 3] *= 8.0  # one loud frame
+    E = H * D
+    cell = ops.AmaxSlots(1, DEV, B)
+    for b in range(B):
+        cell.words[b * ops.AMAX_SHARDS] = int(np.float32(qkv[b].abs().max().item()).view(np.int32))
+    dq = qkv.to(DEV)
+    ref = _mha_ref64(qkv[:, :E], qkv[:, E:2 * E], qkv[:, 2 * E:], H, D, T, D ** -0.5)
+    outs = {}
+    for name, cin in (("f32", None), ("f16", cell[0])):
+        o = torch.empty(B, E, T, device=DEV)
+        oc = ops.AmaxSlots(1, DEV, B)
+        ops.attention(dq, dq[:, E:], dq[:, 2 * E:], o, B=B, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
+                      o_hs=D * T, scale=D ** -0.5, q_bs=3 * E * T, k_bs=3 * E * T, v_bs=3 * E * T, o_bs=E * T,
+                      amax_in=cin, amax_out=oc[0])
+        torch.cuda.synchronize()
+        assert_cell(oc[0], o, B)
+        outs[name] = o.cpu().double()
+    e32 = (outs["f32"] - ref).abs().max().item()
+    e16 = (outs["f16"] - ref).abs().max().item()
+    assert e16 <= 4 * e32 + 1e-6 * ref.abs().max().item(), (e16, e32)
+    assert not torch.equal(outs["f16"], outs["f32"])  # the split-fp16 kernel ran
+
+
+def test_attention_split_f16_relpos_band():
+    """The TextEncoder's rel-pos MHA (synthesizers.py:227-251) in split-fp16 vs the oracle's restatement."""
+    from oracle import synth as osy
+    H, D, T = 2, 96, 300
+    C = H * D
+    W = {}
+    g = gen(30)
+    x = torch.randn(1, C, T, generator=g)
+    for n in ("q", "k", "v", "o"):
+        W[f"a.conv_{n}.weight"] = torch.randn(C, C, 1, generator=g) / math.sqrt(C)
+        W[f"a.conv_{n}.bias"] = torch.randn(C, generator=g) * 0.1
+    W["a.emb_rel_k"] = torch.randn(1, 21, D, generator=g) * D ** -0.5
+    W["a.emb_rel_v"] = torch.randn(1, 21, D, generator=g) * D ** -0.5
+    ref = osy._mha(W, "a.", x, torch.ones(1, 1, T, T), H)[0]
+    wqkv = torch.cat([W["a.conv_q.weight"], W["a.conv_k.weight"], W["a.conv_v.weight"]], 0)
+    bqkv = torch.cat([W["a.conv_q.bias"], W["a.conv_k.bias"], W["a.conv_v.bias"]], 0)
+    cell = ops.AmaxSlots(1, DEV)
+    qkv = ops.Conv(wqkv, bqkv)(x[0].to(DEV), amax_out=cell[0])
+    scale = 1 / math.sqrt(D)
+    rk = ops.Conv(W["a.emb_rel_k"][0].unsqueeze(-1), None)(qkv, B=H, Lin=T, x_bstride=D * T, Lout=T, out_scale=scale)
+    o = torch.empty(C, T, device=DEV)
+    ml = torch.empty(H, 2, T, device=DEV)
+    ops.attention(qkv, qkv[C:], qkv[2 * C:], o, B=1, H=H, D=D, T=T, ldc=T, q_hs=D * T, k_hs=D * T, v_hs=D * T,
+                  o_hs=D * T, scale=scale, rk=rk, ev=W["a.emb_rel_v"][0].contiguous().to(DEV), ml=ml, W=10,
+                  amax_in=cell[0])
+    y = ops.Conv(W["a.conv_o.weight"], W["a.conv_o.bias"])(o).cpu()
+    err = (y - ref).abs().max().item()
+    assert err <= 1e-4 * max(1.0, ref.abs().max().item()), err
