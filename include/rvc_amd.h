@@ -111,9 +111,10 @@ typedef struct rvc_conv1d_args {
        sum_k src_w[k][m] * src_x[b][t * src_stride - src_pad + k] + src_b[m] (zero outside [0, src_len)), after the
        residual and accumulate operands -- a 1-input-channel conv of src_K taps over a [B][src_len] signal (batch
        stride src_bstride, 0 = src_len; src_w KM-packed [src_K][Co] as a Ci = 1 conv weight, src_b [Co] or NULL).
-       The NSF generator's x = ups(x) + noise_convs(har) (synthesizers.py:156) in the upsampling conv's epilogue:
-       no separate launch reading and rewriting the stage output.  The k-sum is an fmaf chain in tap order from 0,
-       then + src_b, so it equals the separate 1-channel conv with accumulate. */
+       The NSF generator's x = ups(x) + noise_convs(har) (synthesizers.py:156) in the upsampling conv's call: a
+       read-modify-write pass right after the conv (a direct kernel, HBM-bound, instead of the 1-channel conv as an
+       implicit GEMM K deep); amax_out then receives the final values' |max|.  The k-sum is an fmaf chain in tap
+       order from 0, then + src_b, so it equals the separate 1-channel conv on the f32 engine with accumulate. */
     const float* src_x;
     const float* src_w;
     const float* src_b;
@@ -138,6 +139,10 @@ int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
 /* The same for the fused ResBlock pair (rvc_resblock_pair): per workgroup, per tile phase stamps (scripts/rb_stamps.py);
  * -1 in a production build. */
 int rvc_resblock_set_stamps(void* buf, int64_t bytes);
+/* The fused pair's output path for this thread's launches (round 6): 1 = split-fp16 pairs at C <= 64 write c2's results
+ * into LDS (over the tile's residual rows) and the loader waves store them during the next tile (the compute waves go
+ * straight on), 0 = the compute waves' own global stores, -1 = RVC_RB_YLDS (default 1).  Same bits either way. */
+int rvc_resblock_set_ylds(int on);
 /* The split-operand engine's epilogue form for this thread's launches: 1 = the tile epilogue through LDS (on the
  * 128-wide tiles where it needs no extra LDS), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI (default 0).  Both give the same bits (tests/test_gpu_ops.py);
  * an A/B switch for measurements in one process. */

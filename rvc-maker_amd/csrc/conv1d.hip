@@ -54,12 +54,6 @@ struct ConvParams {
     unsigned* amax_out;       // or null: max |y| over the stored values (atomic max of the f32 bits)
     int stagger;              // x6: the first round of blocks starts spread over this many shader cycles (0 = off)
     int stagger_blocks;       // ... the blocks of that round (one per CU)
-    // fused 1-channel source conv (rvc_conv1d_args.src_*): y += conv(src_x, src_w)[m][t] + src_b[m] in the epilogue
-    const float* src_x;
-    const float* src_w;  // KM [src_K][Co]
-    const float* src_b;
-    int src_K, src_stride, src_pad;
-    int64_t src_len, src_bstride;
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
@@ -85,21 +79,6 @@ __device__ __forceinline__ int out_pos(const ConvParams& p, int64_t n, int phase
     return t;
 }
 
-// The fused source conv of one output (m, t): sum_k src_w[k][m] * src[t * stride - pad + k] (zero outside the signal)
-// as an fmaf chain in tap order from 0, then + src_b[m] -- the k order and roundings of the 1-input-channel conv on the
-// f32 MFMA engine (v_mfma_f32_16x16x4_f32 is an exact fmaf chain), which this replaces (the NSF generator's
-// noise_convs, synthesizers.py:156: x = ups(x) + noise_convs(har)).
-__device__ __forceinline__ float src_term(const ConvParams& p, const float* sx, int64_t m, int t) {
-    const int64_t q0 = (int64_t)t * p.src_stride - p.src_pad;
-    float s = 0.f;
-    for (int k = 0; k < p.src_K; ++k) {
-        const int64_t q = q0 + k;
-        const float xv = (q >= 0 && q < p.src_len) ? sx[q] : 0.f;
-        s = fmaf(p.src_w[(int64_t)k * p.Co + m], xv, s);
-    }
-    return s + (p.src_b ? p.src_b[m] : 0.f);
-}
-
 // Branch-free epilogue for one element: every load is issued unconditionally from a clamped
 // address (a per-element guarded load makes hipcc branch and wait vmcnt(0) per element).
 // returns the value stored (0 when nothing is stored: a border cell stores 0, a column past the end nothing)
@@ -113,7 +92,6 @@ __device__ __forceinline__ float epilogue_store(const ConvParams& p, float acc, 
     if (p.res) v += p.res[b * p.res_bstride + o];
     float* yb = p.y + b * p.y_bstride;
     if (p.accumulate) v += yb[o];
-    if (p.src_x && ok) v += src_term(p, p.src_x + b * p.src_bstride, m, t);
     if (ok) yb[o] = v;
     else if (t <= -2) yb[m * p.Lout + (-t - 2)] = 0.f;  // 2-D border cell
     return ok ? v : 0.f;
@@ -202,44 +180,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) av[0][j][r] += yb[mrow[r] * Lo + (tcol[j] >= 0 ? tcol[j] : 0)];
-        }
-        if (p.src_x) {
-            // the fused source conv (src_term's chain): taps outer, the fragment's 4 rows x FN columns as running sums;
-            // each step's loads (FN signal samples shared by the 4 rows, 4 weights shared by the columns) issued together
-            const float* sx = p.src_x + b * p.src_bstride;
-            int64_t q0[FN];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) q0[j] = (int64_t)(tcol[j] >= 0 ? tcol[j] : 0) * p.src_stride - p.src_pad;
-            float ns[FN][4];
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) ns[j][r] = 0.f;
-            const int64_t len = p.src_len;
-#pragma unroll 2
-            for (int k = 0; k < p.src_K; ++k) {
-                float xv[FN], wv[4];
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    const int64_t q = q0[j] + k;
-                    xv[j] = sx[q < 0 ? 0 : (q >= len ? len - 1 : q)];
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) wv[r] = p.src_w[(int64_t)k * p.Co + mrow[r]];
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    const int64_t q = q0[j] + k;
-                    const float x = (q >= 0 && q < len) ? xv[j] : 0.f;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) ns[j][r] = fmaf(wv[r], x, ns[j][r]);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float sb = p.src_b ? p.src_b[mrow[r]] : 0.f;
-#pragma unroll
-                for (int j = 0; j < FN; ++j) av[0][j][r] += ns[j][r] + sb;
-            }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -1196,6 +1136,69 @@ __global__ void conv_splitk_reduce(ConvParams p) {
     if (p.amax_out) amax_publish(p.amax_out + (int64_t)(bp / p.nphase) * RVC_AMAX_SHARDS, fabsf(v));
 }
 
+// The source-conv pass of a call with src_x (rvc_conv1d_args.src_*; the NSF generator's x = ups(x) + noise_convs(har),
+// synthesizers.py:156): y[b][m][t] += sum_k src_w[k][m] * src[b][t * stride - pad + k] + src_b[m], the k-sum an fmaf chain
+// in tap order from 0 -- the k order and roundings of that 1-input-channel conv on the f32 MFMA engine (whose
+// v_mfma_f32_16x16x4_f32 is an exact fmaf chain) with accumulate, i.e. the same bits as the separate launch it replaces,
+// as one HBM-bound read-modify-write of y (the engine's 1-channel conv was an implicit GEMM only K deep: 79-164 us per
+// generator stage for 20-50 us of bytes).  A block takes SRC_T positions (lanes along t: coalesced y) x SRC_M channels;
+// the signal span of its positions is staged in LDS once, the weights are wave-uniform (scalar loads).  Round 6 first
+// fused this term into the conv epilogue: the extra live registers took the 128 x 256 tile's spills from 31 to 154 VGPRs
+// in every instantiation (the epilogue is compiled into each), so it is a pass of its own.  It publishes amax_out (the
+// conv itself then publishes nothing: its values are not the final ones).
+struct SrcParams {
+    float* y;
+    const float* x;
+    const float* w;  // KM [K][Co]
+    const float* b;
+    unsigned* amax_out;
+    int64_t Co, Lout, len, xbs, ybs;
+    int K, stride, pad, span;
+};
+constexpr int SRC_T = 256, SRC_M = 16;
+
+__global__ __launch_bounds__(SRC_T) void src_add_kernel(SrcParams p) {
+    extern __shared__ float sx[];  // [span] = (SRC_T - 1) * stride + K signal samples of the block's positions
+    const int b = blockIdx.z;
+    const int64_t t0 = (int64_t)blockIdx.x * SRC_T;
+    const int64_t q0 = t0 * p.stride - p.pad;
+    const float* xb = p.x + b * p.xbs;
+    for (int i = threadIdx.x; i < p.span; i += SRC_T) {
+        const int64_t q = q0 + i;
+        sx[i] = (q >= 0 && q < p.len) ? xb[q] : 0.f;
+    }
+    __syncthreads();
+    const int64_t t = t0 + threadIdx.x;
+    const bool ok = t < p.Lout;
+    const int m0 = blockIdx.y * SRC_M;
+    const int nm = p.Co - m0 < SRC_M ? (int)(p.Co - m0) : SRC_M;  // block-uniform
+    const float* xw = sx + threadIdx.x * p.stride;
+    float* yb = p.y + b * p.ybs + (ok ? t : 0);
+    // taps outer (one LDS read per tap, shared by the block's channels), one fmaf chain per channel in tap order
+    float acc[SRC_M];
+#pragma unroll
+    for (int mi = 0; mi < SRC_M; ++mi) acc[mi] = 0.f;
+    for (int k = 0; k < p.K; ++k) {
+        const float xv = xw[k];
+        const float* wk = p.w + (int64_t)k * p.Co + m0;  // wave-uniform: scalar loads
+#pragma unroll
+        for (int mi = 0; mi < SRC_M; ++mi) acc[mi] = fmaf(wk[mi < nm ? mi : 0], xv, acc[mi]);
+    }
+    float amx = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < SRC_M; ++mi) {
+        if (mi < nm) {
+            const int m = m0 + mi;
+            const float v = (acc[mi] + (p.b ? p.b[m] : 0.f)) + yb[(int64_t)m * p.Lout];
+            if (ok) {
+                yb[(int64_t)m * p.Lout] = v;
+                amx = fmaxf(amx, fabsf(v));
+            }
+        }
+    }
+    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
+}
+
 struct Cfg {
     int FM, FN, WM, WN;
     bool x6;
@@ -1280,14 +1283,6 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.f16_fast = g_f16_fast >= 0 ? g_f16_fast : f16fast;
     p.stagger = 0;
     p.stagger_blocks = 0;
-    p.src_x = a->src_x;
-    p.src_w = a->src_w;
-    p.src_b = a->src_b;
-    p.src_K = a->src_K;
-    p.src_stride = a->src_stride;
-    p.src_pad = a->src_pad;
-    p.src_len = a->src_len;
-    p.src_bstride = a->src_bstride ? a->src_bstride : a->src_len;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -1386,6 +1381,8 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
                                 a->src_len > 0 && a->src_bstride >= 0 && !a->wrap),
                   "conv1d: bad fused source conv (src_K=%d src_stride=%d src_pad=%d src_len=%lld)", a->src_K,
                   a->src_stride, a->src_pad, (long long)a->src_len);
+    RVC_CHECK_ARG(!a->src_x || ((int64_t)255 * a->src_stride + a->src_K) * 4 <= 64 * 1024,
+                  "conv1d: source conv span too large (stride %d, K %d)", a->src_stride, a->src_K);
     if (a->ntoff) {
         RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
         for (int i = 0; i < a->K; ++i) RVC_CHECK_ARG(a->toff[i] >= 0, "conv1d: negative tap offset");
@@ -1451,7 +1448,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         const int tepi = g_tile_epi >= 0 ? g_tile_epi : tepi_env;
         const size_t tile_bytes = (size_t)BM * (BN + 4) * 4;
         const bool plain = a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&
-                           BN <= 128 && !a->src_x;
+                           BN <= 128;
         p.tile_epi = !(tepi && plain) ? 0 : tile_bytes <= lds ? 1 : (cfg.WM % 2 == 0 && tile_bytes / 2 <= lds) ? 2 : 0;
         grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
@@ -1700,6 +1697,7 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
         p.ws = (float*)ws;
     }
     hipStream_t s = (hipStream_t)stream;
+    if (a->src_x) p.amax_out = nullptr;  // the source pass publishes the final values' |max|
     hipError_t e;
     if (cfg.x6) {
         if (cfg.WM == 4 && cfg.FN == 8) e = launch_x6<2, 8, 4, 2>(p, grid, lds, s);
@@ -1723,6 +1721,26 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     if (p.ksplit > 1) {
         hipLaunchKernelGGL(conv_splitk_reduce, dim3(cdiv(p.ncols, 256), (unsigned)p.Co, (unsigned)(p.B * p.nphase)),
                            dim3(256), 0, s, p);
+        RVC_HIP(hipGetLastError());
+    }
+    if (a->src_x) {
+        SrcParams q;
+        q.y = a->y;
+        q.x = a->src_x;
+        q.w = a->src_w;
+        q.b = a->src_b;
+        q.amax_out = a->amax_out;
+        q.Co = a->Co;
+        q.Lout = a->Lout;
+        q.len = a->src_len;
+        q.xbs = a->src_bstride ? a->src_bstride : a->src_len;
+        q.ybs = p.y_bstride;
+        q.K = a->src_K;
+        q.stride = a->src_stride;
+        q.pad = a->src_pad;
+        q.span = (SRC_T - 1) * a->src_stride + a->src_K;
+        hipLaunchKernelGGL(src_add_kernel, dim3(cdiv(a->Lout, SRC_T), cdiv(a->Co, SRC_M), (unsigned)a->B), dim3(SRC_T),
+                           (size_t)q.span * 4, s, q);
         RVC_HIP(hipGetLastError());
     }
     return RVC_OK;

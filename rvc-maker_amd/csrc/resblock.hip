@@ -20,6 +20,7 @@
 // two-launch form.
 #include "rvc_common.h"
 #include "x6_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -33,6 +34,7 @@ struct RbParams {
     int L, K, dil, nmf1, nmf2, accumulate;
     int B;             // clips: tiles are numbered clip-major, tile g = clip g / ntc, time tile g % ntc
     float slope;
+    int ylds;          // split-fp16 at C <= 64: c2's outputs go through R in LDS, the loader waves store them (RB_YLDS)
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][RB_STAMP_W] s_memtime stamps (rvc_resblock_set_stamps)
     int64_t stamp_blocks;
@@ -61,6 +63,7 @@ constexpr int RB_STAMP_W = 256, RB_STAMP_NT = 31;
     } while (0)
 #endif
 #define RB_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
+static thread_local int g_rb_ylds = -1;  // rvc_resblock_set_ylds (-1 = RVC_RB_YLDS, default on)
 #if RVC_CONV_STAMPS
 unsigned long long* g_rb_stamps = nullptr;
 int64_t g_rb_stamp_blocks = 0;
@@ -235,9 +238,40 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             __syncthreads();  // B_pre: tile 0's x max published
             take_scale(0);
         }
+        // YLDS: tile k's finished outputs sit in R (the compute waves' c2 epilogue wrote them in place of the residual
+        // rows) until S0(k + 1); each loader thread stores exactly the R elements its own items cover and then writes
+        // its next residual values to those same elements (no hazard between threads), rows coalesced over the lanes
+        auto ystore = [&](int tile) __attribute__((always_inline)) {
+            if constexpr (G::RLDS && F16) {
+                const int cb = tile / ntc;
+                const int n0 = (tile - cb * ntc) * N;
+                float* yb = p.y + (int64_t)cb * C * L;
+                // (not unrolled over the items: unrolled, hipcc batched every item's LDS reads and store addresses and
+                // the loader registers set the kernel's count -- 51 spilled VGPRs at C = 64)
+#pragma unroll 1
+                for (int it = 0; it < G::NI; ++it) {
+                    if (ltid + 256 * it < nitems) {
+                        int ch, g8, pos;
+                        item(it, ch, g8, pos);
+                        const int rc = pos - H;
+                        if (rc >= 0 && rc < N && n0 + rc < L) {
+                            const int row0 = ch * 32 + g8 * 8;
+                            float v[8];
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) v[e] = Rs[(row0 + e) * RSTR + rc];
+                            float* dst = yb + (int64_t)row0 * L + n0 + rc;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) dst[(int64_t)e * L] = v[e];
+                        }
+                    }
+                }
+            }
+        };
+        const bool ylds = G::RLDS && F16 && p.ylds;  // block-uniform
         if (my_n > 0) xstore(blockIdx.x);
         for (int k = 0; k < my_n; ++k) {
-            __syncthreads();  // S0(k): X(k) staged; R free
+            __syncthreads();  // S0(k): X(k) staged; R free (YLDS: R holds tile k - 1's outputs)
+            if (ylds && k > 0) ystore(blockIdx.x + (k - 1) * gridDim.x);
             rstore();         // R(k) from the registers still holding tile k
             const bool more = k + 1 < my_n;
             // unconditional (the last tile reloads itself): every path issues the same loads, which keeps
@@ -252,6 +286,10 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             if constexpr (F16) take_scale((k + 1) & 1);
             if (more) xstore(blockIdx.x + (k + 1) * gridDim.x);
             if (wave == 8 && k < RB_STAMP_NT) RB_STAMP(8 * k + 7, RB_NOW());
+        }
+        if (ylds) {
+            __syncthreads();  // S_end: the last tile's outputs in R
+            if (my_n > 0) ystore(blockIdx.x + (my_n - 1) * gridDim.x);
         }
         return;
     }
@@ -339,6 +377,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     const float* rs1 = reinterpret_cast<const float*>(p.w1x + (int64_t)K * NCH * p.nmf1 * 3 * 64);
     const float* rs2 = reinterpret_cast<const float*>(p.w2x + (int64_t)K * NCH * p.nmf2 * 3 * 64);
     float t_rs = 1.f;
+    const bool ylds_c = G::RLDS && F16 && p.ylds;  // block-uniform
     if constexpr (F16) __syncthreads();  // B_pre
     // One loop over the block's k-steps (tile k: c1 steps [k SPT, k SPT + SPH), c2 steps after), unrolled by
     // the ring size so every ring slot index is a compile-time constant; the tile / phase seams (barriers,
@@ -472,7 +511,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                                     if constexpr (G::RLDS) v = v + Rs[(m0 + r) * RSTR + col];
                                     else v = v + xres[(int64_t)(m0 + r) * L + q];
                                     if (p.accumulate) v += YREG ? yold[i][j][r] : yb[(int64_t)(m0 + r) * L + q];
-                                    yb[(int64_t)(m0 + r) * L + q] = v;
+                                    if (G::RLDS && F16 && ylds_c) Rs[(m0 + r) * RSTR + col] = v;  // the loaders store it
+                                    else yb[(int64_t)(m0 + r) * L + q] = v;
                                 }
                             }
                         }
@@ -490,6 +530,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             }
         }
     }
+    if (ylds_c) __syncthreads();  // S_end: the last tile's outputs are in R for the loader waves
     if (wave == 0) RB_STAMP(253, RB_NOW());
 }
 
@@ -564,6 +605,9 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     p.accumulate = a->accumulate;
     p.slope = a->slope;
     p.B = a->B > 1 ? a->B : 1;
+    // the outputs through LDS (split-fp16 at C <= 64; RVC_RB_YLDS=0: the compute waves' own global stores, A/B switch)
+    static const int ylds = getenv("RVC_RB_YLDS") ? atoi(getenv("RVC_RB_YLDS")) : 1;
+    p.ylds = g_rb_ylds >= 0 ? g_rb_ylds : ylds;
 #if RVC_CONV_STAMPS
     p.stamps = g_rb_stamps;
     p.stamp_blocks = g_rb_stamp_blocks;
@@ -584,6 +628,11 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     if (a->passes == 6) return launch_rb<64, 6>(p, s);
     if (a->passes == 3) return launch_rb<64, 3>(p, s);
     return launch_rb<64, 1>(p, s);
+}
+
+extern "C" int rvc_resblock_set_ylds(int on) {
+    g_rb_ylds = on < 0 ? -1 : (on ? 1 : 0);
+    return RVC_OK;
 }
 
 // Diagnostic build only (-DRVC_CONV_STAMPS=1): the fused pair's per-tile phase stamps go to buf ([bytes / 2048][256]

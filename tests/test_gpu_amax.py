@@ -168,10 +168,10 @@ def test_amax_fe0(B, N):
 @pytest.mark.parametrize("u,k,ci,co,L,B", [(12, 24, 64, 32, 300, 1), (10, 20, 256, 128, 200, 2), (2, 4, 64, 32, 2001, 1)])
 @pytest.mark.parametrize("target", [-1, 1 << 20])
 def test_fused_source_conv_bit_identical(u, k, ci, co, L, B, target):
-    """ups(x) + noise_convs(har) in one launch (rvc_conv1d_args.src_*, synthesizers.py:156) equals the upsampling
-    conv followed by the separate 1-channel conv on the f32 engine with accumulate -- bit for bit (the fused term
-    is that conv's fmaf chain) -- with and without split-K (its reduce adds the term), and its published |max| is
-    max |y|.  Also against torch's fp32 ConvTranspose1d + Conv1d."""
+    """ups(x) + noise_convs(har) in one call (rvc_conv1d_args.src_*, synthesizers.py:156) equals the upsampling
+    conv followed by the separate 1-channel conv on the f32 engine with accumulate -- bit for bit (the source pass
+    is that conv's fmaf chain) -- with and without split-K, and its published |max| is max |y| of the final values.
+    Also against torch's fp32 ConvTranspose1d + Conv1d."""
     g = gen(u * k + B)
     x = torch.randn(B, ci, L, generator=g)
     w = torch.randn(ci, co, k, generator=g) / math.sqrt(ci * k / u)

@@ -118,3 +118,32 @@ def test_fused_pair_f16x3(C, K, d, scale):
     assert (y.cpu() - r).abs().max().item() <= tol
     assert (ref2.cpu() - r).abs().max().item() <= tol
     assert (yb.cpu() - (r + acc0.cpu())).abs().max().item() <= tol + 2e-6 * acc0.abs().max().item()
+
+
+@pytest.mark.parametrize("C", [32, 64])
+@pytest.mark.parametrize("K,d", [(3, 1), (7, 3), (11, 5)])
+@pytest.mark.parametrize("L,B", [(5003, 1), (241, 1), (16, 1), (3001, 3)])
+def test_fused_pair_outputs_through_lds_bit_identical(C, K, d, L, B):
+    """Round 6: the split-fp16 pair's outputs go through LDS (over the tile's residual rows) and the loader waves store
+    them during the next tile (rvc_resblock_set_ylds).  Same bits as the compute waves' own stores -- plain and
+    accumulating, ragged last tile, fewer tiles than workgroups, batched clips."""
+    w, c1, c2 = make_pair(C, K, seed=C + K + d + L)
+    g = torch.Generator().manual_seed(L + B)
+    x = torch.randn(B, C, L, generator=g).to(DEV)
+    acc0 = torch.randn(B, C, L, generator=g).to(DEV)
+    lib = ops._lib.load()
+    outs = []
+    for on in (0, 1):
+        lib.rvc_resblock_set_ylds(on)
+        try:
+            with ops.precision("f16x3"):
+                y = torch.full_like(x, float("nan"))
+                ops.resblock_pair(x if B > 1 else x[0], y if B > 1 else y[0], c1, c2, d, 0.1)
+                ya = acc0.clone()
+                ops.resblock_pair(x if B > 1 else x[0], ya if B > 1 else ya[0], c1, c2, d, 0.1, accumulate=True)
+            torch.cuda.synchronize()
+            outs.append((y.cpu(), ya.cpu()))
+        finally:
+            lib.rvc_resblock_set_ylds(-1)
+    assert torch.equal(outs[0][0], outs[1][0]) and not torch.isnan(outs[1][0]).any()
+    assert torch.equal(outs[0][1], outs[1][1])
