@@ -1158,11 +1158,21 @@ struct SrcParams {
 constexpr int SRC_T = 256, SRC_M = 16;
 
 __global__ __launch_bounds__(SRC_T) void src_add_kernel(SrcParams p) {
-    extern __shared__ float sx[];  // [span] = (SRC_T - 1) * stride + K signal samples of the block's positions
+    // LDS: the block's channels' weights [K][SRC_M] (16-B aligned rows: broadcast ds_read_b128), then the signal span
+    // (SRC_T - 1) * stride + K of its positions
+    extern __shared__ __attribute__((aligned(16))) float smem_src[];
+    float* sw = smem_src;
+    float* sx = smem_src + p.K * SRC_M;
     const int b = blockIdx.z;
     const int64_t t0 = (int64_t)blockIdx.x * SRC_T;
     const int64_t q0 = t0 * p.stride - p.pad;
     const float* xb = p.x + b * p.xbs;
+    const int m0 = blockIdx.y * SRC_M;
+    const int nm = p.Co - m0 < SRC_M ? (int)(p.Co - m0) : SRC_M;  // block-uniform
+    for (int i = threadIdx.x; i < p.K * SRC_M; i += SRC_T) {
+        const int k = i / SRC_M, mi = i - k * SRC_M;
+        sw[i] = mi < nm ? p.w[(int64_t)k * p.Co + m0 + mi] : 0.f;
+    }
     for (int i = threadIdx.x; i < p.span; i += SRC_T) {
         const int64_t q = q0 + i;
         sx[i] = (q >= 0 && q < p.len) ? xb[q] : 0.f;
@@ -1170,19 +1180,24 @@ __global__ __launch_bounds__(SRC_T) void src_add_kernel(SrcParams p) {
     __syncthreads();
     const int64_t t = t0 + threadIdx.x;
     const bool ok = t < p.Lout;
-    const int m0 = blockIdx.y * SRC_M;
-    const int nm = p.Co - m0 < SRC_M ? (int)(p.Co - m0) : SRC_M;  // block-uniform
     const float* xw = sx + threadIdx.x * p.stride;
     float* yb = p.y + b * p.ybs + (ok ? t : 0);
-    // taps outer (one LDS read per tap, shared by the block's channels), one fmaf chain per channel in tap order
+    // taps outer (one signal read per tap, shared by the block's channels; the 16 weights one broadcast), one fmaf chain
+    // per channel in tap order
     float acc[SRC_M];
 #pragma unroll
     for (int mi = 0; mi < SRC_M; ++mi) acc[mi] = 0.f;
     for (int k = 0; k < p.K; ++k) {
         const float xv = xw[k];
-        const float* wk = p.w + (int64_t)k * p.Co + m0;  // wave-uniform: scalar loads
+        const float4* wk = reinterpret_cast<const float4*>(sw + k * SRC_M);
 #pragma unroll
-        for (int mi = 0; mi < SRC_M; ++mi) acc[mi] = fmaf(wk[mi < nm ? mi : 0], xv, acc[mi]);
+        for (int q = 0; q < SRC_M / 4; ++q) {
+            const float4 w4 = wk[q];
+            acc[4 * q] = fmaf(w4.x, xv, acc[4 * q]);
+            acc[4 * q + 1] = fmaf(w4.y, xv, acc[4 * q + 1]);
+            acc[4 * q + 2] = fmaf(w4.z, xv, acc[4 * q + 2]);
+            acc[4 * q + 3] = fmaf(w4.w, xv, acc[4 * q + 3]);
+        }
     }
     float amx = 0.f;
 #pragma unroll
@@ -1381,7 +1396,7 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
                                 a->src_len > 0 && a->src_bstride >= 0 && !a->wrap),
                   "conv1d: bad fused source conv (src_K=%d src_stride=%d src_pad=%d src_len=%lld)", a->src_K,
                   a->src_stride, a->src_pad, (long long)a->src_len);
-    RVC_CHECK_ARG(!a->src_x || ((int64_t)255 * a->src_stride + a->src_K) * 4 <= 64 * 1024,
+    RVC_CHECK_ARG(!a->src_x || ((int64_t)255 * a->src_stride + 17 * a->src_K) * 4 <= 64 * 1024,
                   "conv1d: source conv span too large (stride %d, K %d)", a->src_stride, a->src_K);
     if (a->ntoff) {
         RVC_CHECK_ARG(a->ntoff == a->K && a->K <= 16, "conv1d: toff needs ntoff == K <= 16");
@@ -1740,7 +1755,7 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
         q.pad = a->src_pad;
         q.span = (SRC_T - 1) * a->src_stride + a->src_K;
         hipLaunchKernelGGL(src_add_kernel, dim3(cdiv(a->Lout, SRC_T), cdiv(a->Co, SRC_M), (unsigned)a->B), dim3(SRC_T),
-                           (size_t)q.span * 4, s, q);
+                           (size_t)(q.span + q.K * SRC_M) * 4, s, q);
         RVC_HIP(hipGetLastError());
     }
     return RVC_OK;
