@@ -147,6 +147,10 @@ int rvc_resblock_set_ylds(int on);
  * 128-wide tiles where it needs no extra LDS), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI (default 0).  Both give the same bits (tests/test_gpu_ops.py);
  * an A/B switch for measurements in one process. */
 int rvc_conv1d_set_tile_epi(int on);
+/* The split-operand engine's in-register epilogue in 128-byte rows (round 6: a v_permlane16_swap per accumulator pair
+ * regroups two 16-column fragments into 2 rows x 32 columns per register, so every residual / accumulate load and
+ * store moves 2 x 128-B segments instead of 4 x 64 B): 1 on, 0 off, -1 RVC_X6_SWZ (default 1).  Same bits. */
+int rvc_conv1d_set_swz(int on);
 /* Per-thread override of the split-fp16 loaders' fast form (used with amax_in on the 8-compute-wave tiles; same
  * bits as the general form): 1 on, 0 off, -1 back to RVC_X6_F16FAST (default on).  Diagnostic / test knob. */
 int rvc_conv1d_set_f16_fast(int on);
@@ -224,8 +228,8 @@ typedef struct rvc_attn_args {
  * workspace of rvc_attention_workspace_bytes(a) bytes (0 when not split). */
 int64_t rvc_attention_workspace_bytes(const rvc_attn_args* a);
 int rvc_attention(const rvc_attn_args* a, void* ws, int64_t ws_bytes, rvc_stream_t stream);
-/* the same, also folding max |o| into a |max| cell per batch element (amax_out as rvc_layernorm_cf_amax; not with the
- * relative band) */
+/* the same, also folding max |o| into a |max| cell per batch element (amax_out as rvc_layernorm_cf_amax; with the
+ * relative band only together with its value term ev, whose kernel publishes the final values) */
 int rvc_attention_amax(const rvc_attn_args* a, unsigned* amax_out, void* ws, int64_t ws_bytes, rvc_stream_t stream);
 /* Round 6: with amax_in (the |max| cell of q, k and v -- the QKV projection's published cell, one per batch element)
  * both products run in split-fp16 on the fp16 matrix cores (power-of-2 scaled operands split into 11 + 11 bit fp16
@@ -244,6 +248,10 @@ int rvc_attention_set_f16(int on);
 /* out = lrelu((lin + emb[pitch]) * scale, slope)       synthesizers.py:367 */
 int rvc_textenc_embed(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B, int64_t C,
                       int64_t T, float scale, float slope, rvc_stream_t stream);
+/* the same, also folding max |out| into a |max| cell per batch element (round 6: the TextEncoder's first split-fp16
+ * GEMM takes its scale from it) */
+int rvc_textenc_embed_amax(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B, int64_t C,
+                           int64_t T, float scale, float slope, unsigned* amax_out, rvc_stream_t stream);
 /* LayerNorm over channels of (x + res)                  synthesizers.py:170-181, fairseq.py:700 */
 int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out, int64_t B,
                      int64_t C, int64_t T, float eps, rvc_stream_t stream);

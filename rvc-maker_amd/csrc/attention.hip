@@ -531,14 +531,18 @@ __global__ __launch_bounds__(256) void attn_relv_band_kernel(AttnParams p, const
         pb[qi][r] = pv;
     }
     __syncthreads();
+    float amx = 0.f;  // amax_out: max |o| of the final values (the band term is the last one added)
     for (int i = tid; i < QB * D; i += 256) {
         const int qi = i % QB, c = i / QB;
         const int64_t qa = q0 + qi;
         if (qa >= T) continue;
         float acc = 0.f;
         for (int r = 0; r < nb; ++r) acc += pb[qi][r] * evs[r * D + c];
-        O[(int64_t)c * p.ldc + qa] += acc;
+        const float v = O[(int64_t)c * p.ldc + qa] + acc;
+        O[(int64_t)c * p.ldc + qa] = v;
+        amx = fmaxf(amx, fabsf(v));
     }
+    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
 }
 
 // Split-KV plan: enough blocks to cover the chip twice, at least 4 key tiles per split.
@@ -582,7 +586,7 @@ extern "C" int rvc_attention_set_f16(int on) {
 extern "C" int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in, unsigned* amax_out, void* ws,
                                 int64_t ws_bytes, rvc_stream_t stream) {
     RVC_CHECK_ARG(a && a->q && a->k && a->v && a->o && a->T > 0 && a->H > 0 && a->B > 0, "attention: bad args");
-    RVC_CHECK_ARG(!amax_out || !a->rk, "attention: amax_out is not built for the relative band");
+    RVC_CHECK_ARG(!amax_out || !a->rk || a->ev, "attention: amax_out with the relative band needs its value term (ev)");
     RVC_CHECK_ARG(a->D == 64 || a->D == 96, "attention: head dim %d unsupported (64, 96)", a->D);
     RVC_CHECK_ARG(!a->rk || (a->ml && a->W >= 0 && a->W <= 15), "attention: rel band needs ml and W <= 15");
     RVC_CHECK_ARG(!a->ev || (a->rk && (2 * a->W + 1) * a->D <= 31 * 96), "attention: ev band too large");
@@ -592,7 +596,7 @@ extern "C" int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in,
     p.q_hs = a->q_hs; p.k_hs = a->k_hs; p.v_hs = a->v_hs; p.o_hs = a->o_hs;
     p.q_bs = a->q_bs; p.k_bs = a->k_bs; p.v_bs = a->v_bs; p.o_bs = a->o_bs;
     p.H = a->H; p.W = a->W; p.scale = a->scale;
-    p.amax_out = amax_out;
+    p.amax_out = (a->rk && a->ev) ? nullptr : amax_out;  // with the rel-v band its kernel publishes (final values)
     p.amax_in = amax_in;
     static const int f16_env = getenv("RVC_ATTN_F16") ? atoi(getenv("RVC_ATTN_F16")) : 1;
     const bool f16 = amax_in && (g_attn_f16 >= 0 ? g_attn_f16 : f16_env);
@@ -621,6 +625,7 @@ extern "C" int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in,
         RVC_HIP(hipGetLastError());
     }
     if (a->rk && a->ev) {
+        p.amax_out = amax_out;
         hipLaunchKernelGGL(attn_relv_band_kernel, dim3(cdiv(a->T, 32), (unsigned)a->H, (unsigned)a->B), dim3(256), 0,
                            s, p, a->ev, a->D);
         RVC_HIP(hipGetLastError());

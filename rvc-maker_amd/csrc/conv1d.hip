@@ -54,6 +54,7 @@ struct ConvParams {
     unsigned* amax_out;       // or null: max |y| over the stored values (atomic max of the f32 bits)
     int stagger;              // x6: the first round of blocks starts spread over this many shader cycles (0 = off)
     int stagger_blocks;       // ... the blocks of that round (one per CU)
+    int swz;                  // x6: the 128-byte-row epilogue (conv_epilogue_swz; RVC_X6_SWZ, rvc_conv1d_set_swz)
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
@@ -62,6 +63,8 @@ struct ConvParams {
 
 // per-thread override of the split-fp16 fast loader form (rvc_conv1d_set_f16_fast; -1 = RVC_X6_F16FAST, default on)
 static thread_local int g_f16_fast = -1;
+// per-thread override of the 128-byte-row epilogue (rvc_conv1d_set_swz; -1 = RVC_X6_SWZ, default on)
+static thread_local int g_swz = -1;
 
 __device__ __forceinline__ int tap_off(const ConvParams& p, int t) { return p.ntoff ? p.toff[t] : t * p.dil; }
 
@@ -194,6 +197,91 @@ __device__ __forceinline__ void conv_epilogue(const ConvParams& p, floatx4 (&acc
             }
     }
     if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // the batch element's cell
+}
+
+// The same epilogue with 128-byte rows (round 6, x6 engine, even FN, no split-K): a 16x16 accumulator register holds 4
+// rows x 16 columns (4 x 64-B segments per load / store instruction, a shape the guide leaves unmeasured); one
+// v_permlane16_swap per register pair of two adjacent column fragments regroups them so that each register holds 2 rows
+// x 32 consecutive columns -- 2 x 128-B segments, the access shape MI355X_MICROARCH.md rates at full rate -- for every
+// residual / accumulate load and every store.  After the swap of fragments (2 jp, 2 jp + 1), register r of the first is
+// row r + 8 h, of the second row 4 + r + 8 h (h = lane >> 5), both at column 32 jp + (lane & 31).  Same operations in
+// the same order per element as conv_epilogue, so the same bits.
+template <int FM, int FN, int WM, int WN>
+__device__ __forceinline__ void conv_epilogue_swz(const ConvParams& p, floatx4 (&acc)[FM][FN], int lane, int wm, int wn,
+                                                  int phase, int b, int g, int Cog, int m0g, int64_t n0) {
+    static_assert(FN % 2 == 0, "column fragments in pairs");
+    constexpr int NP = FN / 2;
+    const int h = lane >> 5, lc = lane & 31;
+    int tcol[NP];
+#pragma unroll
+    for (int jp = 0; jp < NP; ++jp) tcol[jp] = out_pos(p, n0 + wn * 16 * FN + jp * 32 + lc, phase);
+    float* yb = p.y + b * p.y_bstride;
+    const float* rb2 = p.res ? p.res + b * p.res_bstride : nullptr;
+    const int Lo = (int)p.Lout;
+    float amx = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int jp = 0; jp < NP; ++jp)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                                 __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+                acc[i][2 * jp][r] = __uint_as_float(sw[0]);
+                acc[i][2 * jp + 1][r] = __uint_as_float(sw[1]);
+            }
+        // element (jp, k): k < 4 register k of fragment 2 jp, else register k - 4 of fragment 2 jp + 1; row k + 8 h
+        floatx4 (&av)[1][FN] = *reinterpret_cast<floatx4 (*)[1][FN]>(&acc[i][0]);
+        int mrow[8];
+        bool mok[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int mg = m0g + wm * 16 * FM + i * 16 + 8 * h + k;
+            mok[k] = mg < Cog;
+            mrow[k] = g * Cog + (mg < Cog ? mg : 0);
+            float bs = 0.f;
+            if (p.bias) bs = p.bias[mrow[k]];
+            if (p.bias2) bs += p.bias2[mrow[k]];
+#pragma unroll
+            for (int jp = 0; jp < NP; ++jp) av[0][2 * jp + (k >> 2)][k & 3] += bs;
+        }
+        switch (p.out_act) {
+            case RVC_ACT_LRELU: apply_act<RVC_ACT_LRELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_RELU: apply_act<RVC_ACT_RELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_TANH: apply_act<RVC_ACT_TANH, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_GELU: apply_act<RVC_ACT_GELU, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_SIGMOID: apply_act<RVC_ACT_SIGMOID, 1, FN>(av, p.out_slope, p.out_scale); break;
+            case RVC_ACT_LOGCLAMP: apply_act<RVC_ACT_LOGCLAMP, 1, FN>(av, p.out_slope, p.out_scale); break;
+            default: apply_act<RVC_ACT_NONE, 1, FN>(av, p.out_slope, p.out_scale); break;
+        }
+        if (rb2) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int jp = 0; jp < NP; ++jp)
+                    av[0][2 * jp + (k >> 2)][k & 3] += rb2[mrow[k] * Lo + (tcol[jp] >= 0 ? tcol[jp] : 0)];
+        }
+        if (p.accumulate) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int jp = 0; jp < NP; ++jp)
+                    av[0][2 * jp + (k >> 2)][k & 3] += yb[mrow[k] * Lo + (tcol[jp] >= 0 ? tcol[jp] : 0)];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int jp = 0; jp < NP; ++jp) {
+                const float v = av[0][2 * jp + (k >> 2)][k & 3];
+                if (mok[k] && tcol[jp] >= 0) {
+                    yb[mrow[k] * Lo + tcol[jp]] = v;
+                    amx = fmaxf(amx, fabsf(v));
+                } else if (mok[k] && tcol[jp] <= -2) {
+                    yb[mrow[k] * Lo + (-tcol[jp] - 2)] = 0.f;  // 2-D border cell
+                }
+            }
+    }
+    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
 }
 
 template <int FM, int FN, int WM, int WN>
@@ -1107,6 +1195,8 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             __syncthreads();
             x6_tile_epilogue<BM / 2, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g + BM / 2, n0);
         }
+    } else if (p.swz && p.ksplit == 1) {
+        conv_epilogue_swz<FM, FN, WM, WN>(p, acc, lane, wm, wn, phase, b, 0, Cog, m0g, n0);
     } else {
         conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
     }
@@ -1298,6 +1388,8 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.f16_fast = g_f16_fast >= 0 ? g_f16_fast : f16fast;
     p.stagger = 0;
     p.stagger_blocks = 0;
+    static const int swz_env = getenv("RVC_X6_SWZ") ? atoi(getenv("RVC_X6_SWZ")) : 1;
+    p.swz = g_swz >= 0 ? g_swz : swz_env;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -1676,6 +1768,11 @@ extern "C" void rvc_conv1d_set_probe_event(void* hip_event) { g_probe_event = (h
 
 extern "C" int rvc_conv1d_set_f16_fast(int on) {
     g_f16_fast = on < 0 ? -1 : (on ? 1 : 0);
+    return RVC_OK;
+}
+
+extern "C" int rvc_conv1d_set_swz(int on) {
+    g_swz = on < 0 ? -1 : (on ? 1 : 0);
     return RVC_OK;
 }
 

@@ -79,26 +79,38 @@ extern "C" int rvc_rand_triang(float* out, int64_t n, float lo, float hi, uint64
 
 // ---------------------------------------------------------------- TextEncoder input
 // out[c][t] = lrelu((lin[c][t] + emb[pitch[t]][c]) * scale, slope)     (synthesizers.py:367)
+// amax_out (or null): max |out| per batch element into a |max| cell (the first QKV projection's split-fp16 scale)
 __global__ void textenc_embed_kernel(const float* lin, const float* emb, const int64_t* pitch, float* out, int C,
-                                     int64_t T, float scale, float slope) {
+                                     int64_t T, float scale, float slope, unsigned* amax_out) {
     int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int c = blockIdx.y;
     int b = blockIdx.z;
-    if (t >= T) return;
-    int64_t o = ((int64_t)b * C + c) * T + t;
-    float v = lin[o];
-    if (emb) v += emb[pitch[(int64_t)b * T + t] * C + c];
-    v *= scale;
-    out[o] = v >= 0.f ? v : v * slope;
+    float m = 0.f;
+    if (t < T) {
+        int64_t o = ((int64_t)b * C + c) * T + t;
+        float v = lin[o];
+        if (emb) v += emb[pitch[(int64_t)b * T + t] * C + c];
+        v *= scale;
+        v = v >= 0.f ? v : v * slope;
+        out[o] = v;
+        m = fabsf(v);
+    }
+    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, m);  // every lane (the wave's shuffles)
+}
+
+extern "C" int rvc_textenc_embed_amax(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B,
+                                      int64_t C, int64_t T, float scale, float slope, unsigned* amax_out,
+                                      rvc_stream_t stream) {
+    RVC_CHECK_ARG(lin && out && (!emb || pitch) && B > 0 && C > 0 && T > 0, "textenc_embed: bad args");
+    hipLaunchKernelGGL(textenc_embed_kernel, dim3(cdiv(T, 256), (unsigned)C, (unsigned)B), dim3(256), 0,
+                       (hipStream_t)stream, lin, emb, pitch, out, (int)C, T, scale, slope, amax_out);
+    RVC_HIP(hipGetLastError());
+    return RVC_OK;
 }
 
 extern "C" int rvc_textenc_embed(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B,
                                  int64_t C, int64_t T, float scale, float slope, rvc_stream_t stream) {
-    RVC_CHECK_ARG(lin && out && (!emb || pitch) && B > 0 && C > 0 && T > 0, "textenc_embed: bad args");
-    hipLaunchKernelGGL(textenc_embed_kernel, dim3(cdiv(T, 256), (unsigned)C, (unsigned)B), dim3(256), 0,
-                       (hipStream_t)stream, lin, emb, pitch, out, (int)C, T, scale, slope);
-    RVC_HIP(hipGetLastError());
-    return RVC_OK;
+    return rvc_textenc_embed_amax(lin, emb, pitch, out, B, C, T, scale, slope, nullptr, stream);
 }
 
 // ---------------------------------------------------------------- prior sample

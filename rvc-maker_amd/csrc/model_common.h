@@ -56,6 +56,7 @@ struct rvc_ctx {
     bool fe_amax = true;      // RVC_AMD_FE_AMAX as contentvec.py: the feature extractor's convs through |max| cells
     bool fused_noise = true;  // RVC_AMD_FUSED_NOISE as synth.py: noise_convs fused into the upsampling convs
     bool attn_f16 = true;     // RVC_AMD_ATTN_F16 as contentvec.py / synth.py: QKV |max| cells, split-fp16 attention
+    bool te_amax = true;      // RVC_AMD_TE_AMAX as synth.py: the TextEncoder's and the flow's GEMMs through |max| cells
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;

@@ -122,7 +122,9 @@ Bufs plan_bufs(const Synth& S, int64_t T) {
     b.xpre = p.take((int64_t)g.upsample_initial_channel * T);
     // the |max| cells of the ResBlock stages, then one per stage output and one for conv_pre (synth.py generator)
     b.amax = p.take((kAmaxPerStage * 8 + 8 + 1) * RVC_AMAX_SHARDS);
-    b.tcell = p.take((int64_t)S.layers.size() * RVC_AMAX_SHARDS);  // the TextEncoder's QKV |max| cells
+    // the TextEncoder's |max| cells (embedding, then per layer qkv, o, ln1, ffn1, ln2) and the flow's (the constant 1.0
+    // cell of the gate outputs, then per flow h0, h1, h2, the skip sum, post's x1): synth.py text_encoder / flow_reverse
+    b.tcell = p.take((int64_t)(1 + 5 * S.layers.size() + 1 + 5 * 4) * RVC_AMAX_SHARDS);
     int64_t Lc = T;
     for (size_t i = 0; i < S.ups.size(); ++i) {
         Lc = convT_out_len(S.ups[i], Lc);
@@ -165,17 +167,26 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         CallOpts o;
         MTRY(conv(c, S, S.emb_phone, phone_cf, T, lin, o, s));
     }
-    MTRY(rvc_textenc_embed(lin, S.emb_pitch, pitch, x, 1, H, T, (float)sqrt((double)H), 0.1f, s));
+    // |max| cells (synth.py TE_AMAX): one memset for the TextEncoder's and the flow's, then the flow's 1.0 cell
+    const int64_t nl = (int64_t)S.layers.size();
+    unsigned* tcells = c->te_amax ? reinterpret_cast<unsigned*>(A + bf.tcell) : nullptr;
+    auto tcell = [&](int64_t k) { return tcells ? tcells + RVC_AMAX_SHARDS * k : nullptr; };
+    if (tcells) {
+        MHIP(hipMemsetAsync(tcells, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * (1 + 5 * nl + 1 + 5 * 4), s));
+        MHIP(hipMemsetD32Async((hipDeviceptr_t)tcell(1 + 5 * nl), 0x3F800000, 1, s));  // 1.0f: |tanh * sigmoid| < 1
+    }
+    MTRY(rvc_textenc_embed_amax(lin, S.emb_pitch, pitch, x, 1, H, T, (float)sqrt((double)H), 0.1f, tcell(0), s));
+    const unsigned* te_cell = tcell(0);  // the current x's
     const float scale = (float)(1.0 / sqrt((double)kc));
-    // QKV |max| cells (synth.py text_encoder): the attention runs split-fp16 from them
-    unsigned* tcells = c->attn_f16 ? reinterpret_cast<unsigned*>(A + bf.tcell) : nullptr;
-    if (tcells) MHIP(hipMemsetAsync(tcells, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * S.layers.size(), s));
-    for (size_t li = 0; li < S.layers.size(); ++li) {
+    for (int64_t li = 0; li < nl; ++li) {
         const Layer& Ly = S.layers[li];
-        unsigned* c_qkv = tcells ? tcells + RVC_AMAX_SHARDS * li : nullptr;
+        unsigned *c_qkv = tcell(1 + 5 * li), *c_o = tcell(2 + 5 * li), *c_l1 = tcell(3 + 5 * li),
+                 *c_f1 = tcell(4 + 5 * li), *c_l2 = tcell(5 + 5 * li);
         CallOpts o;
+        o.amax_in = te_cell;
         o.amax_out = c_qkv;
         MTRY(conv(c, S, Ly.qkv, x, T, qkv, o, s));
+        o.amax_in = nullptr;
         o.amax_out = nullptr;
         CallOpts orl;
         orl.B = nh;
@@ -204,20 +215,27 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         MCHECK(need >= 0, "rvc_synth_infer: attention shape H=%lld D=%lld T=%lld unsupported", (long long)nh,
                (long long)kc, (long long)T);
         MTRY(ensure_ws(S, need, s));
-        MTRY(rvc_attention_ex(&at, c_qkv, nullptr, need ? S.ws : nullptr, need, s));
-        MTRY(conv(c, S, Ly.o, ob, T, tmp, o, s));
-        MTRY(rvc_layernorm_cf(x, tmp, Ly.ln1g, Ly.ln1b, x, 1, H, T, 1e-5f, s));
+        MTRY(rvc_attention_ex(&at, c->attn_f16 ? c_qkv : nullptr, c_o, need ? S.ws : nullptr, need, s));
+        CallOpts oo;
+        oo.amax_in = c_o;
+        MTRY(conv(c, S, Ly.o, ob, T, tmp, oo, s));
+        MTRY(rvc_layernorm_cf_amax(x, tmp, Ly.ln1g, Ly.ln1b, x, 1, H, T, 1e-5f, c_l1, s));
         CallOpts f1;
         f1.pad = (g.kernel_size - 1) / 2;
         f1.out_act = RVC_ACT_RELU;
+        f1.amax_in = c_l1;
+        f1.amax_out = c_f1;
         MTRY(conv(c, S, Ly.ffn1, x, T, ffh, f1, s));
         CallOpts f2;
         f2.pad = (g.kernel_size - 1) / 2;
+        f2.amax_in = c_f1;
         MTRY(conv(c, S, Ly.ffn2, ffh, T, tmp, f2, s));
-        MTRY(rvc_layernorm_cf(x, tmp, Ly.ln2g, Ly.ln2b, x, 1, H, T, 1e-5f, s));
+        MTRY(rvc_layernorm_cf_amax(x, tmp, Ly.ln2g, Ly.ln2b, x, 1, H, T, 1e-5f, c_l2, s));
+        te_cell = c_l2;
     }
     {
         CallOpts o;
+        o.amax_in = te_cell;
         MTRY(conv(c, S, S.proj, x, T, stats, o, s));
     }
     // ---- prior sample (synthesizers.py:449)
@@ -232,38 +250,54 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     float *h = A + bf.h, *acts = A + bf.acts, *outacc = A + bf.outacc, *xin = A + bf.xin;
     float* bufs[2] = {A + bf.fb0, A + bf.fb1};
     float* xf_cur = zp;
-    for (int f = 3; f >= 0; --f) {
+    // the flow's |max| cells (synth.py flow_reverse): after the TextEncoder's, the 1.0 cell then 5 per flow
+    const unsigned* unit = tcell(1 + 5 * nl);
+    const unsigned* post_cell = nullptr;
+    for (int f = 3, n = 0; f >= 0; --f, ++n) {
         const Flow& F = S.flows[f];
+        unsigned* c_h[3] = {tcell(2 + 5 * nl + 5 * n), tcell(3 + 5 * nl + 5 * n), tcell(4 + 5 * nl + 5 * n)};
+        unsigned *c_acc = tcell(5 + 5 * nl + 5 * n), *c_post = tcell(6 + 5 * nl + 5 * n);
         float* xf = (xf_cur != bufs[0]) ? bufs[0] : bufs[1];
         MTRY(rvc_flip_channels(xf_cur, xf, 1, I, T, s));
         float *x0 = xf, *x1 = xf + half * T;
         {
             CallOpts o;
+            o.amax_in = post_cell;
+            o.amax_out = c_h[0];
             MTRY(conv(c, S, F.pre, x0, T, h, o, s));
         }
         for (int l = 0; l < 3; ++l) {
             CallOpts oi;
             oi.pad = (F.ins[l].K - 1) / 2;
             oi.bias2 = gc + (int64_t)f * 6 * H + (int64_t)l * 2 * H;
+            oi.amax_in = c_h[l];
             MTRY(conv(c, S, F.ins[l], h, T, xin, oi, s));
             MTRY(rvc_gate(xin, acts, 1, H, T, s));
             if (l < 2) {
                 CallOpts ra;
                 ra.res = h;
+                ra.amax_in = unit;
+                ra.amax_out = c_h[l + 1];
                 MTRY(conv(c, S, F.rs_a[l], acts, T, h, ra, s));
                 CallOpts rb;
                 rb.accumulate = l > 0;
+                rb.amax_in = unit;
                 MTRY(conv(c, S, F.rs_b[l], acts, T, outacc, rb, s));
             } else {
                 CallOpts rb;
                 rb.accumulate = 1;
+                rb.amax_in = unit;
+                rb.amax_out = c_acc;
                 MTRY(conv(c, S, F.rs_b[l], acts, T, outacc, rb, s));
             }
         }
         CallOpts po;
         po.res = x1;
         po.out_scale = -1.f;
+        po.amax_in = c_acc;
+        po.amax_out = c_post;
         MTRY(conv(c, S, F.post, outacc, T, x1, po, s));
+        post_cell = c_post;
         xf_cur = xf;
     }
     const float* z = xf_cur;
@@ -430,6 +464,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->fe_amax = env_on("RVC_AMD_FE_AMAX");
     c->fused_noise = env_on("RVC_AMD_FUSED_NOISE");
     c->attn_f16 = env_on("RVC_AMD_ATTN_F16");
+    c->te_amax = env_on("RVC_AMD_TE_AMAX");
     *out = c;
     return RVC_OK;
 }

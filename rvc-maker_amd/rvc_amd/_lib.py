@@ -134,6 +134,7 @@ SIGNATURES = {
     "rvc_resblock_set_stamps": [c_void_p, c_int64],
     "rvc_resblock_set_ylds": [c_int],
     "rvc_conv1d_set_tile_epi": [c_int],
+    "rvc_conv1d_set_swz": [c_int],
     "rvc_conv1d_set_f16_fast": [c_int],
     "rvc_bigru64_set_f32": [c_int],
     "rvc_conv1d_set_splitk_target": [c_int],
@@ -157,6 +158,8 @@ SIGNATURES = {
                               c_void_p, c_void_p],
     "rvc_textenc_embed": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
                           c_void_p],
+    "rvc_textenc_embed_amax": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_float,
+                               c_void_p, c_void_p],
     "rvc_layernorm_cf": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
                          c_void_p],
     "rvc_chnorm_gelu": [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_int, c_void_p],

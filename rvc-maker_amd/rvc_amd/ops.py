@@ -456,9 +456,12 @@ def attention(q, k, v, o, *, B, H, D, T, ldc, q_hs, k_hs, v_hs, o_hs, scale, q_b
     return o
 
 
-def textenc_embed(lin, emb, pitch, out, B, C, T, scale, slope):
-    check(_lib.load().rvc_textenc_embed(_p(lin), _p(emb), _p(pitch), _p(out), B, C, T, scale, slope, _stream()),
-          "textenc_embed")
+def textenc_embed(lin, emb, pitch, out, B, C, T, scale, slope, amax_out=None):
+    """``amax_out``: a |max| cell (``AmaxSlots``) that receives max |out| per batch element."""
+    if amax_out is not None and amax_out.numel() < B * AMAX_SHARDS:
+        raise ValueError("textenc_embed: amax_out needs a cell per batch element")
+    check(_lib.load().rvc_textenc_embed_amax(_p(lin), _p(emb), _p(pitch), _p(out), B, C, T, scale, slope,
+                                             _p(amax_out), _stream()), "textenc_embed")
     return out
 
 

@@ -39,6 +39,9 @@ AMAX_PER_STAGE = 16
 FUSED_NOISE = os.environ.get("RVC_AMD_FUSED_NOISE", "1") != "0"
 # round 6: the TextEncoder's rel-pos attention in split-fp16 from the QKV projection's |max| (contentvec.ATTN_F16)
 ATTN_F16 = os.environ.get("RVC_AMD_ATTN_F16", "1") != "0"
+# round 6: the TextEncoder's and the flow's GEMMs in split-fp16 from their producers' |max| cells (RVC_AMD_TE_AMAX=0: the
+# 6-pass split-bf16 form of round 5; rvc_model.cpp reads the same switch)
+TE_AMAX = os.environ.get("RVC_AMD_TE_AMAX", "1") != "0"
 
 
 def fold_weight_norm(weight: dict) -> dict:
@@ -143,30 +146,38 @@ class SynthesizerAMD:
         H, dev, nh, kc = self.hidden, phone_cf.device, self.n_heads, self.kc
         lin = self.emb_phone(phone_cf.reshape(B, -1, T))
         x = torch.empty(B, H, T, device=dev)
-        ops.textenc_embed(lin, self.emb_pitch if pitch is not None else None, pitch, x, B, H, T, math.sqrt(H), 0.1)
+        # |max| cells (round 6, TE_AMAX): the embedding and every LayerNorm, the QKV projection (-> split-fp16
+        # attention), the attention output (its rel-v band kernel publishes) and ffn1 publish, and the GEMM reading each
+        # runs split-fp16 from it; cell 0 the embedding's, then per layer (qkv, o, ln1, ffn1, ln2)
+        nl = len(self.layers)
+        cells = ops.AmaxSlots(1 + 5 * nl, dev, B) if TE_AMAX else None
+        cell = (lambda k: cells[k]) if cells is not None else (lambda k: None)
+        ops.textenc_embed(lin, self.emb_pitch if pitch is not None else None, pitch, x, B, H, T, math.sqrt(H), 0.1,
+                          amax_out=cell(0))
+        x_cell = cell(0)
         tmp = torch.empty(B, H, T, device=dev)
         o = torch.empty(B, H, T, device=dev)
         ml = torch.empty(B, nh, 2, T, device=dev)
         rk = torch.empty(B, nh, 21, T, device=dev)
         scale = 1.0 / math.sqrt(kc)
-        # round 6: each layer's QKV projection publishes max |q|, |k|, |v| and the attention runs split-fp16 from it
-        tcells = ops.AmaxSlots(len(self.layers), dev, B) if ATTN_F16 else None
         for li, L in enumerate(self.layers):
-            c_qkv = tcells[li] if tcells else None
-            qkv = L["qkv"](x, amax_out=c_qkv)
+            c_qkv, c_o, c_l1, c_f1, c_l2 = (cell(1 + 5 * li + k) for k in range(5))
+            qkv = L["qkv"](x, amax_in=x_cell, amax_out=c_qkv)
             for b in range(B):  # Rk of clip b's heads: one K=1 conv over its nh query slices
                 L["relk"](qkv[b] if B > 1 else qkv, B=nh, Lin=T, x_bstride=kc * T, Lout=T, out_scale=scale,
                           out=rk[b])
             qb = qkv.view(B, 3 * H, T)
             ops.attention(qb, qb[:, H:], qb[:, 2 * H:], o, B=B, H=nh, D=kc, T=T, ldc=T, q_hs=kc * T,
                           k_hs=kc * T, v_hs=kc * T, o_hs=kc * T, q_bs=3 * H * T, k_bs=3 * H * T, v_bs=3 * H * T,
-                          o_bs=H * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10, amax_in=c_qkv)
-            y = L["o"](o, out=tmp)
-            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, H, T)
-            h = L["ffn1"](x, pad=(self.ksz - 1) // 2, out_act=ACT_RELU)
-            y = L["ffn2"](h, pad=(self.ksz - 1) // 2, out=tmp)
-            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, B, H, T)
-        return self.proj(x).view(B, 2 * self.inter, T)
+                          o_bs=H * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10,
+                          amax_in=c_qkv if ATTN_F16 else None, amax_out=c_o)
+            y = L["o"](o, out=tmp, amax_in=c_o)
+            ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, H, T, amax_out=c_l1)
+            h = L["ffn1"](x, pad=(self.ksz - 1) // 2, out_act=ACT_RELU, amax_in=c_l1, amax_out=c_f1)
+            y = L["ffn2"](h, pad=(self.ksz - 1) // 2, out=tmp, amax_in=c_f1)
+            ops.layernorm_cf(x, y, L["ln2"][0], L["ln2"][1], x, B, H, T, amax_out=c_l2)
+            x_cell = c_l2
+        return self.proj(x, amax_in=x_cell).view(B, 2 * self.inter, T)
 
     def flow_reverse(self, z_p, gc, T, B=1):
         """ResidualCouplingBlock reverse (residuals.py:87-95, 127-137) + WaveNet (modules.py:35-51);
@@ -177,23 +188,36 @@ class SynthesizerAMD:
         h = torch.empty(B, H, T, device=dev)
         acts = torch.empty(B, H, T, device=dev)
         out_acc = torch.empty(B, H, T, device=dev)
-        for f in reversed(range(4)):
+        # |max| cells (round 6, TE_AMAX): per flow the WaveNet's h (pre, then each rs_a), the skip sum (the last rs_b) and
+        # post's output x1 (the next flow's pre input, flipped) publish; the gate's output is tanh * sigmoid, |.| < 1,
+        # so the res/skip convs take a constant 1.0 cell (cell 0)
+        cells = ops.AmaxSlots(1 + 5 * 4, dev, B) if TE_AMAX else None
+        cell = (lambda k: cells[k]) if cells is not None else (lambda k: None)
+        if cells is not None:
+            cells[0].view(B, ops.AMAX_SHARDS)[:, 0].fill_(0x3F800000)  # 1.0f
+        unit = cell(0)
+        post_cell = None
+        for n, f in enumerate(reversed(range(4))):
             F = self.flows[f]
+            c_h = [cell(1 + 5 * n + k) for k in range(3)]
+            c_acc, c_post = cell(1 + 5 * n + 3), cell(1 + 5 * n + 4)
             xf = bufs[0] if x is not bufs[0] else bufs[1]
             ops.flip_channels(x, xf, B, I, T)
             # x0 = xf[:, :half], x1 = xf[:, half:]: batch stride I*T
-            F["pre"](xf, B=B, Lin=T, x_bstride=I * T, out=h)
+            F["pre"](xf, B=B, Lin=T, x_bstride=I * T, out=h, amax_in=post_cell, amax_out=c_h[0])
             for l in range(3):
                 g_l = gc[f * 6 * H + l * 2 * H: f * 6 * H + (l + 1) * 2 * H]
-                xin = F["ins"][l](h, pad=2, bias2=g_l)
+                xin = F["ins"][l](h, pad=2, bias2=g_l, amax_in=c_h[l])
                 ops.gate(xin, acts, B, H, T)
                 if l < 2:
-                    F["rs_a"][l](acts, out=h, res=h)
-                    F["rs_b"][l](acts, out=out_acc, accumulate=(l > 0))
+                    F["rs_a"][l](acts, out=h, res=h, amax_in=unit, amax_out=c_h[l + 1])
+                    F["rs_b"][l](acts, out=out_acc, accumulate=(l > 0), amax_in=unit)
                 else:
-                    F["rs_b"][l](acts, out=out_acc, accumulate=True)
+                    F["rs_b"][l](acts, out=out_acc, accumulate=True, amax_in=unit, amax_out=c_acc)
             x1 = xf[:, half:]
-            F["post"](out_acc, out=x1, res=x1, y_bstride=I * T, res_bstride=I * T, out_scale=-1.0)
+            F["post"](out_acc, out=x1, res=x1, y_bstride=I * T, res_bstride=I * T, out_scale=-1.0, amax_in=c_acc,
+                      amax_out=c_post)
+            post_cell = c_post
             x = xf
         return x
 

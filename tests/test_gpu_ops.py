@@ -477,3 +477,54 @@ def test_fe0_gn_gelu(ops, B, N):
     out = ops.fe0_gn_gelu(wav.to(DEV).contiguous(), c.w, gamma.to(DEV), beta.to(DEV), B, N, 512, 10, 5)
     got = out.cpu().double().reshape(ref.shape)
     assert (got - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp32x6", "bf16x3", "bf16"])
+@pytest.mark.parametrize("case", [
+    ("rb", 128, 128, 11, 5, 5003, 1),      # the 128 x 256 split-fp16 tile, ragged last tile
+    ("full", 64, 64, 5, 1, 3001, 2),       # bias2 / tanh / scale / residual / accumulate, batched, Lout % 4 != 0
+    ("full", 40, 72, 3, 1, 777, 1),        # ragged rows and channels
+    ("rb", 256, 256, 7, 1, 300, 1),
+    ("rb", 32, 32, 3, 1, 4099, 3),         # 32 x 128 tiles, batched
+    ("convT", 64, 32, 12, 0, 300, 1),      # polyphase stores (ConvTranspose u = 12)
+    ("convT", 256, 128, 10, 0, 200, 2),
+])
+def test_x6_epilogue_128b_rows_bit_identical(ops, prec, case):
+    """The x6 engine's in-register epilogue in 128-byte rows (round 6, rvc_conv1d_set_swz: a v_permlane16_swap per
+    accumulator pair of adjacent column fragments) gives the same bits as the 16-column form, for every epilogue feature,
+    polyphase stores and batched launches."""
+    epi, Ci, Co, K, d, L, B = case
+    g = gen(Ci + Co + K)
+    outs = []
+    lib = ops._lib.load()
+    if epi == "convT":
+        u = K
+        w = torch.randn(Ci, Co, 2 * u, generator=g) / math.sqrt(Ci * 2)
+        c = ops.ConvT(w, torch.randn(Co, generator=g), u, u // 2)
+        x = torch.randn(B, Ci, L, generator=g).to(DEV)
+    else:
+        w = torch.randn(Co, Ci, K, generator=g) / math.sqrt(Ci * K)
+        c = ops.Conv(w, torch.randn(Co, generator=g))
+        x = torch.randn(B, Ci, L, generator=g).to(DEV)
+        b2 = torch.randn(Co, generator=g).to(DEV)
+        res = torch.randn(B, Co, L, generator=g).to(DEV)
+        acc0 = torch.randn(B, Co, L, generator=g).to(DEV)
+    for on in (0, 1):
+        lib.rvc_conv1d_set_swz(on)
+        try:
+            with ops.precision(prec), ops.splitk_target(0):
+                if epi == "convT":
+                    y = c(x if B > 1 else x[0], in_act=ops.ACT_LRELU, in_slope=0.1)
+                else:
+                    y = acc0.clone() if epi == "full" else torch.empty(B, Co, L, device=DEV)
+                    kw = dict(pad=d * (K - 1) // 2, dil=d, out=y if B > 1 else y[0], res=res if B > 1 else res[0],
+                              in_act=ops.ACT_LRELU, in_slope=0.1)
+                    if epi == "full":
+                        kw.update(bias2=b2, accumulate=True, in_scale=0.5, out_act=ops.ACT_TANH, out_scale=-1.0)
+                    c(x if B > 1 else x[0], **kw)
+                assert ops.LAST_CONV_ENGINE == 1
+            torch.cuda.synchronize()
+            outs.append(y.cpu())
+        finally:
+            lib.rvc_conv1d_set_swz(-1)
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
