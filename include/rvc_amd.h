@@ -87,8 +87,10 @@ typedef struct rvc_conv1d_args {
     int ntoff, wrap;
     int toff[16];
     /* Split-bf16 engine: wx = the same weights pre-split into bf16 h/m/l planes by
-       rvc_conv1d_pack_x6 (NULL = f32 MFMA engine).  Used for stride-1, ungrouped, 1-D convs;
-       other shapes ignore it.  wx_nmf = its padded 16-row fragment count.
+       rvc_conv1d_pack_x6 (NULL = f32 MFMA engine).  Used for stride-1 (and stride-2) 1-D convs --
+       ungrouped (<= 64 taps), or grouped (<= 128 taps, nphase 1, stride 1, no src_*) with the image packed
+       with the groups as phases: pack_x6(w, groups, Ci/g, K, Co/g); other shapes ignore it.
+       wx_nmf = its padded 16-row fragment count.
        wx_passes: bf16 MFMA passes per product -- 0 or 6 = f32-accurate (hH+hM+mH+hL+mM+lH, products to
        2^-24), RVC_ARITH_FP32_SA = the same 6 passes with hH and the 5 corrections accumulated apart (RMVPE,
        whose f0 is a per-frame decision), 3 = hH+hM+mH (16-bit operand mantissas), 1 = hH (bf16 operands);
@@ -143,6 +145,11 @@ int rvc_resblock_set_stamps(void* buf, int64_t bytes);
  * into LDS (over the tile's residual rows) and the loader waves store them during the next tile (the compute waves go
  * straight on), 0 = the compute waves' own global stores, -1 = RVC_RB_YLDS (default 1).  Same bits either way. */
 int rvc_resblock_set_ylds(int on);
+/* The fused pair's C = 64 tiling for this thread's launches (round 6): 1 = 2 row fragments per compute wave, 240
+ * outputs per tile (the <= 2-plane pass sets; 6-pass pairs keep the narrow form), 0 = 1 row fragment, 112 outputs,
+ * -1 = RVC_RB_WIDE64 (default 1).  The same sums in the same order; split-fp16's power-of-2 tile scales follow the
+ * tile, so results agree to that arithmetic's precision rather than bit for bit.  Returns the previous setting. */
+int rvc_resblock_set_wide64(int on);
 /* The split-operand engine's epilogue form for this thread's launches: 1 = the tile epilogue through LDS (on the
  * 128-wide tiles where it needs no extra LDS), 0 = the in-register epilogue, -1 = RVC_X6_TILE_EPI (default 0).  Both give the same bits (tests/test_gpu_ops.py);
  * an A/B switch for measurements in one process. */

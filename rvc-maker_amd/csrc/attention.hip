@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void attn_relv_band_kernel(AttnParams p, const
         O[(int64_t)c * p.ldc + qa] = v;
         amx = fmaxf(amx, fabsf(v));
     }
-    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
+    if (p.amax_out) amax_publish_block(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // one atomic per block
 }
 
 // Split-KV plan: enough blocks to cover the chip twice, at least 4 key tiles per split.

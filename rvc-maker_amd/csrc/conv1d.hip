@@ -55,6 +55,7 @@ struct ConvParams {
     int stagger;              // x6: the first round of blocks starts spread over this many shader cycles (0 = off)
     int stagger_blocks;       // ... the blocks of that round (one per CU)
     int swz;                  // x6: the 128-byte-row epilogue (conv_epilogue_swz; RVC_X6_SWZ, rvc_conv1d_set_swz)
+    int gx6;                  // x6 grouped conv: the phase index is the group (Ci, Co per group; image packed per group)
 #if RVC_CONV_STAMPS
     unsigned long long* stamps;  // diagnostic build only: [block][X6_STAMP_W] s_memtime stamps (rvc_conv1d_set_stamps)
     int64_t stamp_blocks;
@@ -683,6 +684,10 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
     zb /= p.ksplit;
     const int phase = zb % p.nphase;
     const int b = zb / p.nphase;
+    // a grouped conv (gx6, ContentVec's pos_conv) runs its groups as phases: the phase selects the group's weight image,
+    // input channel rows and output channel rows; its outputs are stored unphased
+    const int grp = p.gx6 ? phase : 0;
+    const int ophase = p.gx6 ? 0 : phase;
     const int Cog = (int)p.Co;
     const int Cig = (int)p.Ci;
     const int m0g = by * BM;
@@ -730,7 +735,7 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
         const bool lw0 = wave == NCW;
         if (lw0) X6_STAMP(8, X6_NOW());
         const int lin = (int)p.Lin;
-        const float* xb = p.x + b * p.x_bstride;
+        const float* xb = p.x + b * p.x_bstride + (int64_t)grp * Cig * p.Lin;
         const int base = (int)(n0 * p.stride - p.pad);
         int ipos[X6_NI], ig8[X6_NI];
         unsigned iok = 0;
@@ -1196,9 +1201,9 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
             x6_tile_epilogue<BM / 2, BN, 64 * (NCW + 4)>(p, ot, tid, split, b, m0g + BM / 2, n0);
         }
     } else if (p.swz && p.ksplit == 1) {
-        conv_epilogue_swz<FM, FN, WM, WN>(p, acc, lane, wm, wn, phase, b, 0, Cog, m0g, n0);
+        conv_epilogue_swz<FM, FN, WM, WN>(p, acc, lane, wm, wn, ophase, b, grp, Cog, m0g, n0);
     } else {
-        conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, phase, b, 0, Cog, m0g, n0);
+        conv_epilogue<FM, FN, WM, WN>(p, acc, lane, wm, wn, split, ophase, b, grp, Cog, m0g, n0);
     }
 #if RVC_CONV_STAMPS
     if (wave == 0) {
@@ -1213,17 +1218,26 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
 // reduce inside the conv launch -- plain slab stores, an agent release per split block, an acquire in the
 // last -- measured 11 % slower end to end, 780 vs 880 xRT on one box: each block's release writes back a
 // 64 KB+ partial tile and the last arriver sums up to 16 of them alone; profiles/r3_ab_splitk_fused_rmvpe_sa.txt.)
-__global__ void conv_splitk_reduce(ConvParams p) {
+// A block takes 256 columns x RED_ROWS rows (round 6: one row per block made a 576-row reduce 7k blocks, and with a
+// |max| cell 30k atomics; now one per block, amax_publish_block).  Same sums in the same split order.
+constexpr int RED_ROWS = 8;
+__global__ __launch_bounds__(256) void conv_splitk_reduce(ConvParams p) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t m = blockIdx.y;
     const int bp = blockIdx.z;
-    if (n >= p.ncols && !p.amax_out) return;  // (amax: every lane of the wave joins the shuffle)
     const int64_t sstride = p.B * p.nphase * p.Co * p.ncols;
-    const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + (n < p.ncols ? n : 0);
-    float s = 0.f;
-    for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
-    const float v = epilogue_store(p, s, bp / p.nphase, m, out_pos(p, n, bp % p.nphase));
-    if (p.amax_out) amax_publish(p.amax_out + (int64_t)(bp / p.nphase) * RVC_AMAX_SHARDS, fabsf(v));
+    float amx = 0.f;
+    if (n < p.ncols) {
+        const int t = out_pos(p, n, bp % p.nphase);
+        for (int r = 0; r < RED_ROWS; ++r) {
+            const int64_t m = (int64_t)blockIdx.y * RED_ROWS + r;
+            if (m >= p.Co) break;
+            const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + n;
+            float s = 0.f;
+            for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
+            amx = fmaxf(amx, fabsf(epilogue_store(p, s, bp / p.nphase, m, t)));
+        }
+    }
+    if (p.amax_out) amax_publish_block(p.amax_out + (int64_t)(bp / p.nphase) * RVC_AMAX_SHARDS, amx);
 }
 
 // The source-conv pass of a call with src_x (rvc_conv1d_args.src_*; the NSF generator's x = ups(x) + noise_convs(har),
@@ -1289,19 +1303,24 @@ __global__ __launch_bounds__(SRC_T) void src_add_kernel(SrcParams p) {
             acc[4 * q + 3] = fmaf(w4.w, xv, acc[4 * q + 3]);
         }
     }
+    // every y load first, then the stores: interleaved, hipcc kept each load behind the previous channel's store (it
+    // cannot prove the rows apart) -- 16 dependent round trips per thread
+    float yo[SRC_M];
+#pragma unroll
+    for (int mi = 0; mi < SRC_M; ++mi) yo[mi] = yb[(int64_t)(m0 + (mi < nm ? mi : 0)) * p.Lout];
     float amx = 0.f;
 #pragma unroll
     for (int mi = 0; mi < SRC_M; ++mi) {
         if (mi < nm) {
             const int m = m0 + mi;
-            const float v = (acc[mi] + (p.b ? p.b[m] : 0.f)) + yb[(int64_t)m * p.Lout];
+            const float v = (acc[mi] + (p.b ? p.b[m] : 0.f)) + yo[mi];
             if (ok) {
                 yb[(int64_t)m * p.Lout] = v;
                 amx = fmaxf(amx, fabsf(v));
             }
         }
     }
-    if (p.amax_out) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
+    if (p.amax_out) amax_publish_block(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
 }
 
 struct Cfg {
@@ -1390,6 +1409,7 @@ void fill_common(const rvc_conv1d_args* a, ConvParams& p) {
     p.stagger_blocks = 0;
     static const int swz_env = getenv("RVC_X6_SWZ") ? atoi(getenv("RVC_X6_SWZ")) : 1;
     p.swz = g_swz >= 0 ? g_swz : swz_env;
+    p.gx6 = 0;
 #if RVC_CONV_STAMPS
     p.stamps = g_stamps;
     p.stamp_blocks = g_stamp_blocks;
@@ -1454,6 +1474,9 @@ int max_tap_off(const rvc_conv1d_args* a) {
 // Taps per conv on the split-bf16 engine: CREPE's k=64 layers (CREPE.py:11-69) are the widest; the staged
 // span (BN - 1) * stride + (K - 1) * dil + 1 is checked against the loader's item budget below.
 constexpr int X6_K_MAX = 64;
+// grouped convs (ContentVec's pos_conv: 16 groups of 48 channels, k = 128) run one group per phase (ConvParams.gx6): stride
+// 1, plain stores, the image packed with the groups as phases (ops.Conv, make_images), no split-K, up to 128 taps
+constexpr int X6_K_MAX_GROUPED = 128;
 
 // stride 2 only with >= 32 input channels (ContentVec's feature extractor): the staged span doubles,
 // and the operand reads of even positions are 2-way bank conflicted
@@ -1462,11 +1485,16 @@ bool x6_eligible(const rvc_conv1d_args* a) {
     // RVC_X6_K1=0: the K = 1 GEMMs (ContentVec / TextEncoder linears) on the f32 MFMA engine instead (A/B switch)
     static const int k1 = getenv("RVC_X6_K1") ? atoi(getenv("RVC_X6_K1")) : 1;
     if (a->K == 1 && !k1) return false;
+    static const int grouped = getenv("RVC_X6_GROUPED") ? atoi(getenv("RVC_X6_GROUPED")) : 1;
+    const bool grp_ok = a->groups == 1 ||
+                        (grouped && a->stride == 1 && a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 &&
+                         !a->ntoff && !a->wrap && !a->src_x && a->Ci % a->groups == 0 && a->Co % a->groups == 0);
     return a->wx && a->Lin < (1 << 24) &&
-           (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && a->groups == 1 &&
-           a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) && a->K <= X6_K_MAX &&
+           (a->stride == 1 || (s2 && a->stride == 2 && a->Ci >= 32 && !a->ntoff)) && grp_ok &&
+           a->w_bstride == 0 && (!a->ntoff || a->ntoff == a->K) &&
+           a->K <= (a->groups == 1 ? X6_K_MAX : X6_K_MAX_GROUPED) &&
            (X6_BN - 1) * a->stride + max_tap_off(a) + 1 <= 64 * X6_NI_MAX - 2 && a->wx_nmf % 8 == 0 &&
-           (int64_t)a->wx_nmf * 16 >= a->Co && (a->wx_passes == 0 || a->wx_passes == 6 ||
+           (int64_t)a->wx_nmf * 16 >= a->Co / a->groups && (a->wx_passes == 0 || a->wx_passes == 6 ||
                                                 a->wx_passes == RVC_ARITH_FP32_SA || a->wx_passes == 3 ||
                                                 a->wx_passes == 1 || a->wx_passes == RVC_ARITH_F16X3);
 }
@@ -1539,8 +1567,16 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         p.wx_nmf = a->wx_nmf;
         p.wx_nch = (int)((Cig + 31) / 32);
         p.mtiles_per_group = (int)((Cog + BM - 1) / BM);
-        const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase;
+        const int64_t tiles = (int64_t)p.mtiles_per_group * ((ncols + BN - 1) / BN) * a->B * a->nphase * a->groups;
         split_k(p, tiles, p.wx_nch, cfg.WM * cfg.WN == 8 ? 1 : 2);
+        if (a->groups > 1) {  // groups as phases (gx6), each over its own Cig input / Cog output rows; never split-K
+            p.gx6 = 1;
+            p.nphase = a->groups;
+            p.Ci = Cig;
+            p.Co = Cog;
+            p.chunks_per_split = p.wx_nch;
+            p.ksplit = 1;
+        }
         lds = (size_t)2 * (p.wx_passes == 6 || p.wx_passes == RVC_ARITH_FP32_SA ? 3 : (p.wx_passes == 1 ? 1 : 2)) *
               p.span * 64 + 16;  // + the split-fp16 tile |max|
         // the tile epilogue (x6_tile_epilogue) for plain stores: one phase, output column = GEMM column, no 2-D border;
@@ -1556,8 +1592,9 @@ int plan(const rvc_conv1d_args* a, ConvParams& p, Cfg& cfg, dim3& grid, size_t& 
         const size_t tile_bytes = (size_t)BM * (BN + 4) * 4;
         const bool plain = a->nphase == 1 && a->ostride == 1 && a->ooffset == 0 && !a->wrap && !(p.dbg & 1) &&
                            BN <= 128;
-        p.tile_epi = !(tepi && plain) ? 0 : tile_bytes <= lds ? 1 : (cfg.WM % 2 == 0 && tile_bytes / 2 <= lds) ? 2 : 0;
-        grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * a->nphase * p.ksplit));
+        p.tile_epi = !(tepi && plain && a->groups == 1) ? 0
+                     : tile_bytes <= lds ? 1 : (cfg.WM % 2 == 0 && tile_bytes / 2 <= lds) ? 2 : 0;
+        grid = dim3(cdiv(ncols, BN), (unsigned)p.mtiles_per_group, (unsigned)(a->B * p.nphase * p.ksplit));
         RVC_CHECK_ARG(grid.y < 65536 && grid.z < 65536, "conv1d: grid too large");
         // staggered start (RVC_X6_STAGGER shader cycles) when the launch runs more than one round of blocks per CU
         static const int stagger = getenv("RVC_X6_STAGGER") ? atoi(getenv("RVC_X6_STAGGER")) : 0;
@@ -1831,7 +1868,8 @@ extern "C" int rvc_conv1d(const rvc_conv1d_args* a, void* ws, int64_t ws_bytes, 
     RVC_HIP(e);
     if (g_probe_event) RVC_HIP(hipEventRecord(g_probe_event, s));
     if (p.ksplit > 1) {
-        hipLaunchKernelGGL(conv_splitk_reduce, dim3(cdiv(p.ncols, 256), (unsigned)p.Co, (unsigned)(p.B * p.nphase)),
+        hipLaunchKernelGGL(conv_splitk_reduce,
+                           dim3(cdiv(p.ncols, 256), (unsigned)cdiv(p.Co, RED_ROWS), (unsigned)(p.B * p.nphase)),
                            dim3(256), 0, s, p);
         RVC_HIP(hipGetLastError());
     }

@@ -95,7 +95,7 @@ __global__ void textenc_embed_kernel(const float* lin, const float* emb, const i
         out[o] = v;
         m = fabsf(v);
     }
-    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, m);  // every lane (the wave's shuffles)
+    if (amax_out) amax_publish_block(amax_out + (int64_t)b * RVC_AMAX_SHARDS, m);  // one atomic per block
 }
 
 extern "C" int rvc_textenc_embed_amax(const float* lin, const float* emb, const int64_t* pitch, float* out, int64_t B,

@@ -56,7 +56,8 @@ struct rvc_ctx {
     bool fe_amax = true;      // RVC_AMD_FE_AMAX as contentvec.py: the feature extractor's convs through |max| cells
     bool fused_noise = true;  // RVC_AMD_FUSED_NOISE as synth.py: noise_convs fused into the upsampling convs
     bool attn_f16 = true;     // RVC_AMD_ATTN_F16 as contentvec.py / synth.py: QKV |max| cells, split-fp16 attention
-    bool te_amax = true;      // RVC_AMD_TE_AMAX as synth.py: the TextEncoder's and the flow's GEMMs through |max| cells
+    bool te_amax = false;     // RVC_AMD_TE_AMAX as synth.py: the TextEncoder's GEMMs through |max| cells (default off)
+    bool flow_amax = false;   // RVC_AMD_FLOW_AMAX as synth.py: the flow's (default off)
     Synth* syn = nullptr;
     ContentVec* cv = nullptr;
     Rmvpe* rm = nullptr;
@@ -230,17 +231,19 @@ inline int upload(ModelBase& m, const std::vector<float>& h, float** out) {
     return RVC_OK;
 }
 
-// the split-operand images (ops.pack_x6): ungrouped convs with <= 64 taps
+// the split-operand images (ops.pack_x6): ungrouped convs with <= 64 taps, grouped ones (the groups packed as phases,
+// conv1d.hip's gx6) with <= 128
 inline int make_images(rvc_ctx* c, ModelBase& m, ConvW& cw) {
-    if (!c->x6 || cw.groups != 1 || cw.K > 64) return RVC_OK;
-    const int64_t nb = rvc_conv1d_x6_bytes(cw.nphase, cw.Ci, cw.K, cw.Co);
-    const int64_t nh = rvc_conv1d_f16_bytes(cw.nphase, cw.Ci, cw.K, cw.Co);
+    if (!c->x6 || cw.K > (cw.groups == 1 ? 64 : 128) || (cw.groups > 1 && cw.nphase > 1)) return RVC_OK;
+    const int64_t np = cw.nphase * cw.groups, Ci = cw.Ci / cw.groups, Co = cw.Co / cw.groups;
+    const int64_t nb = rvc_conv1d_x6_bytes(np, Ci, cw.K, Co);
+    const int64_t nh = rvc_conv1d_f16_bytes(np, Ci, cw.K, Co);
     MCHECK(nb > 0 && nh > 0, "model load: bad conv shape %lld x %lld x %d", (long long)cw.Co, (long long)cw.Ci, cw.K);
     MTRY(dev_alloc(m, nb, &cw.wx_bf));
     MTRY(dev_alloc(m, nh, &cw.wx_hf));
     int nmf = 0;
-    MTRY(rvc_conv1d_pack_x6(cw.w, cw.nphase, cw.Ci, cw.K, cw.Co, cw.wx_bf, &nmf, nullptr));
-    MTRY(rvc_conv1d_pack_f16(cw.w, cw.nphase, cw.Ci, cw.K, cw.Co, cw.wx_hf, &nmf, nullptr));
+    MTRY(rvc_conv1d_pack_x6(cw.w, np, Ci, cw.K, Co, cw.wx_bf, &nmf, nullptr));
+    MTRY(rvc_conv1d_pack_f16(cw.w, np, Ci, cw.K, Co, cw.wx_hf, &nmf, nullptr));
     cw.nmf = nmf;
     return RVC_OK;
 }
@@ -455,6 +458,12 @@ struct Plan {
 inline bool env_on(const char* name) {
     const char* v = getenv(name);
     return !(v && strcmp(v, "0") == 0);
+}
+
+// a switch that is off unless set to something other than "0"
+inline bool env_set(const char* name) {
+    const char* v = getenv(name);
+    return v && strcmp(v, "0") != 0;
 }
 
 }  // namespace rvcm

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void layernorm_cf_kernel(const float* x, const
             amx = fmaxf(amx, fabsf(y));
         }
     }
-    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
+    if (amax_out) amax_publish_block(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // one atomic per block
 }
 
 // Register-resident form for the path's small column counts (ContentVec: 1599 columns, TextEncoder: 3198):
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(1024) void layernorm_cf_reg_kernel(const float* x, 
             amx = fmaxf(amx, fabsf(y));
         }
     }
-    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
+    if (amax_out) amax_publish_block(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // one atomic per block
 }
 
 extern "C" int rvc_layernorm_cf(const float* x, const float* res, const float* gamma, const float* beta, float* out,
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void fe0_apply_kernel(const float* x, int64_t 
             amx = fmaxf(amx, fabsf(o));
         }
     }
-    if (amax_out) amax_publish(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // every lane (the wave's shuffles)
+    if (amax_out) amax_publish_block(amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);  // one atomic per block
 }
 
 extern "C" int64_t rvc_fe0_ws_bytes(int64_t B, int64_t C, int64_t T) {

@@ -83,13 +83,17 @@ constexpr int RB_FM = RB_FM_;  // row fragments per compute wave
 constexpr int RB_FN = RB_FN_;  // column fragments per compute wave
 constexpr int RB_MAXSPAN = 64; // (K - 1) * dil bound (generator: 10 * 5 = 50)
 
-template <int C>
+template <int C, bool WIDE = false>
 struct RbGeom {
     // C = 128 (round 4): 2 row fragments per compute wave, so the 8 waves are 4 row groups x 2 column groups and
     // a tile is 112 outputs (not 48); its residual rows are read from x in the epilogue instead of LDS (the X and
     // T tiles alone take 157 KB at 2 split planes), and only the 1- and 2-plane pass sets fit (<= 3 passes)
-    static constexpr int FM = C >= 128 ? 2 : RB_FM;
-    static constexpr bool RLDS = C <= 64;        // residual rows staged in LDS
+    // WIDE (C = 64, round 6): the same 2 row fragments per wave -- 2 row groups x 4 column groups, 240 outputs per
+    // tile (not 112) -- so each B fragment read from LDS feeds twice the MFMAs (at 1 row fragment the 8 waves' B reads,
+    // 64 KB per k-step, outran the LDS's 128 B/clk: c1 / c2 ran at ~45 % of their MFMA bound, rb_stamps r6a) and the
+    // per-tile barriers / epilogues are amortised over twice the outputs; the residual from x as at C = 128
+    static constexpr int FM = (C >= 128 || WIDE) ? 2 : RB_FM;
+    static constexpr bool RLDS = C <= 64 && !WIDE;  // residual rows staged in LDS
     static constexpr int RF = C / 16;            // row fragments
     static constexpr int NCH = C / 32;           // 32-channel chunks
     static constexpr int RG = RF / FM;           // row groups
@@ -102,9 +106,9 @@ struct RbGeom {
     static constexpr int NI = (NCH * (TW + RB_MAXSPAN) * 4 + 255) / 256;  // loader items per thread
 };
 
-template <int C, int NP>
+template <int C, int NP, bool WIDE = false>
 size_t rb_lds_bytes(int K, int dil) {
-    using G = RbGeom<C>;
+    using G = RbGeom<C, WIDE>;
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     const int Wx = G::TW + (K - 1) * dil;
     return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (G::RLDS ? (size_t)C * G::RSTR * 4 : 0) + 64;  // + fp16 scales
@@ -114,15 +118,19 @@ size_t rb_lds_bytes(int K, int dil) {
 // |max| (they hold the whole tile in registers) and publish it per wave in LDS (slots by tile parity); c1's
 // epilogue takes the T tile's |max| over the 8 compute waves (one extra barrier per tile, B_T) before
 // splitting T; the c1 / c2 epilogues undo the weight-row and tile scales (powers of 2: exact).
-template <int C, int NP, bool F16>
-__global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
-    using G = RbGeom<C>;
+// x_ / y_: p.x / p.y again as __restrict__ kernel arguments (rb_check: x != y) -- so hipcc may issue the c2 epilogue's
+// residual / accumulate loads from x / y ahead of its stores to y; through the struct's pointers it kept each load
+// behind the previous store (32 dependent round trips per wave: 20k of a wide C = 64 tile's 85k cycles, r6e)
+template <int C, int NP, bool F16, bool WIDE>
+__global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const float* __restrict__ x_,
+                                                             float* __restrict__ y_) {
+    using G = RbGeom<C, WIDE>;
     static_assert(!F16 || NP == 3, "split-fp16: 3 passes");
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     constexpr int N = G::N, TW = G::TW, NCH = G::NCH, NF1 = G::NF1, NF2 = G::NF2, RSTR = G::RSTR;
     constexpr int FM = G::FM, FN = RB_FN;
-    constexpr bool YREG = RB_YREG && C <= 64;  // C = 128: no register room for the accumulate operands
-    static_assert(G::RLDS || NP <= 3, "C = 128: at most 2 split planes fit LDS");
+    constexpr bool YREG = RB_YREG && C <= 64 && !WIDE;  // 2 row fragments: no register room for the accumulate operands
+    static_assert(G::RLDS || NP <= 3, "C = 128 / WIDE: at most 2 split planes fit LDS");
     extern __shared__ uint4 lds[];
     const int K = p.K, d = p.dil, L = p.L;
     const int hk = (K - 1) / 2;
@@ -163,7 +171,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
         auto xload = [&](int tile) __attribute__((always_inline)) {
             const int cb = tile / ntc;
             const int base = (tile - cb * ntc) * N - H;
-            const float* xb = p.x + (int64_t)cb * C * L;
+            const float* xb = x_ + (int64_t)cb * C * L;
 #pragma unroll
             for (int it = 0; it < G::NI; ++it) {
                 int ch, g8, pos;
@@ -245,7 +253,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
             if constexpr (G::RLDS && F16) {
                 const int cb = tile / ntc;
                 const int n0 = (tile - cb * ntc) * N;
-                float* yb = p.y + (int64_t)cb * C * L;
+                float* yb = y_ + (int64_t)cb * C * L;
                 // (not unrolled over the items: unrolled, hipcc batched every item's LDS reads and store addresses and
                 // the loader registers set the kernel's count -- 51 spilled VGPRs at C = 64)
 #pragma unroll 1
@@ -371,8 +379,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     int ch = 0, t = 0, k = 0;
     float yold[YREG ? FM : 1][YREG ? FN : 1][4];
     int n0 = 0;
-    float* yb = p.y;  // the current tile's clip
-    const float* xres = p.x;  // C = 128: the current tile's clip of x, the residual
+    float* yb = y_;  // the current tile's clip
+    const float* xres = x_;  // C = 128 / WIDE: the current tile's clip of x, the residual
     // F16: row reciprocal scales of both images (after each image), the x tile's and T tile's reciprocals
     const float* rs1 = reinterpret_cast<const float*>(p.w1x + (int64_t)K * NCH * p.nmf1 * 3 * 64);
     const float* rs2 = reinterpret_cast<const float*>(p.w2x + (int64_t)K * NCH * p.nmf2 * 3 * 64);
@@ -395,8 +403,8 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                     const int g = (int)blockIdx.x + k * (int)gridDim.x;
                     const int cb = g / ntc;
                     n0 = (g - cb * ntc) * N;
-                    yb = p.y + (int64_t)cb * C * L;
-                    xres = p.x + (int64_t)cb * C * L;
+                    yb = y_ + (int64_t)cb * C * L;
+                    xres = x_ + (int64_t)cb * C * L;
                     __syncthreads();  // S0(k)
                     if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k, RB_NOW());
 #pragma unroll
@@ -497,6 +505,58 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                 if (two && last_ch) {
                     if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 4, RB_NOW());
                     // ---- c2 epilogue: + bias, + residual (from R) (+ accumulate) -> y
+                    if constexpr (!G::RLDS) {
+                        // residual from x (C = 128, WIDE): per row fragment, bias in place, then every residual (and
+                        // accumulate) load at once from clamped addresses, then the masked stores -- the same
+                        // operations per element in the same order.  The per-element form (guarded load, add, store)
+                        // kept each load behind the previous store's branch: 32 dependent round trips per wave, 20k
+                        // of a wide C = 64 tile's 85k cycles (rb_stamps r6e)
+#pragma unroll
+                        for (int i = 0; i < FM; ++i) {
+                            const int m0 = (rg * FM + i) * 16 + 4 * lg;
+                            int qc[FN];
+#pragma unroll
+                            for (int j = 0; j < FN; ++j) {
+                                const int q = n0 + (cg * FN + j) * 16 + ln;
+                                qc[j] = q < L ? q : L - 1;
+                            }
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const float f = F16 ? rs2[m0 + r] * t_rs : 1.f, bb = p.b2[m0 + r];
+#pragma unroll
+                                for (int j = 0; j < FN; ++j) acc[i][j][r] = (F16 ? acc[i][j][r] * f : acc[i][j][r]) + bb;
+                            }
+                            float tmp[FN][4];
+#pragma unroll
+                            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) tmp[j][r] = xres[(int64_t)(m0 + r) * L + qc[j]];
+#pragma unroll
+                            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] + tmp[j][r];
+                            if (p.accumulate) {
+#pragma unroll
+                                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                                    for (int r = 0; r < 4; ++r)
+                                        tmp[j][r] = YREG ? yold[i][j][r] : yb[(int64_t)(m0 + r) * L + qc[j]];
+#pragma unroll
+                                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                                    for (int r = 0; r < 4; ++r) acc[i][j][r] += tmp[j][r];
+                            }
+#pragma unroll
+                            for (int j = 0; j < FN; ++j) {
+                                const int col = (cg * FN + j) * 16 + ln;
+                                const int q = n0 + col;
+                                if (cg * FN + j < NF2 && col < N && q < L) {
+#pragma unroll
+                                    for (int r = 0; r < 4; ++r) yb[(int64_t)(m0 + r) * L + q] = acc[i][j][r];
+                                }
+                            }
+                        }
+                    } else {
 #pragma unroll
                     for (int i = 0; i < FM; ++i) {
                         const int m0 = (rg * FM + i) * 16 + 4 * lg;
@@ -517,6 +577,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
                             }
                         }
                     }
+                    }
                     if (RVC_CONV_STAMPS && wave == 0 && k < RB_STAMP_NT) RB_STAMP(8 * k + 5, RB_NOW());
                 }
             }
@@ -534,7 +595,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p) {
     if (wave == 0) RB_STAMP(253, RB_NOW());
 }
 
-template <int C, int NP, bool F16 = false>
+template <int C, int NP, bool F16 = false, bool WIDE = false>
 int launch_rb(const RbParams& p, hipStream_t s) {
     static int ncu = 0;
     if (!ncu) {
@@ -543,19 +604,20 @@ int launch_rb(const RbParams& p, hipStream_t s) {
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         if (ncu <= 0) ncu = 256;
     }
-    const size_t lds = rb_lds_bytes<C, NP>(p.K, p.dil);
+    const size_t lds = rb_lds_bytes<C, NP, WIDE>(p.K, p.dil);
     static bool attr = false;
     if (!attr) {
-        RVC_HIP(hipFuncSetAttribute((const void*)resblock_x6_kernel<C, NP, F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024));
+        RVC_HIP(hipFuncSetAttribute((const void*)resblock_x6_kernel<C, NP, F16, WIDE>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     // workgroups per CU: 1 = persistent; more = shorter tile runs that the dispatcher hands to CUs as they free
     // up (a CU held by a concurrent stream's kernel then delays fewer tiles)
     static const int per_cu = getenv("RVC_RB_PER_CU") ? atoi(getenv("RVC_RB_PER_CU")) : 1;
-    const int ntiles = p.B * ((p.L + RbGeom<C>::N - 1) / RbGeom<C>::N);
+    const int ntiles = p.B * ((p.L + RbGeom<C, WIDE>::N - 1) / RbGeom<C, WIDE>::N);
     const int nwg = ncu * (per_cu > 0 ? per_cu : 1);
-    hipLaunchKernelGGL((resblock_x6_kernel<C, NP, F16>), dim3(ntiles < nwg ? ntiles : nwg), dim3(768), lds, s, p);
+    hipLaunchKernelGGL((resblock_x6_kernel<C, NP, F16, WIDE>), dim3(ntiles < nwg ? ntiles : nwg), dim3(768), lds, s, p,
+                       p.x, p.y);
     RVC_HIP(hipGetLastError());
     return RVC_OK;
 }
@@ -575,9 +637,19 @@ int rb_check(const rvc_resblock_args* a) {
     return RVC_OK;
 }
 
+// the wide C = 64 geometry (RbGeom WIDE) for the <= 2-plane pass sets (RVC_RB_WIDE64=0: 1 row fragment per wave, the
+// round-5 form; rvc_resblock_set_wide64)
+static thread_local int g_rb_wide64 = -1;
+bool rb_wide64(int passes) {
+    static const int env = getenv("RVC_RB_WIDE64") ? atoi(getenv("RVC_RB_WIDE64")) : 1;
+    return (g_rb_wide64 >= 0 ? g_rb_wide64 : env) && passes != 6;
+}
+
 }  // namespace
 
 extern "C" int64_t rvc_resblock_lds_bytes(int64_t C, int K, int dil, int passes) {
+    if (C == 64 && rb_wide64(passes))
+        return passes == 1 ? rb_lds_bytes<64, 1, true>(K, dil) : rb_lds_bytes<64, 3, true>(K, dil);
     if (passes == RVC_ARITH_F16X3) passes = 3;  // same planes
     if (C == 32) return passes == 6 ? rb_lds_bytes<32, 6>(K, dil) : passes == 3 ? rb_lds_bytes<32, 3>(K, dil)
                                                                                 : rb_lds_bytes<32, 1>(K, dil);
@@ -624,10 +696,21 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
         if (a->passes == 3) return launch_rb<128, 3>(p, s);
         return launch_rb<128, 1>(p, s);
     }
+    if (rb_wide64(a->passes)) {
+        if (a->passes == RVC_ARITH_F16X3) return launch_rb<64, 3, true, true>(p, s);
+        if (a->passes == 3) return launch_rb<64, 3, false, true>(p, s);
+        return launch_rb<64, 1, false, true>(p, s);
+    }
     if (a->passes == RVC_ARITH_F16X3) return launch_rb<64, 3, true>(p, s);
     if (a->passes == 6) return launch_rb<64, 6>(p, s);
     if (a->passes == 3) return launch_rb<64, 3>(p, s);
     return launch_rb<64, 1>(p, s);
+}
+
+extern "C" int rvc_resblock_set_wide64(int on) {
+    const int prev = g_rb_wide64;
+    g_rb_wide64 = on < 0 ? -1 : (on ? 1 : 0);
+    return prev;
 }
 
 extern "C" int rvc_resblock_set_ylds(int on) {

@@ -167,21 +167,24 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         CallOpts o;
         MTRY(conv(c, S, S.emb_phone, phone_cf, T, lin, o, s));
     }
-    // |max| cells (synth.py TE_AMAX): one memset for the TextEncoder's and the flow's, then the flow's 1.0 cell
+    // |max| cells (synth.py text_encoder / flow_reverse): the QKV projections' (attn_f16), the TextEncoder's others
+    // (te_amax) and the flow's (flow_amax); one memset for all, then the flow's 1.0 cell
     const int64_t nl = (int64_t)S.layers.size();
-    unsigned* tcells = c->te_amax ? reinterpret_cast<unsigned*>(A + bf.tcell) : nullptr;
+    unsigned* cbase = reinterpret_cast<unsigned*>(A + bf.tcell);
+    unsigned* tcells = c->te_amax ? cbase : nullptr;
     auto tcell = [&](int64_t k) { return tcells ? tcells + RVC_AMAX_SHARDS * k : nullptr; };
-    if (tcells) {
-        MHIP(hipMemsetAsync(tcells, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * (1 + 5 * nl + 1 + 5 * 4), s));
-        MHIP(hipMemsetD32Async((hipDeviceptr_t)tcell(1 + 5 * nl), 0x3F800000, 1, s));  // 1.0f: |tanh * sigmoid| < 1
+    auto fcell = [&](int64_t k) { return c->flow_amax ? cbase + RVC_AMAX_SHARDS * k : nullptr; };
+    if (c->te_amax || c->flow_amax || c->attn_f16) {
+        MHIP(hipMemsetAsync(cbase, 0, sizeof(unsigned) * RVC_AMAX_SHARDS * (1 + 5 * nl + 1 + 5 * 4), s));
+        MHIP(hipMemsetD32Async((hipDeviceptr_t)(cbase + RVC_AMAX_SHARDS * (1 + 5 * nl)), 0x3F800000, 1, s));  // 1.0f
     }
     MTRY(rvc_textenc_embed_amax(lin, S.emb_pitch, pitch, x, 1, H, T, (float)sqrt((double)H), 0.1f, tcell(0), s));
     const unsigned* te_cell = tcell(0);  // the current x's
     const float scale = (float)(1.0 / sqrt((double)kc));
     for (int64_t li = 0; li < nl; ++li) {
         const Layer& Ly = S.layers[li];
-        unsigned *c_qkv = tcell(1 + 5 * li), *c_o = tcell(2 + 5 * li), *c_l1 = tcell(3 + 5 * li),
-                 *c_f1 = tcell(4 + 5 * li), *c_l2 = tcell(5 + 5 * li);
+        unsigned *c_qkv = c->attn_f16 ? cbase + RVC_AMAX_SHARDS * (1 + 5 * li) : nullptr, *c_o = tcell(2 + 5 * li),
+                 *c_l1 = tcell(3 + 5 * li), *c_f1 = tcell(4 + 5 * li), *c_l2 = tcell(5 + 5 * li);
         CallOpts o;
         o.amax_in = te_cell;
         o.amax_out = c_qkv;
@@ -215,7 +218,7 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
         MCHECK(need >= 0, "rvc_synth_infer: attention shape H=%lld D=%lld T=%lld unsupported", (long long)nh,
                (long long)kc, (long long)T);
         MTRY(ensure_ws(S, need, s));
-        MTRY(rvc_attention_ex(&at, c->attn_f16 ? c_qkv : nullptr, c_o, need ? S.ws : nullptr, need, s));
+        MTRY(rvc_attention_ex(&at, c_qkv, c_o, need ? S.ws : nullptr, need, s));
         CallOpts oo;
         oo.amax_in = c_o;
         MTRY(conv(c, S, Ly.o, ob, T, tmp, oo, s));
@@ -250,13 +253,14 @@ int synth_one(rvc_ctx* c, const float* phone, const int64_t* pitch, const float*
     float *h = A + bf.h, *acts = A + bf.acts, *outacc = A + bf.outacc, *xin = A + bf.xin;
     float* bufs[2] = {A + bf.fb0, A + bf.fb1};
     float* xf_cur = zp;
-    // the flow's |max| cells (synth.py flow_reverse): after the TextEncoder's, the 1.0 cell then 5 per flow
-    const unsigned* unit = tcell(1 + 5 * nl);
+    // the flow's |max| cells (synth.py flow_reverse): after the TextEncoder's, the 1.0 cell (|tanh * sigmoid| < 1) then
+    // 5 per flow
+    const unsigned* unit = fcell(1 + 5 * nl);
     const unsigned* post_cell = nullptr;
     for (int f = 3, n = 0; f >= 0; --f, ++n) {
         const Flow& F = S.flows[f];
-        unsigned* c_h[3] = {tcell(2 + 5 * nl + 5 * n), tcell(3 + 5 * nl + 5 * n), tcell(4 + 5 * nl + 5 * n)};
-        unsigned *c_acc = tcell(5 + 5 * nl + 5 * n), *c_post = tcell(6 + 5 * nl + 5 * n);
+        unsigned* c_h[3] = {fcell(2 + 5 * nl + 5 * n), fcell(3 + 5 * nl + 5 * n), fcell(4 + 5 * nl + 5 * n)};
+        unsigned *c_acc = fcell(5 + 5 * nl + 5 * n), *c_post = fcell(6 + 5 * nl + 5 * n);
         float* xf = (xf_cur != bufs[0]) ? bufs[0] : bufs[1];
         MTRY(rvc_flip_channels(xf_cur, xf, 1, I, T, s));
         float *x0 = xf, *x1 = xf + half * T;
@@ -464,7 +468,8 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->fe_amax = env_on("RVC_AMD_FE_AMAX");
     c->fused_noise = env_on("RVC_AMD_FUSED_NOISE");
     c->attn_f16 = env_on("RVC_AMD_ATTN_F16");
-    c->te_amax = env_on("RVC_AMD_TE_AMAX");
+    c->te_amax = env_set("RVC_AMD_TE_AMAX");
+    c->flow_amax = env_set("RVC_AMD_FLOW_AMAX");
     *out = c;
     return RVC_OK;
 }

@@ -133,6 +133,7 @@ SIGNATURES = {
     "rvc_conv1d_set_stamps": [c_void_p, c_int64],
     "rvc_resblock_set_stamps": [c_void_p, c_int64],
     "rvc_resblock_set_ylds": [c_int],
+    "rvc_resblock_set_wide64": [c_int],
     "rvc_conv1d_set_tile_epi": [c_int],
     "rvc_conv1d_set_swz": [c_int],
     "rvc_conv1d_set_f16_fast": [c_int],

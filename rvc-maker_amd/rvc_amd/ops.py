@@ -171,8 +171,8 @@ def pack_x6(w_km: torch.Tensor, nphase: int, Ci: int, K: int, Co: int):
 
 
 class Conv:
-    """A packed Conv1d (weight [Co, Ci/g, K], bias [Co]) resident on the device.  Ungrouped convs also
-    carry the split-bf16 image, which the library uses for stride-1 calls."""
+    """A packed Conv1d (weight [Co, Ci/g, K], bias [Co]) resident on the device, with the split-operand images
+    (pack_x6) the library's engine reads."""
 
     def __init__(self, w, b=None, groups=1, device="cuda"):
         self.Co, self.Cig, self.K = (int(s) for s in w.shape)
@@ -180,10 +180,15 @@ class Conv:
         self.Ci = self.Cig * groups
         self.w = pack_km(w.float(), groups).to(device)
         self.b = b.float().to(device) if b is not None else None
-        # the split-bf16 engine takes ungrouped convs with <= 64 taps (X6_K_MAX / x6_eligible in conv1d.hip;
-        # CREPE's k=64 layers are the widest)
-        self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co) if groups == 1 and self.K <= 64 \
-            else (None, 0)
+        # the split-operand engine takes ungrouped convs with <= 64 taps (X6_K_MAX / x6_eligible in conv1d.hip;
+        # CREPE's k=64 layers are the widest) and grouped ones with <= 128 (ContentVec's pos_conv), whose image holds
+        # the groups as phases (ConvParams.gx6)
+        if groups == 1 and self.K <= 64:
+            self.wx, self.wx_nmf = pack_x6(self.w, 1, self.Ci, self.K, self.Co)
+        elif groups > 1 and self.K <= 128:
+            self.wx, self.wx_nmf = pack_x6(self.w, groups, self.Cig, self.K, self.Co // groups)
+        else:
+            self.wx, self.wx_nmf = None, 0
 
     def __call__(self, x, Lout=None, stride=1, pad=0, dil=1, **kw):
         return conv1d(x, self.w, self.Ci, self.Co, self.K, bias=self.b, stride=stride, pad=pad, dil=dil,

@@ -37,11 +37,17 @@ AMAX_PER_STAGE = 16
 # round 6: noise_convs[i](har) fused into ups[i]'s epilogue (x = ups(x) + noise_convs(har), synthesizers.py:156: one
 # launch writes the stage input once, the same bits); RVC_AMD_FUSED_NOISE=0: the separate accumulating launch (A/B)
 FUSED_NOISE = os.environ.get("RVC_AMD_FUSED_NOISE", "1") != "0"
-# round 6: the TextEncoder's rel-pos attention in split-fp16 from the QKV projection's |max| (contentvec.ATTN_F16)
+# round 6: the TextEncoder's rel-pos attention in split-fp16 from the QKV projection's |max| (contentvec.ATTN_F16): the
+# TextEncoder alone, 30 s, 2.89 -> 2.64 ms (scripts/synth_stage_time.py, r6d)
 ATTN_F16 = os.environ.get("RVC_AMD_ATTN_F16", "1") != "0"
-# round 6: the TextEncoder's and the flow's GEMMs in split-fp16 from their producers' |max| cells (RVC_AMD_TE_AMAX=0: the
-# 6-pass split-bf16 form of round 5; rvc_model.cpp reads the same switch)
-TE_AMAX = os.environ.get("RVC_AMD_TE_AMAX", "1") != "0"
+# round 6: the TextEncoder's GEMMs in split-fp16 from their producers' |max| cells (the embedding's, every LayerNorm's,
+# ffn1's, the attention's) -- off by default: on these 192-channel, 3000-frame GEMMs split-fp16 ran slower than the
+# 6-pass split-bf16 form (TextEncoder alone 2.14 -> 2.64 ms; clip stream 979 -> 949 xRT with the flow's below, r6d).
+# Kept as RVC_AMD_TE_AMAX=1 (tested); the QKV projection publishes its cell for the attention either way.
+TE_AMAX = os.environ.get("RVC_AMD_TE_AMAX", "0") != "0"
+# ... and the flow's (RVC_AMD_FLOW_AMAX=1; off by default: flow^-1 alone 0.93 -> 1.50 ms with it, r6d; rvc_model.cpp
+# reads both switches)
+FLOW_AMAX = os.environ.get("RVC_AMD_FLOW_AMAX", "0") != "0"
 
 
 def fold_weight_norm(weight: dict) -> dict:
@@ -146,12 +152,13 @@ class SynthesizerAMD:
         H, dev, nh, kc = self.hidden, phone_cf.device, self.n_heads, self.kc
         lin = self.emb_phone(phone_cf.reshape(B, -1, T))
         x = torch.empty(B, H, T, device=dev)
-        # |max| cells (round 6, TE_AMAX): the embedding and every LayerNorm, the QKV projection (-> split-fp16
-        # attention), the attention output (its rel-v band kernel publishes) and ffn1 publish, and the GEMM reading each
-        # runs split-fp16 from it; cell 0 the embedding's, then per layer (qkv, o, ln1, ffn1, ln2)
+        # |max| cells (round 6): the QKV projection's (ATTN_F16: the split-fp16 attention's scale) and, with TE_AMAX, the
+        # embedding's, every LayerNorm's, the attention output's (its rel-v band kernel publishes) and ffn1's, the GEMM
+        # reading each then running split-fp16 from it; cell 0 the embedding's, then per layer (qkv, o, ln1, ffn1, ln2)
         nl = len(self.layers)
-        cells = ops.AmaxSlots(1 + 5 * nl, dev, B) if TE_AMAX else None
-        cell = (lambda k: cells[k]) if cells is not None else (lambda k: None)
+        cells = ops.AmaxSlots(1 + 5 * nl, dev, B) if (TE_AMAX or ATTN_F16) else None
+        cell = (lambda k: cells[k]) if (cells is not None and TE_AMAX) else (lambda k: None)
+        qkv_cell = (lambda li: cells[1 + 5 * li]) if (cells is not None and ATTN_F16) else (lambda li: None)
         ops.textenc_embed(lin, self.emb_pitch if pitch is not None else None, pitch, x, B, H, T, math.sqrt(H), 0.1,
                           amax_out=cell(0))
         x_cell = cell(0)
@@ -161,7 +168,8 @@ class SynthesizerAMD:
         rk = torch.empty(B, nh, 21, T, device=dev)
         scale = 1.0 / math.sqrt(kc)
         for li, L in enumerate(self.layers):
-            c_qkv, c_o, c_l1, c_f1, c_l2 = (cell(1 + 5 * li + k) for k in range(5))
+            c_o, c_l1, c_f1, c_l2 = (cell(2 + 5 * li + k) for k in range(4))
+            c_qkv = qkv_cell(li)
             qkv = L["qkv"](x, amax_in=x_cell, amax_out=c_qkv)
             for b in range(B):  # Rk of clip b's heads: one K=1 conv over its nh query slices
                 L["relk"](qkv[b] if B > 1 else qkv, B=nh, Lin=T, x_bstride=kc * T, Lout=T, out_scale=scale,
@@ -170,7 +178,7 @@ class SynthesizerAMD:
             ops.attention(qb, qb[:, H:], qb[:, 2 * H:], o, B=B, H=nh, D=kc, T=T, ldc=T, q_hs=kc * T,
                           k_hs=kc * T, v_hs=kc * T, o_hs=kc * T, q_bs=3 * H * T, k_bs=3 * H * T, v_bs=3 * H * T,
                           o_bs=H * T, scale=scale, rk=rk, ev=L["ev"], ml=ml, W=10,
-                          amax_in=c_qkv if ATTN_F16 else None, amax_out=c_o)
+                          amax_in=c_qkv, amax_out=c_o)
             y = L["o"](o, out=tmp, amax_in=c_o)
             ops.layernorm_cf(x, y, L["ln1"][0], L["ln1"][1], x, B, H, T, amax_out=c_l1)
             h = L["ffn1"](x, pad=(self.ksz - 1) // 2, out_act=ACT_RELU, amax_in=c_l1, amax_out=c_f1)
@@ -188,10 +196,10 @@ class SynthesizerAMD:
         h = torch.empty(B, H, T, device=dev)
         acts = torch.empty(B, H, T, device=dev)
         out_acc = torch.empty(B, H, T, device=dev)
-        # |max| cells (round 6, TE_AMAX): per flow the WaveNet's h (pre, then each rs_a), the skip sum (the last rs_b) and
+        # |max| cells (round 6, FLOW_AMAX): per flow the WaveNet's h (pre, then each rs_a), the skip sum (the last rs_b) and
         # post's output x1 (the next flow's pre input, flipped) publish; the gate's output is tanh * sigmoid, |.| < 1,
         # so the res/skip convs take a constant 1.0 cell (cell 0)
-        cells = ops.AmaxSlots(1 + 5 * 4, dev, B) if TE_AMAX else None
+        cells = ops.AmaxSlots(1 + 5 * 4, dev, B) if FLOW_AMAX else None
         cell = (lambda k: cells[k]) if cells is not None else (lambda k: None)
         if cells is not None:
             cells[0].view(B, ops.AMAX_SHARDS)[:, 0].fill_(0x3F800000)  # 1.0f

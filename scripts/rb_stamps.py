@@ -23,7 +23,7 @@ SHAPES = [("c64_k3_d1", 64, 3, 1, 767520), ("c64_k7_d3", 64, 7, 3, 767520), ("c6
           ("c32_k3_d1", 32, 3, 1, 1535040), ("c32_k7_d3", 32, 7, 3, 1535040), ("c32_k11_d5", 32, 11, 5, 1535040)]
 
 
-def analyse(st, C, K, passes):
+def analyse(st, C, K, passes, wide):
     ok = st[:, 248] > 0
     st = st[ok].astype(np.float64)
     nt = int(np.median(st[:, 251]))
@@ -46,7 +46,9 @@ def analyse(st, C, K, passes):
     nch = C // 32
     f16 = passes == 16
     np_ = 3 if passes in (3, 16) else passes
-    fm, fn = 1, 4
+    fm, fn = (2 if C == 128 or (C == 64 and wide) else 1), 4  # RbGeom: row fragments per wave (WIDE at C = 64)
+    rg = C // 16 // fm
+    med["outputs_per_tile"] = 16 * (4 * (8 // rg) - 1)
     mfma = 2 * nch * K * fm * fn * np_ * 16  # per SIMD per conv: 2 compute waves per SIMD
     med["mfma_bound_per_conv"] = mfma
     med["mfma_busy_tile"] = 2 * mfma / max(med["tile"], 1)
@@ -59,6 +61,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--wide64", type=int, default=1, help="the C = 64 geometry (rvc_resblock_set_wide64)")
     args = ap.parse_args()
     from rvc_amd import _lib, ops
     from rvc_amd.ops import Conv
@@ -69,7 +72,8 @@ def main():
     import ctypes
     if lib.rvc_resblock_set_stamps(ctypes.c_void_p(buf.data_ptr()), buf.numel() * 8) != 0:
         raise SystemExit("this library has no stamps: build with EXTRA=-DRVC_CONV_STAMPS=1")
-    print("lib:", _lib.LIB_PATH, "precision:", args.precision)
+    lib.rvc_resblock_set_wide64(args.wide64)
+    print("lib:", _lib.LIB_PATH, "precision:", args.precision, "wide64:", args.wide64)
     g = torch.Generator().manual_seed(0)
     out = {}
     from torch.profiler import ProfilerActivity, profile
@@ -88,15 +92,17 @@ def main():
         kn = [e for e in prof.events() if "resblock_x6_kernel" in e.name]
         us = kn[0].time_range.elapsed_us() if kn else float("nan")
         st = buf.view(nb, W).cpu().numpy().astype(np.uint64)
-        r = analyse(st, C, K, ops.rb_passes(K))
+        r = analyse(st, C, K, ops.rb_passes(K), args.wide64 and ops.rb_passes(K) != 6)
         r.update(kernel_us=us, tflops=4.0 * C * C * K * L / us / 1e6, passes=ops.rb_passes(K))
         out[name] = r
-        print(f"{name:11s} {us:7.1f} us {r['tflops']:6.1f} TF  tiles/block {r['tiles_per_block']}  tile {r['tile']:.0f} cyc "
+        print(f"{name:11s} {us:7.1f} us {r['tflops']:6.1f} TF  tiles/block {r['tiles_per_block']} x {r['outputs_per_tile']}"
+              f"  tile {r['tile']:.0f} cyc "
               f"(MFMA-bound {2 * r['mfma_bound_per_conv']}, busy {r['mfma_busy_tile']:.2f}):  S0 wait {r['s0_wait']:.0f}"
               f" | c1 {r['c1']:.0f} | c1 epi->B_T {r['c1_epi_to_BT']:.0f} | T + S1 {r['T_write_S1']:.0f} | c2 {r['c2']:.0f}"
               f" | c2 epi {r['c2_epi']:.0f};  loader: loads issued +{r['loader_load_issue']:.0f}, staged "
               f"{r['loader_stage']:.0f}")
     lib.rvc_resblock_set_stamps(None, 0)
+    lib.rvc_resblock_set_wide64(-1)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(out, f, indent=1)

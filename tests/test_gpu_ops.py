@@ -76,6 +76,33 @@ def test_conv1d(ops, engine, case):
     close(y, ref)
 
 
+@pytest.mark.parametrize("case", [(768, 768, 128, 64, 16, 1599, 2, False), (768, 768, 128, 64, 16, 333, 1, True),
+                                  (256, 256, 16, 8, 4, 1000, 2, True), (96, 96, 5, 2, 3, 777, 1, False)])
+def test_conv1d_grouped_x6(ops, case):
+    """Grouped convs on the split-operand engine, one group per phase (conv1d.hip gx6): ContentVec's pos_conv epilogue
+    (GELU, + x, SamePad's dropped last column via Lout) over a clip batch, with and without the input's |max| cell
+    (Cig = 64: the fast loader form), against torch fp32; the output cell holds max |y| per clip."""
+    Ci, Co, K, p, g, L, B, cell_in = case
+    x = torch.randn(B, Ci, L, generator=gen(30))
+    w = torch.randn(Co, Ci // g, K, generator=gen(31)) / math.sqrt(Ci // g * K)
+    b = torch.randn(Co, generator=gen(32)) * 0.1
+    Lout = L
+    ref = F.gelu(F.conv1d(x, w, b, 1, p, 1, g)[..., :Lout]) + x
+    c = ops.Conv(w, b, groups=g)
+    xd = x.to(DEV)
+    cells = ops.AmaxSlots(2, DEV, B)
+    if cell_in:
+        cells[0].view(B, ops.AMAX_SHARDS)[:, 0] = torch.tensor(
+            [float(x[i].abs().max()) for i in range(B)]).view(torch.int32).to(DEV)
+    y = c(xd if B > 1 else xd[0], pad=p, Lout=Lout, out_act=ops.ACT_GELU, res=xd if B > 1 else xd[0],
+          amax_in=cells[0] if cell_in else None, amax_out=cells[1])
+    assert ops.LAST_CONV_ENGINE == 1 and ops.LAST_CONV_WS == 0
+    close(y.view(B, Co, Lout), ref)
+    torch.cuda.synchronize()
+    for i in range(B):
+        assert ops.amax_value(cells[1], i) == float(y.view(B, Co, Lout)[i].abs().max().cpu())
+
+
 @pytest.mark.parametrize("prec,lo,hi", [("bf16x3", 0.0, 1e-4), ("bf16", 1e-4, 1e-2)])
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] == 1 and c[6] == 1 and c[2] <= 16])
 def test_conv1d_reduced_precision(ops, case, prec, lo, hi):

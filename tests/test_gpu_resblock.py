@@ -133,6 +133,7 @@ def test_fused_pair_outputs_through_lds_bit_identical(C, K, d, L, B):
     acc0 = torch.randn(B, C, L, generator=g).to(DEV)
     lib = ops._lib.load()
     outs = []
+    prev = lib.rvc_resblock_set_wide64(0)  # the LDS output path is the narrow C = 64 geometry's
     for on in (0, 1):
         lib.rvc_resblock_set_ylds(on)
         try:
@@ -145,5 +146,46 @@ def test_fused_pair_outputs_through_lds_bit_identical(C, K, d, L, B):
             outs.append((y.cpu(), ya.cpu()))
         finally:
             lib.rvc_resblock_set_ylds(-1)
+    lib.rvc_resblock_set_wide64(prev)
     assert torch.equal(outs[0][0], outs[1][0]) and not torch.isnan(outs[1][0]).any()
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("K,d", [(3, 1), (7, 3), (11, 5)])
+@pytest.mark.parametrize("L,B", [(5003, 1), (1, 1), (239, 1), (240, 1), (241, 1), (481, 2), (3001, 3)])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+def test_fused_pair_wide64(K, d, L, B, precision):
+    """Round 6: the C = 64 pair with 2 row fragments per wave (240 outputs per tile, residual from x) against the narrow
+    form (1 row fragment, 112 outputs) -- bit-identical at bf16x3 / bf16 (no tile scales), within split-fp16's 2e-5 of
+    the fp32 reference at "fp32" (its power-of-2 tile scales follow the tile) -- plain and accumulating, ragged and
+    single-column lengths, batched clips."""
+    C = 64
+    w, c1, c2 = make_pair(C, K, seed=K * 7 + d + L)
+    g = torch.Generator().manual_seed(L * 3 + B)
+    x = torch.randn(B, C, L, generator=g).to(DEV)
+    acc0 = torch.randn(B, C, L, generator=g).to(DEV)
+    lib = ops._lib.load()
+    outs = []
+    for wide in (0, 1):
+        prev = lib.rvc_resblock_set_wide64(wide)
+        try:
+            with ops.precision(precision):
+                y = torch.full_like(x, float("nan"))
+                ops.resblock_pair(x if B > 1 else x[0], y if B > 1 else y[0], c1, c2, d, 0.1)
+                ya = acc0.clone()
+                ops.resblock_pair(x if B > 1 else x[0], ya if B > 1 else ya[0], c1, c2, d, 0.1, accumulate=True)
+            torch.cuda.synchronize()
+            outs.append((y.cpu(), ya.cpu()))
+        finally:
+            lib.rvc_resblock_set_wide64(prev)
+    assert not torch.isnan(outs[1][0]).any()
+    if precision == "fp32":
+        for b in range(B):
+            r = torch_ref(x[b].cpu(), w, K, d)
+            tol = 2e-5 * max(1.0, r.abs().max().item())
+            for o in outs:
+                assert (o[0][b] - r).abs().max().item() <= tol
+                assert (o[1][b] - (r + acc0[b].cpu())).abs().max().item() <= tol + 2e-6 * acc0.abs().max().item()
+    else:
+        assert torch.equal(outs[0][0], outs[1][0])
+        assert torch.equal(outs[0][1], outs[1][1])

@@ -16,9 +16,18 @@ def rms(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2)))
 
 
+# the TextEncoder / flow |max| switches (synth.py): the defaults, every cell on, and the f32 attention without cells
+SWITCHES = {"default": {}, "cells_on": dict(TE_AMAX=True, FLOW_AMAX=True, ATTN_F16=True),
+            "cells_off": dict(TE_AMAX=False, FLOW_AMAX=False, ATTN_F16=False)}
+
+
+@pytest.mark.parametrize("sw", list(SWITCHES))
 @pytest.mark.parametrize("name", ["synth_48k_v2", "synth_40k_v2", "synth_32k_v1"])
-def test_synth_infer_matches_reference_golden(golden, name):
+def test_synth_infer_matches_reference_golden(golden, name, sw, monkeypatch):
+    from rvc_amd import synth
     from rvc_amd.synth import SynthesizerAMD
+    for k, v in SWITCHES[sw].items():
+        monkeypatch.setattr(synth, k, v)
     g = golden(name)
     ck = synthetic.make_synth_ckpt(int(g["sr"]), str(g["version"]), seed=int(g["seed"]))
     net = SynthesizerAMD(ck, DEV)
