@@ -1219,25 +1219,71 @@ __global__ __launch_bounds__(64 * (WM * WN + 4), (x6_min_blocks<FM, FN, WM * WN,
 // last -- measured 11 % slower end to end, 780 vs 880 xRT on one box: each block's release writes back a
 // 64 KB+ partial tile and the last arriver sums up to 16 of them alone; profiles/r3_ab_splitk_fused_rmvpe_sa.txt.)
 // A block takes 256 columns x RED_ROWS rows (round 6: one row per block made a 576-row reduce 7k blocks, and with a
-// |max| cell 30k atomics; now one per block, amax_publish_block).  Same sums in the same split order.
+// |max| cell 30k atomics; now one per block, amax_publish_block).  Every load is issued ahead of the stores it could
+// alias (the RED_ROWS rows' partials per split, then their residual / accumulate operands from clamped addresses): the
+// per-element form waited one round trip per split and per row.  Same sums in the same split order, and the epilogue of
+// epilogue_store per element.
 constexpr int RED_ROWS = 8;
 __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvParams p) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int bp = blockIdx.z;
+    const int bp = blockIdx.z, b = bp / p.nphase;
+    const int64_t m0 = (int64_t)blockIdx.y * RED_ROWS;
+    const int nr = p.Co - m0 < RED_ROWS ? (int)(p.Co - m0) : RED_ROWS;
+    const bool okn = n < p.ncols;
+    const int t = okn ? out_pos(p, n, bp % p.nphase) : -1;
     const int64_t sstride = p.B * p.nphase * p.Co * p.ncols;
+    const float* src = p.ws + ((int64_t)bp * p.Co + m0) * p.ncols + (okn ? n : 0);
+    float s[RED_ROWS];
+#pragma unroll
+    for (int r = 0; r < RED_ROWS; ++r) s[r] = 0.f;
+    for (int k = 0; k < p.ksplit; ++k) {
+        float v[RED_ROWS];
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) v[r] = src[k * sstride + (int64_t)(r < nr ? r : nr - 1) * p.ncols];
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) s[r] += v[r];
+    }
+    const bool ok = t >= 0;
+    const int64_t Lo = p.Lout;
+    float v[RED_ROWS];
+    int64_t o[RED_ROWS];
+#pragma unroll
+    for (int r = 0; r < RED_ROWS; ++r) {
+        const int64_t m = m0 + (r < nr ? r : nr - 1);
+        o[r] = m * Lo + (ok ? t : 0);
+        float x = s[r];
+        if (p.bias) x += p.bias[m];
+        if (p.bias2) x += p.bias2[m];
+        v[r] = act_apply(x, p.out_act, p.out_slope) * p.out_scale;
+    }
+    if (p.res) {
+        float rr[RED_ROWS];
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) rr[r] = p.res[b * p.res_bstride + o[r]];
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) v[r] += rr[r];
+    }
+    float* yb = p.y + b * p.y_bstride;
+    if (p.accumulate) {
+        float aa[RED_ROWS];
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) aa[r] = yb[o[r]];
+#pragma unroll
+        for (int r = 0; r < RED_ROWS; ++r) v[r] += aa[r];
+    }
     float amx = 0.f;
-    if (n < p.ncols) {
-        const int t = out_pos(p, n, bp % p.nphase);
-        for (int r = 0; r < RED_ROWS; ++r) {
-            const int64_t m = (int64_t)blockIdx.y * RED_ROWS + r;
-            if (m >= p.Co) break;
-            const float* src = p.ws + ((int64_t)bp * p.Co + m) * p.ncols + n;
-            float s = 0.f;
-            for (int k = 0; k < p.ksplit; ++k) s += src[k * sstride];
-            amx = fmaxf(amx, fabsf(epilogue_store(p, s, bp / p.nphase, m, t)));
+#pragma unroll
+    for (int r = 0; r < RED_ROWS; ++r) {
+        if (r < nr) {
+            if (ok) {
+                yb[o[r]] = v[r];
+                amx = fmaxf(amx, fabsf(v[r]));
+            } else if (t <= -2) {
+                yb[(m0 + r) * Lo + (-t - 2)] = 0.f;  // 2-D border cell
+            }
         }
     }
-    if (p.amax_out) amax_publish_block(p.amax_out + (int64_t)(bp / p.nphase) * RVC_AMAX_SHARDS, amx);
+    if (p.amax_out) amax_publish_block(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
 }
 
 // The source-conv pass of a call with src_x (rvc_conv1d_args.src_*; the NSF generator's x = ups(x) + noise_convs(har),
