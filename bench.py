@@ -23,7 +23,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement): metric/value = 
 audio-seconds per wall-second for the whole job, plus "roofline" for the dominant kernel
 family (the split-operand MFMA conv engine: conv_x6_kernel + the fused ResBlock pairs; algorithmic FLOPs over the
 device's own kernel stamps of one instrumented per-call pass, torch.profiler, with the HIP-event time beside it),
-its "families" (attention on the f32 MFMA, the BiGRU's us per step against its hand-off floor, and the HBM GB/s of
+its "families" (attention -- split-fp16 or f32 MFMA --, the BiGRU's us per step against its hand-off floor, and the HBM GB/s of
 LayerNorm / fe0 / STFT / filtfilt), and "cpu_baseline" (the torch-CPU oracle on a bounded clip, rank 0, N=1 only).
 """
 from __future__ import annotations
@@ -256,6 +256,7 @@ def _pass_set(name):
 
 # kernel families beside the split-operand conv engine (the roofline's "families"): name prefix -> family
 FAMILY_KERNELS = (("attn_fwd_kernel<64>", "attention_d64"), ("attn_combine_kernel<64>", "attention_d64"),
+                  ("attn_f16_kernel<64>", "attention_d64"), ("attn_f16_kernel<96>", "attention_d96"),
                   ("attn_fwd_kernel<96>", "attention_d96"), ("attn_combine_kernel<96>", "attention_d96"),
                   ("attn_relv_band_kernel", "attention_d96"), ("bigru", "bigru"), ("layernorm_cf", "layernorm"),
                   ("fe0_", "fe0"), ("filt_", "filtfilt"), ("stft_mag_kernel", "stft"))
@@ -268,7 +269,8 @@ BIGRU_FLOOR_US = 1.43
 def profiler_kernel_times(fn, families=None):
     """{pass set: (launches, device ms)} of the split-operand kernels one call of ``fn`` launches, from
     torch.profiler's device records; None when the profiler is unavailable (or rocprofv3 already traces).
-    ``families`` (a dict) receives {family: [launches, device ms]} of the FAMILY_KERNELS of the same call."""
+    ``families`` (a dict) receives {family: [launches, device ms, matched prefixes]} of the FAMILY_KERNELS of the same
+    call."""
     if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
         return None
     try:
@@ -283,9 +285,10 @@ def profiler_kernel_times(fn, families=None):
             if families is not None:
                 for pre, fam in FAMILY_KERNELS:
                     if name.startswith(pre):
-                        g = families.setdefault(fam, [0, 0.0])
+                        g = families.setdefault(fam, [0, 0.0, set()])
                         g[0] += 1
                         g[1] += e.time_range.elapsed_us() * 1e-3
+                        g[2].add(pre)
                         break
             if not (name.startswith("conv_x6_kernel<") or name.startswith("resblock_x6_kernel<")):
                 continue
@@ -312,16 +315,21 @@ def family_rooflines(aux, fam_ms):
     for fam, (fl, by, calls, T) in sorted(tot.items()):
         if fam not in fam_ms:
             continue
-        n, ms = fam_ms[fam]
+        n, ms, kinds = fam_ms[fam]
         e = {"calls": calls, "launches": n, "kernel_ms": round(ms, 4)}
         if fam.startswith("attention"):
             tf = fl / (ms * 1e-3) / 1e12
-            e.update(bound="mfma", achieved=round(tf, 2), peak=PEAK_F32_MFMA_TFLOPS, unit="TFLOP/s",
-                     frac=round(tf / PEAK_F32_MFMA_TFLOPS, 4), gflop=round(fl / 1e9, 2),
+            # split-fp16 (attn_f16_kernel, round 6): 3 fp16 MFMA passes per product -> 2.5 PF / 3 f32-equivalent
+            f16 = any(k.startswith("attn_f16") for k in kinds)
+            peak = PEAK_MFMA16_TFLOPS / 3 if f16 else PEAK_F32_MFMA_TFLOPS
+            engine = ("split-fp16 flash attention (hH + hL + lH on v_mfma_f32_16x16x32_f16, scales from the QKV "
+                      "projection's |max| cell; peak = 2.5 PF / 3)" if f16 else
+                      "flash attention on the f32 MFMA (v_mfma_f32_16x16x4_f32), split-KV + combine")
+            e.update(bound="mfma", achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s",
+                     frac=round(tf / peak, 4), gflop=round(fl / 1e9, 2),
                      kernel=("ContentVec MHA 12 x 64 (fairseq.py:355)" if fam == "attention_d64" else
                              "TextEncoder rel-pos MHA 2 x 96, window 10, + its rel-v band kernel (synthesizers.py:227-251)")
-                     + ": flash attention on the f32 MFMA (v_mfma_f32_16x16x4_f32), split-KV + combine; FLOPs = "
-                       "4 T^2 D per head (+ the relative band)")
+                     + ": " + engine + "; FLOPs = 4 T^2 D per head (+ the relative band)")
         elif fam == "bigru":
             us = ms * 1e3 / max(T, 1)
             e.update(bound="latency", unit="us/step", achieved=round(us, 3), floor=BIGRU_FLOOR_US,

@@ -490,18 +490,20 @@ def test_x6_f16_fast_loader_bit_identical(ops, Ci, Co, K, d, L, act):
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
 
 
-@pytest.mark.parametrize("B,N", [(1, 16000 * 3 + 123), (2, 8000), (1, 400)])
-def test_fe0_gn_gelu(ops, B, N):
+@pytest.mark.parametrize("B,N,C,K,S", [(1, 16000 * 3 + 123, 512, 10, 5), (2, 8000, 512, 10, 5), (1, 400, 512, 10, 5),
+                                       (1, 9001, 4096, 16, 8), (2, 3000, 100, 3, 1)])
+def test_fe0_gn_gelu(ops, B, N, C, K, S):
     """ContentVec's first layer fused (rvc_fe0_gn_gelu: conv 1 -> 512, k10 s5, GroupNorm(512, 512), GELU) against
-    torch's f64 evaluation of the reference's layers (fairseq.py:1165-1195)."""
+    torch's f64 evaluation of the reference's layers (fairseq.py:1165-1195); and at the entry's limits (the widest
+    layer, K = 16 taps, stride 8; a ragged last channel group)."""
     g = gen(21)
     wav = torch.randn(B, N, generator=g) * 0.3
-    w = torch.randn(512, 1, 10, generator=g) * 0.3
-    gamma, beta = torch.rand(512, generator=g) + 0.5, torch.randn(512, generator=g) * 0.1
-    y = F.conv1d(wav.double().unsqueeze(1), w.double(), None, 5)
-    ref = F.gelu(F.group_norm(y, 512, gamma.double(), beta.double(), 1e-5))
+    w = torch.randn(C, 1, K, generator=g) * 0.3
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    y = F.conv1d(wav.double().unsqueeze(1), w.double(), None, S)
+    ref = F.gelu(F.group_norm(y, C, gamma.double(), beta.double(), 1e-5))
     c = ops.Conv(w, None)
-    out = ops.fe0_gn_gelu(wav.to(DEV).contiguous(), c.w, gamma.to(DEV), beta.to(DEV), B, N, 512, 10, 5)
+    out = ops.fe0_gn_gelu(wav.to(DEV).contiguous(), c.w, gamma.to(DEV), beta.to(DEV), B, N, C, K, S)
     got = out.cpu().double().reshape(ref.shape)
     assert (got - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
