@@ -488,8 +488,11 @@ def cpu_baseline(seconds=30.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    # 12 clips per timed stream (round 6; 5 before): the stream's fill -- clip 1's front end with nothing under it, the
+    # last clip's synthesizer alone -- is ~11 ms, so the value grows with K (one box, r6h: 1013 xRT at 5 clips, 1053-1064
+    # at 12); 12 x 30 s clips still time in ~0.35 s
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-call", action="store_true", help="skip the per-call comparison after a clip stream")

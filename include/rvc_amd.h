@@ -143,7 +143,8 @@ int rvc_conv1d_set_stamps(void* buf, int64_t bytes);
 int rvc_resblock_set_stamps(void* buf, int64_t bytes);
 /* The fused pair's output path for this thread's launches (round 6): 1 = split-fp16 pairs at C <= 64 write c2's results
  * into LDS (over the tile's residual rows) and the loader waves store them during the next tile (the compute waves go
- * straight on), 0 = the compute waves' own global stores, -1 = RVC_RB_YLDS (default 1).  Same bits either way. */
+ * straight on); 2 = the same, and at C = 32 (two R buffers by tile parity) after the next tile's c1 barriers instead of
+ * before them; 0 = the compute waves' own global stores; -1 = RVC_RB_YLDS (default 2).  Same bits in every form. */
 int rvc_resblock_set_ylds(int on);
 /* The fused pair's C = 64 tiling for this thread's launches (round 6): 1 = 2 row fragments per compute wave, 240
  * outputs per tile (the <= 2-plane pass sets; 6-pass pairs keep the narrow form), 0 = 1 row fragment, 112 outputs,

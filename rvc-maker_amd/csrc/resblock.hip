@@ -106,12 +106,18 @@ struct RbGeom {
     static constexpr int NI = (NCH * (TW + RB_MAXSPAN) * 4 + 255) / 256;  // loader items per thread
 };
 
+// R buffers: C = 32 with 2 split planes (round 6) keeps two by tile parity, so the loader waves store tile k - 1's outputs
+// (YLDS) after S1(k) instead of before the c1 epilogue's barrier -- there its 40 stores queued ahead of the next tile's
+// 40 loads in vmcnt and the loaders reached B_T late (the K = 3 pair's critical path, rb_stamps r6f); 3 planes: no room
+template <int C, int NP>
+constexpr int rb_nr() { return C == 32 && NP == 3 ? 2 : 1; }
+
 template <int C, int NP, bool WIDE = false>
 size_t rb_lds_bytes(int K, int dil) {
     using G = RbGeom<C, WIDE>;
     constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
     const int Wx = G::TW + (K - 1) * dil;
-    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (G::RLDS ? (size_t)C * G::RSTR * 4 : 0) + 64;  // + fp16 scales
+    return (size_t)G::NCH * (Wx + G::TW) * NPL * 64 + (G::RLDS ? (size_t)rb_nr<C, NP>() * C * G::RSTR * 4 : 0) + 64;  // + scales
 }
 
 // F16 (with NP = 3): split-fp16 operands (x6_common.h split2h).  The loader waves take each staged x tile's
@@ -138,8 +144,10 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const f
     const int Wx = TW + (K - 1) * d;
     uint4* Xs = lds;                          // [NCH][Wx][NPL][4]
     uint4* Ts = Xs + NCH * Wx * NPL * 4;      // [NCH][TW][NPL][4]
-    float* Rs = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [C][RSTR] (C <= 64)
-    float* xmax = Rs + (G::RLDS ? C * RSTR : 0);  // F16: [2 tile parities][4 loader waves] x tile |max|
+    float* Rs0 = reinterpret_cast<float*>(Ts + NCH * TW * NPL * 4);  // [NR][C][RSTR] (C <= 64)
+    constexpr int NR = rb_nr<C, NP>();
+    auto Rbuf = [&](int k) __attribute__((always_inline)) { return Rs0 + (NR == 2 ? (k & 1) * C * RSTR : 0); };
+    float* xmax = Rs0 + (G::RLDS ? NR * C * RSTR : 0);  // F16: [2 tile parities][4 loader waves] x tile |max|
     float* tmaxs = xmax + 8;      // F16: [8 compute waves] T tile |max|
     const int ntc = (L + N - 1) / N;  // time tiles per clip
     const int ntiles = p.B * ntc;
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const f
                 }
             }
         };
-        auto rstore = [&]() __attribute__((always_inline)) {  // raw residual rows of the staged tile
+        auto rstore = [&](float* Rs) __attribute__((always_inline)) {  // raw residual rows of the staged tile
             if constexpr (!G::RLDS) return;
 #pragma unroll
             for (int it = 0; it < G::NI; ++it) {
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const f
         // YLDS: tile k's finished outputs sit in R (the compute waves' c2 epilogue wrote them in place of the residual
         // rows) until S0(k + 1); each loader thread stores exactly the R elements its own items cover and then writes
         // its next residual values to those same elements (no hazard between threads), rows coalesced over the lanes
-        auto ystore = [&](int tile) __attribute__((always_inline)) {
+        auto ystore = [&](int tile, const float* Rs) __attribute__((always_inline)) {
             if constexpr (G::RLDS && F16) {
                 const int cb = tile / ntc;
                 const int n0 = (tile - cb * ntc) * N;
@@ -276,11 +284,12 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const f
             }
         };
         const bool ylds = G::RLDS && F16 && p.ylds;  // block-uniform
+        const bool ylate = ylds && NR == 2 && p.ylds == 2;  // two R buffers: tile k - 1's stores after S1(k)
         if (my_n > 0) xstore(blockIdx.x);
         for (int k = 0; k < my_n; ++k) {
             __syncthreads();  // S0(k): X(k) staged; R free (YLDS: R holds tile k - 1's outputs)
-            if (ylds && k > 0) ystore(blockIdx.x + (k - 1) * gridDim.x);
-            rstore();         // R(k) from the registers still holding tile k
+            if (ylds && !ylate && k > 0) ystore(blockIdx.x + (k - 1) * gridDim.x, Rbuf(k - 1));
+            rstore(Rbuf(k));  // R(k) from the registers still holding tile k
             const bool more = k + 1 < my_n;
             // unconditional (the last tile reloads itself): every path issues the same loads, which keeps
             // hipcc's vmcnt bookkeeping exact across the loop (a guarded load made it wait vmcnt(0))
@@ -293,11 +302,13 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const f
             __syncthreads();  // S1(k): c1 of tile k done -> X free
             if constexpr (F16) take_scale((k + 1) & 1);
             if (more) xstore(blockIdx.x + (k + 1) * gridDim.x);
+            // two R buffers: tile k - 1's outputs (its buffer is rewritten only by rstore(k + 1), after S0(k + 1))
+            if (ylate && k > 0) ystore(blockIdx.x + (k - 1) * gridDim.x, Rbuf(k - 1));
             if (wave == 8 && k < RB_STAMP_NT) RB_STAMP(8 * k + 7, RB_NOW());
         }
         if (ylds) {
             __syncthreads();  // S_end: the last tile's outputs in R
-            if (my_n > 0) ystore(blockIdx.x + (my_n - 1) * gridDim.x);
+            if (my_n > 0) ystore(blockIdx.x + (my_n - 1) * gridDim.x, Rbuf(my_n - 1));
         }
         return;
     }
@@ -568,10 +579,10 @@ __global__ __launch_bounds__(768, 1) void resblock_x6_kernel(RbParams p, const f
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
                                     float v = (F16 ? acc[i][j][r] * (rs2[m0 + r] * t_rs) : acc[i][j][r]) + p.b2[m0 + r];
-                                    if constexpr (G::RLDS) v = v + Rs[(m0 + r) * RSTR + col];
+                                    if constexpr (G::RLDS) v = v + Rbuf(k)[(m0 + r) * RSTR + col];
                                     else v = v + xres[(int64_t)(m0 + r) * L + q];
                                     if (p.accumulate) v += YREG ? yold[i][j][r] : yb[(int64_t)(m0 + r) * L + q];
-                                    if (G::RLDS && F16 && ylds_c) Rs[(m0 + r) * RSTR + col] = v;  // the loaders store it
+                                    if (G::RLDS && F16 && ylds_c) Rbuf(k)[(m0 + r) * RSTR + col] = v;  // the loaders store it
                                     else yb[(int64_t)(m0 + r) * L + q] = v;
                                 }
                             }
@@ -678,7 +689,9 @@ extern "C" int rvc_resblock_pair(const rvc_resblock_args* a, rvc_stream_t stream
     p.slope = a->slope;
     p.B = a->B > 1 ? a->B : 1;
     // the outputs through LDS (split-fp16 at C <= 64; RVC_RB_YLDS=0: the compute waves' own global stores, A/B switch)
-    static const int ylds = getenv("RVC_RB_YLDS") ? atoi(getenv("RVC_RB_YLDS")) : 1;
+    // (2, the default: with C = 32's two R buffers the loaders store tile k - 1 after S1(k) -- 1 keeps them before the
+    // c1 epilogue's barrier, the round-6 first form; same bits)
+    static const int ylds = getenv("RVC_RB_YLDS") ? atoi(getenv("RVC_RB_YLDS")) : 2;
     p.ylds = g_rb_ylds >= 0 ? g_rb_ylds : ylds;
 #if RVC_CONV_STAMPS
     p.stamps = g_rb_stamps;
@@ -714,7 +727,7 @@ extern "C" int rvc_resblock_set_wide64(int on) {
 }
 
 extern "C" int rvc_resblock_set_ylds(int on) {
-    g_rb_ylds = on < 0 ? -1 : (on ? 1 : 0);
+    g_rb_ylds = on < 0 ? -1 : (on > 2 ? 2 : on);
     return RVC_OK;
 }
 

@@ -125,8 +125,9 @@ def test_fused_pair_f16x3(C, K, d, scale):
 @pytest.mark.parametrize("L,B", [(5003, 1), (241, 1), (16, 1), (3001, 3)])
 def test_fused_pair_outputs_through_lds_bit_identical(C, K, d, L, B):
     """Round 6: the split-fp16 pair's outputs go through LDS (over the tile's residual rows) and the loader waves store
-    them during the next tile (rvc_resblock_set_ylds).  Same bits as the compute waves' own stores -- plain and
-    accumulating, ragged last tile, fewer tiles than workgroups, batched clips."""
+    them during the next tile (rvc_resblock_set_ylds 1; 2: at C = 32 from two R buffers by tile parity, after the next
+    tile's c1 barriers).  Same bits as the compute waves' own stores -- plain and accumulating, ragged last tile, fewer
+    tiles than workgroups, batched clips."""
     w, c1, c2 = make_pair(C, K, seed=C + K + d + L)
     g = torch.Generator().manual_seed(L + B)
     x = torch.randn(B, C, L, generator=g).to(DEV)
@@ -134,7 +135,7 @@ def test_fused_pair_outputs_through_lds_bit_identical(C, K, d, L, B):
     lib = ops._lib.load()
     outs = []
     prev = lib.rvc_resblock_set_wide64(0)  # the LDS output path is the narrow C = 64 geometry's
-    for on in (0, 1):
+    for on in (0, 1, 2):
         lib.rvc_resblock_set_ylds(on)
         try:
             with ops.precision("f16x3"):
@@ -147,8 +148,9 @@ def test_fused_pair_outputs_through_lds_bit_identical(C, K, d, L, B):
         finally:
             lib.rvc_resblock_set_ylds(-1)
     lib.rvc_resblock_set_wide64(prev)
-    assert torch.equal(outs[0][0], outs[1][0]) and not torch.isnan(outs[1][0]).any()
-    assert torch.equal(outs[0][1], outs[1][1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0]) and not torch.isnan(o[0]).any()
+        assert torch.equal(outs[0][1], o[1])
 
 
 @pytest.mark.parametrize("K,d", [(3, 1), (7, 3), (11, 5)])
