@@ -224,11 +224,17 @@ __device__ __forceinline__ int af_vs(int r, int q, int u) {
     return r * 16 + 8 * (q ^ (r & 1)) + (u ^ (r & 7));
 }
 
+// Round 6, second form: at D = 64 each wave owns 32 queries as two 16-query fragments (af_qf), so every K / V operand
+// read from LDS feeds both (the 16-query form read 32 KB of LDS per wave per key tile for 48 MFMAs: LDS-bound at 2
+// waves per SIMD); a block is 4 waves = af_qb queries.  D = 96 keeps one fragment (two spill 37 VGPRs).
+constexpr int af_qf(int D) { return D == 64 ? 2 : 1; }
+constexpr int af_qb(int D) { return 64 * af_qf(D); }
 template <int D>
 __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
     constexpr int NC = D / 32;        // 32-channel chunks: k-steps of S^T
     constexpr int NF = D / 16;        // output channel fragments
     constexpr int VI = D * 8 / 256;   // V staging items (channel row, key octet) per thread
+    constexpr int QF = af_qf(D);      // query fragments per wave
     static_assert(D % 32 == 0 && (D * 8) % 256 == 0, "D = 64 or 96");
     __shared__ uint4 Ks[NC * AF_KT * 8];
     __shared__ uint4 Vs[D * 16];
@@ -238,8 +244,10 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
     const int split = blockIdx.z % p.S, b = blockIdx.z / p.S;
     const int64_t T = p.T;
     const int lq = lane & 15, lg = lane >> 4;
-    const int64_t q0 = (int64_t)blockIdx.x * 64 + wave * 16;
-    const int64_t qa = q0 + lq;
+    const int64_t q0 = (int64_t)blockIdx.x * af_qb(D) + wave * 16 * QF;
+    int64_t qa[QF];  // this lane's query in fragment g
+#pragma unroll
+    for (int g = 0; g < QF; ++g) qa[g] = q0 + 16 * g + lq;
     const int64_t kbeg = (int64_t)split * p.kps;
     const int64_t kend = kbeg + p.kps < T ? kbeg + p.kps : T;
     const float* Q = p.q + b * p.q_bs + h * p.q_hs;
@@ -253,11 +261,12 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
     const float s_un = ldexpf(1.f, -(eq + ek));
     const float o_un = ldexpf(1.f, -(ev + 14));
 
-    // Q' as the B operand of every S^T fragment (loop-invariant): chunk c, lane (query lq, group lg) -> channels
-    // 32 c + 8 lg .. + 7
-    uint4 qh[NC], ql[NC];
-    {
-        const int64_t qc = qa < T ? qa : T - 1;
+    // Q' as the B operand of every S^T fragment (loop-invariant): fragment g, chunk c, lane (query lq, group lg) ->
+    // channels 32 c + 8 lg .. + 7
+    uint4 qh[QF][NC], ql[QF][NC];
+#pragma unroll
+    for (int g = 0; g < QF; ++g) {
+        const int64_t qc = qa[g] < T ? qa[g] : T - 1;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             float v[8];
@@ -266,8 +275,8 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
             uint32_t hw[4], lw[4];
 #pragma unroll
             for (int e2 = 0; e2 < 4; ++e2) split2h_pk(v[2 * e2], v[2 * e2 + 1], hw[e2], lw[e2]);
-            qh[c] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-            ql[c] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+            qh[g][c] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+            ql[g][c] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
         }
     }
 
@@ -324,10 +333,17 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
         }
     };
 
-    floatx4 acc_o[NF];
+    floatx4 acc_o[QF][NF];
 #pragma unroll
-    for (int f = 0; f < NF; ++f) acc_o[f] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float m_run = -INFINITY, l_run = 0.f;
+    for (int g = 0; g < QF; ++g)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc_o[g][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m_run[QF], l_run[QF];
+#pragma unroll
+    for (int g = 0; g < QF; ++g) {
+        m_run[g] = -INFINITY;
+        l_run[g] = 0.f;
+    }
     const float* RK = p.rk ? p.rk + ((int64_t)b * p.H + h) * (2 * p.W + 1) * T : nullptr;
 
     gload(kbeg);
@@ -336,75 +352,89 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
     for (int64_t kt = kbeg; kt < kend; kt += AF_KT) {
         const bool more = kt + AF_KT < kend;
         if (more) gload(kt + AF_KT);
-        // S^T fragments: rows = keys af_key(f, .), columns = this wave's 16 queries
-        floatx4 s[4];
+        // S^T fragments: rows = keys af_key(f, .), columns = query fragment g's 16 queries; each K operand read once
+        floatx4 s[QF][4];
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
             const int krow = af_key(f, lq);
-            floatx4 a4 = floatx4{0.f, 0.f, 0.f, 0.f};
+            floatx4 a4[QF];
+#pragma unroll
+            for (int g = 0; g < QF; ++g) a4[g] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 const uint4 ah = Ks[c * AF_KT * 8 + af_ks(krow, 0, lg)];
                 const uint4 al = Ks[c * AF_KT * 8 + af_ks(krow, 1, lg)];
-                a4 = mfma_f16(ah, qh[c], a4);
-                a4 = mfma_f16(ah, ql[c], a4);
-                a4 = mfma_f16(al, qh[c], a4);
+#pragma unroll
+                for (int g = 0; g < QF; ++g) {
+                    a4[g] = mfma_f16(ah, qh[g][c], a4[g]);
+                    a4[g] = mfma_f16(ah, ql[g][c], a4[g]);
+                    a4[g] = mfma_f16(al, qh[g][c], a4[g]);
+                }
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s[f][r] = a4[r] * s_un;
+            for (int g = 0; g < QF; ++g)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[g][f][r] = a4[g][r] * s_un;
         }
-        // element (f, r) of this lane: key kt + af_key(f, 4 lg + r), query qa
-        if (RK && kt - (q0 + 15) <= p.W && kt + AF_KT - 1 - q0 >= -p.W) {
+        // element (g, f, r) of this lane: key kt + af_key(f, 4 lg + r), query qa[g]
+        if (RK && kt - (q0 + 16 * QF - 1) <= p.W && kt + AF_KT - 1 - q0 >= -p.W) {
+#pragma unroll
+            for (int g = 0; g < QF; ++g)
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t key = kt + af_key(f, 4 * lg + r);
+                        const int64_t d = key - qa[g];
+                        const bool in = d >= -p.W && d <= p.W && qa[g] < T && key < T;
+                        const float rv = RK[(in ? d + p.W : 0) * T + (qa[g] < T ? qa[g] : 0)];
+                        s[g][f][r] += in ? rv : 0.f;
+                    }
+        }
+        uint4 ph[QF][2], pl[QF][2];
+        float alpha[QF];
+#pragma unroll
+        for (int g = 0; g < QF; ++g) {
+            float mloc = -INFINITY;
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int64_t key = kt + af_key(f, 4 * lg + r);
-                    const int64_t d = key - qa;
-                    const bool in = d >= -p.W && d <= p.W && qa < T && key < T;
-                    const float rv = RK[(in ? d + p.W : 0) * T + (qa < T ? qa : 0)];
-                    s[f][r] += in ? rv : 0.f;
+                    if (kt + af_key(f, 4 * lg + r) >= kend) s[g][f][r] = -INFINITY;
+                    mloc = fmaxf(mloc, s[g][f][r]);
                 }
-        }
-        float mloc = -INFINITY;
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+            const float m_new = fmaxf(m_run[g], mloc);
+            alpha[g] = expf(m_run[g] - m_new);
+            float lsum = 0.f;
 #pragma unroll
-        for (int f = 0; f < 4; ++f)
+            for (int f = 0; f < 4; ++f)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                if (kt + af_key(f, 4 * lg + r) >= kend) s[f][r] = -INFINITY;
-                mloc = fmaxf(mloc, s[f][r]);
+                for (int r = 0; r < 4; ++r) {
+                    const float e = expf(s[g][f][r] - m_new);
+                    s[g][f][r] = e;
+                    lsum += e;
+                }
+            lsum += __shfl_xor(lsum, 16, 64);
+            lsum += __shfl_xor(lsum, 32, 64);
+            l_run[g] = l_run[g] * alpha[g] + lsum;
+            m_run[g] = m_new;
+            // P^T as the B operand of key step st: keys 32 st + 8 lg + i = fragment 2 st (i < 4) / 2 st + 1 (i >= 4)
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                uint32_t hw[4], lw[4];
+                split2h_pk(s[g][2 * st][0] * 16384.f, s[g][2 * st][1] * 16384.f, hw[0], lw[0]);
+                split2h_pk(s[g][2 * st][2] * 16384.f, s[g][2 * st][3] * 16384.f, hw[1], lw[1]);
+                split2h_pk(s[g][2 * st + 1][0] * 16384.f, s[g][2 * st + 1][1] * 16384.f, hw[2], lw[2]);
+                split2h_pk(s[g][2 * st + 1][2] * 16384.f, s[g][2 * st + 1][3] * 16384.f, hw[3], lw[3]);
+                ph[g][st] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+                pl[g][st] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
             }
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        const float m_new = fmaxf(m_run, mloc);
-        const float alpha = expf(m_run - m_new);
-        float lsum = 0.f;
 #pragma unroll
-        for (int f = 0; f < 4; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float e = expf(s[f][r] - m_new);
-                s[f][r] = e;
-                lsum += e;
-            }
-        lsum += __shfl_xor(lsum, 16, 64);
-        lsum += __shfl_xor(lsum, 32, 64);
-        l_run = l_run * alpha + lsum;
-        m_run = m_new;
-        // P^T as the B operand of key step st: keys 32 st + 8 lg + i = fragment 2 st (i < 4) / 2 st + 1 (i >= 4)
-        uint4 ph[2], pl[2];
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            uint32_t hw[4], lw[4];
-            split2h_pk(s[2 * st][0] * 16384.f, s[2 * st][1] * 16384.f, hw[0], lw[0]);
-            split2h_pk(s[2 * st][2] * 16384.f, s[2 * st][3] * 16384.f, hw[1], lw[1]);
-            split2h_pk(s[2 * st + 1][0] * 16384.f, s[2 * st + 1][1] * 16384.f, hw[2], lw[2]);
-            split2h_pk(s[2 * st + 1][2] * 16384.f, s[2 * st + 1][3] * 16384.f, hw[3], lw[3]);
-            ph[st] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-            pl[st] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+            for (int f = 0; f < NF; ++f) acc_o[g][f] *= alpha[g];
         }
-#pragma unroll
-        for (int f = 0; f < NF; ++f) acc_o[f] *= alpha;
+        // O^T += V P^T: each V operand read once for both query fragments
 #pragma unroll
         for (int fc = 0; fc < NF; ++fc) {
             const int row = 16 * fc + lq;
@@ -412,9 +442,12 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
             for (int st = 0; st < 2; ++st) {
                 const uint4 ah = Vs[af_vs(row, 0, 4 * st + lg)];
                 const uint4 al = Vs[af_vs(row, 1, 4 * st + lg)];
-                acc_o[fc] = mfma_f16(ah, ph[st], acc_o[fc]);
-                acc_o[fc] = mfma_f16(ah, pl[st], acc_o[fc]);
-                acc_o[fc] = mfma_f16(al, ph[st], acc_o[fc]);
+#pragma unroll
+                for (int g = 0; g < QF; ++g) {
+                    acc_o[g][fc] = mfma_f16(ah, ph[g][st], acc_o[g][fc]);
+                    acc_o[g][fc] = mfma_f16(ah, pl[g][st], acc_o[g][fc]);
+                    acc_o[g][fc] = mfma_f16(al, ph[g][st], acc_o[g][fc]);
+                }
             }
         }
         __syncthreads();
@@ -423,32 +456,35 @@ __global__ __launch_bounds__(256, 2) void attn_f16_kernel(AttnParams p) {
     }
 
     float amx = 0.f;
-    if (qa < T) {
-        const float inv = 1.f / l_run;
-        float* O;
-        int64_t ldo;
-        float* ML = nullptr;
-        if (p.S > 1) {
-            const int64_t bs = (int64_t)b * p.S + split;
-            O = p.ws + (bs * p.H + h) * D * T;
-            ldo = T;
-            ML = p.ws + (int64_t)gridDim.z * p.H * D * T + (bs * p.H + h) * 2 * T;
-        } else {
-            O = p.o + b * p.o_bs + h * p.o_hs;
-            ldo = p.ldc;
-            if (p.ml) ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;
-        }
 #pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float o = acc_o[f][r] * o_un * inv;
-                O[(int64_t)(16 * f + lg * 4 + r) * ldo + qa] = o;
-                amx = fmaxf(amx, fabsf(o));
+    for (int g = 0; g < QF; ++g) {
+        if (qa[g] < T) {
+            const float inv = 1.f / l_run[g];
+            float* O;
+            int64_t ldo;
+            float* ML = nullptr;
+            if (p.S > 1) {
+                const int64_t bs = (int64_t)b * p.S + split;
+                O = p.ws + (bs * p.H + h) * D * T;
+                ldo = T;
+                ML = p.ws + (int64_t)gridDim.z * p.H * D * T + (bs * p.H + h) * 2 * T;
+            } else {
+                O = p.o + b * p.o_bs + h * p.o_hs;
+                ldo = p.ldc;
+                if (p.ml) ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;
             }
-        if (ML && lg == 0) {
-            ML[qa] = m_run;
-            ML[T + qa] = l_run;
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float o = acc_o[g][f][r] * o_un * inv;
+                    O[(int64_t)(16 * f + lg * 4 + r) * ldo + qa[g]] = o;
+                    amx = fmaxf(amx, fabsf(o));
+                }
+            if (ML && lg == 0) {
+                ML[qa[g]] = m_run[g];
+                ML[T + qa[g]] = l_run[g];
+            }
         }
     }
     if (p.amax_out && p.S == 1) amax_publish(p.amax_out + (int64_t)b * RVC_AMAX_SHARDS, amx);
@@ -502,29 +538,45 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnParams p) {
 // out[c][q] += sum_{|j-q|<=W} softmax_p(q, j) * Ev[j-q+W][c]   (synthesizers.py:250, heads_share)
 // p recomputed from scale*Q.K + Rk with the forward's saved (max, sum).  A block owns 32 queries:
 // phase 1 computes the 32 x (2W+1) band probabilities (one dot product per thread-slot) into LDS,
-// phase 2 applies them to Ev for the 32 x D outputs.
+// phase 2 applies them to Ev for the 32 x D outputs.  Round 6: the block's Q columns and the K columns its band
+// touches (32 + 2W) are staged in LDS first by coalesced row loads -- each dot product had walked D strided global
+// loads per operand, one latency each (84 us per TextEncoder layer, 30 s); same products in the same order.
+constexpr int RELV_QB = 32, RELV_KW = RELV_QB + 2 * 15;  // W <= 15 (rvc_attention_ex)
 __global__ __launch_bounds__(256) void attn_relv_band_kernel(AttnParams p, const float* ev, int D) {
-    constexpr int QB = 32;
+    constexpr int QB = RELV_QB;
     __shared__ float pb[QB][32];
     __shared__ float evs[31 * 96];
+    __shared__ float qs[96][QB + 1];
+    __shared__ float ks[96][RELV_KW + 1];
     const int h = blockIdx.y, b = blockIdx.z;
     const int64_t T = p.T;
     const int64_t q0 = (int64_t)blockIdx.x * QB;
     const int tid = threadIdx.x;
-    const int nb = 2 * p.W + 1;
+    const int nb = 2 * p.W + 1, kw = QB + 2 * p.W;
     const float* Q = p.q + b * p.q_bs + h * p.q_hs;
     const float* K = p.k + b * p.k_bs + h * p.k_hs;
     const float* RK = p.rk + ((int64_t)b * p.H + h) * nb * T;
     const float* ML = p.ml + ((int64_t)b * p.H + h) * 2 * T;
     float* O = p.o + b * p.o_bs + h * p.o_hs;
     for (int i = tid; i < nb * D; i += 256) evs[i] = ev[i];
+    for (int i = tid; i < D * QB; i += 256) {  // Q[c][q0 .. q0 + QB): lanes along t
+        const int c = i / QB, qi = i - c * QB;
+        const int64_t qa = q0 + qi;
+        qs[c][qi] = qa < T ? Q[(int64_t)c * p.ldc + qa] : 0.f;
+    }
+    for (int i = tid; i < D * kw; i += 256) {  // K[c][q0 - W .. q0 + QB + W)
+        const int c = i / kw, ji = i - c * kw;
+        const int64_t j = q0 - p.W + ji;
+        ks[c][ji] = (j >= 0 && j < T) ? K[(int64_t)c * p.ldc + j] : 0.f;
+    }
+    __syncthreads();
     for (int i = tid; i < QB * nb; i += 256) {
         const int qi = i % QB, r = i / QB;
         const int64_t qa = q0 + qi, j = qa + r - p.W;
         float pv = 0.f;
         if (qa < T && j >= 0 && j < T) {
             float sc = 0.f;
-            for (int c = 0; c < D; ++c) sc += (Q[(int64_t)c * p.ldc + qa] * p.scale) * K[(int64_t)c * p.ldc + j];
+            for (int c = 0; c < D; ++c) sc += (qs[c][qi] * p.scale) * ks[c][qi + r];
             sc += RK[(int64_t)r * T + qa];
             pv = expf(sc - ML[qa]) / ML[T + qa];
         }
@@ -546,8 +598,9 @@ __global__ __launch_bounds__(256) void attn_relv_band_kernel(AttnParams p, const
 }
 
 // Split-KV plan: enough blocks to cover the chip twice, at least 4 key tiles per split.
-void attn_plan(const rvc_attn_args* a, int& S, int& kps) {
-    const int64_t blocks = (int64_t)cdiv(a->T, 64) * a->H * a->B;
+// qpb: queries per block (64: attn_fwd_kernel; af_qb(D): attn_f16_kernel)
+void attn_plan(const rvc_attn_args* a, int& S, int& kps, int qpb = 64) {
+    const int64_t blocks = (int64_t)cdiv(a->T, qpb) * a->H * a->B;
     int64_t s = (512 + blocks - 1) / blocks;
     const int64_t smax = a->T / 256;
     if (s > smax) s = smax;
@@ -560,8 +613,10 @@ void attn_plan(const rvc_attn_args* a, int& S, int& kps) {
 
 extern "C" int64_t rvc_attention_workspace_bytes(const rvc_attn_args* a) {
     if (!a || a->T <= 0 || a->H <= 0 || a->B <= 0 || (a->D != 64 && a->D != 96)) return -1;
-    int S, kps;
+    int S, kps, S16, kps16;
     attn_plan(a, S, kps);
+    attn_plan(a, S16, kps16, af_qb(a->D));  // the split-fp16 kernel's plan (a call with a |max| cell): the larger
+    S = S16 > S ? S16 : S;
     if (S <= 1) return 0;
     return (int64_t)4 * a->B * S * a->H * a->T * (a->D + 2);
 }
@@ -600,7 +655,7 @@ extern "C" int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in,
     p.amax_in = amax_in;
     static const int f16_env = getenv("RVC_ATTN_F16") ? atoi(getenv("RVC_ATTN_F16")) : 1;
     const bool f16 = amax_in && (g_attn_f16 >= 0 ? g_attn_f16 : f16_env);
-    attn_plan(a, p.S, p.kps);
+    attn_plan(a, p.S, p.kps, f16 ? af_qb(a->D) : 64);
     p.ws = nullptr;
     if (p.S > 1) {
         const int64_t need = (int64_t)4 * a->B * p.S * a->H * a->T * (a->D + 2);
@@ -613,8 +668,9 @@ extern "C" int rvc_attention_ex(const rvc_attn_args* a, const unsigned* amax_in,
     dim3 grid(cdiv(a->T, 64), (unsigned)a->H, (unsigned)(a->B * p.S));
     hipStream_t s = (hipStream_t)stream;
     if (f16) {
-        if (a->D == 64) hipLaunchKernelGGL(attn_f16_kernel<64>, grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL(attn_f16_kernel<96>, grid, dim3(256), 0, s, p);
+        const dim3 g16(cdiv(a->T, af_qb(a->D)), (unsigned)a->H, (unsigned)(a->B * p.S));
+        if (a->D == 64) hipLaunchKernelGGL(attn_f16_kernel<64>, g16, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(attn_f16_kernel<96>, g16, dim3(256), 0, s, p);
     } else if (a->D == 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(attn_fwd_kernel<96>, grid, dim3(256), 0, s, p);
     RVC_HIP(hipGetLastError());

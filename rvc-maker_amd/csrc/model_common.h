@@ -54,7 +54,7 @@ struct rvc_ctx {
     bool amax_ups = true;     // RVC_AMD_AMAX_UPS as synth.py: the upsampling convs' inputs through |max| cells
     bool amax_s2 = true;      // RVC_AMD_AMAX_S2 as ops.py: stride-2 convs with a producer's |max| in split-fp16
     bool fe_amax = true;      // RVC_AMD_FE_AMAX as contentvec.py: the feature extractor's convs through |max| cells
-    bool fused_noise = true;  // RVC_AMD_FUSED_NOISE as synth.py: noise_convs fused into the upsampling convs
+    bool fused_noise = false; // RVC_AMD_FUSED_NOISE as synth.py: noise_convs fused into the upsampling convs (off)
     bool attn_f16 = true;     // RVC_AMD_ATTN_F16 as contentvec.py / synth.py: QKV |max| cells, split-fp16 attention
     bool te_amax = false;     // RVC_AMD_TE_AMAX as synth.py: the TextEncoder's GEMMs through |max| cells (default off)
     bool flow_amax = false;   // RVC_AMD_FLOW_AMAX as synth.py: the flow's (default off)

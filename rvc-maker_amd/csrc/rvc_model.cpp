@@ -466,7 +466,7 @@ extern "C" int rvc_ctx_create(int hip_device, rvc_ctx** out) {
     c->amax_ups = env_on("RVC_AMD_AMAX_UPS");
     c->amax_s2 = env_on("RVC_AMD_AMAX_S2");
     c->fe_amax = env_on("RVC_AMD_FE_AMAX");
-    c->fused_noise = env_on("RVC_AMD_FUSED_NOISE");
+    c->fused_noise = env_set("RVC_AMD_FUSED_NOISE");
     c->attn_f16 = env_on("RVC_AMD_ATTN_F16");
     c->te_amax = env_set("RVC_AMD_TE_AMAX");
     c->flow_amax = env_set("RVC_AMD_FLOW_AMAX");

@@ -16,9 +16,10 @@ def rms(a, b):
     return float(np.sqrt(np.mean((a - b) ** 2)))
 
 
-# the TextEncoder / flow |max| switches (synth.py): the defaults, every cell on, and the f32 attention without cells
+# the TextEncoder / flow |max| switches (synth.py): the defaults, every cell on, the f32 attention without cells, and the
+# noise convs as the upsampling call's source pass (off by default)
 SWITCHES = {"default": {}, "cells_on": dict(TE_AMAX=True, FLOW_AMAX=True, ATTN_F16=True),
-            "cells_off": dict(TE_AMAX=False, FLOW_AMAX=False, ATTN_F16=False)}
+            "cells_off": dict(TE_AMAX=False, FLOW_AMAX=False, ATTN_F16=False), "fused_noise": dict(FUSED_NOISE=True)}
 
 
 @pytest.mark.parametrize("sw", list(SWITCHES))
