@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--clips", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--empty-cache", action="store_true", help="release the caching allocator's blocks after the "
+                    "per-call references")
     a = ap.parse_args()
     from rvc_amd import synthetic
     from rvc_amd.contentvec import ContentVecAMD
@@ -40,6 +42,8 @@ def main():
         vc.seed = 21 + k
         refs.append(vc.pipeline_device(hub, net_g, 0, x, 0, "v2", 0.33).clone())
     torch.cuda.synchronize()
+    if a.empty_cache:
+        torch.cuda.empty_cache()
     vc.seed = 0
     for rep in range(a.reps):
         vc.seed = 21
