@@ -36,10 +36,9 @@ AMAX_UPS = os.environ.get("RVC_AMD_AMAX_UPS", "1") != "0"
 AMAX_PER_STAGE = 16
 # round 6: noise_convs[i](har) as a source pass inside ups[i]'s call (x = ups(x) + noise_convs(har), synthesizers.py:156;
 # rvc_conv1d_args.src_*).  Off by default (RVC_AMD_FUSED_NOISE=1 turns it on; +1.3 % in the clip stream, r6h): with it
-# on, the clip stream's first clip departs from the per-call pipeline by ~2e-3 once the process has run per-call
-# pipelines -- only under the caching allocator (PYTORCH_NO_CUDA_MEMORY_CACHING=1: identical) and not with the pass
-# itself serialised, i.e. a cross-stream use-after-free somewhere in the stream whose allocation pattern the pass
-# exposes (scripts/stream_diff.py, runs r6j-r6p).  Until that is found, the two-launch form.
+# on, the clip stream's first clip -- the one whose synthesizer runs beside the next clip's front end -- intermittently
+# departs from the per-call pipeline by 2e-3 to 9e-3, first at this stage's output (z and g identical;
+# scripts/stream_stage_diff.py).  Until that race is found, the two-launch form.
 FUSED_NOISE = os.environ.get("RVC_AMD_FUSED_NOISE", "0") != "0"
 # round 6: the TextEncoder's rel-pos attention in split-fp16 from the QKV projection's |max| (contentvec.ATTN_F16): the
 # TextEncoder alone, 30 s, 2.89 -> 2.64 ms (scripts/synth_stage_time.py, r6d)
